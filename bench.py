@@ -1,0 +1,214 @@
+"""Benchmark: Mrays/s and ms/frame for the Cornell Box (CornellBox1 scene) at
+512x512, 128 spp, depth 8 (BASELINE.json configs[1]) on N MI355X GPUs.
+
+One step = one full frame: every rank renders its interleaved pixel-row tiles
+with the HIP megakernel (librtmi.so) straight into an HBM buffer, then the
+tiles are gathered to rank 0 with one RCCL gather over xGMI (N > 1). The frame
+work is fixed as N grows (strong scaling).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+N > 1 is launched by torch.distributed.run (one process per GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "Mrays/sec + ms/frame, Cornell Box 512×512 spp=128, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+# Algorithmic bytes per record touched: plane 40 B, sphere
+# 20 B, moving sphere 36 B, mesh AABB 24 B, triangle (v0,E1,E2) 36 B, BVH node
+# 32 B, and 12 B per output pixel.
+BYTES = {"plane": 40, "sphere": 20, "moving_sphere": 36, "box": 24, "tri": 36, "node": 32, "pixel": 12}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--width", type=int, default=512)
+    ap.add_argument("--height", type=int, default=512)
+    ap.add_argument("--spp", type=int, default=128)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--row-block", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-spp", type=int, default=32)
+    return ap.parse_args()
+
+
+def object_bytes_per_segment(r) -> int:
+    """Bytes of the non-mesh object records every segment scans."""
+    import raytracingthenextweekcuda_amd.scene  # noqa: F401
+
+    counts = r.object_counts()
+    return counts["plane"] * BYTES["plane"] + counts["sphere"] * BYTES["sphere"] + \
+        counts["moving_sphere"] * BYTES["moving_sphere"]
+
+
+def cpu_baseline(args, threads: int):
+    """The CPU restatement (oracle/, a port of the reference's integrator) on a
+    bounded sample of the same workload: full frame at --cpu-spp spp."""
+    from oracle import oracle as orc
+
+    sc = orc.yaml_scene(os.path.join(REPO, "assets", "scenes", "cornellbox1.yaml"),
+                        os.path.join(REPO, "assets", "models"), args.width, args.height)
+    sc.render(64, 64, 1, args.depth, threads=threads)  # warm-up
+    t0 = time.perf_counter()
+    _, st = sc.render(args.width, args.height, args.cpu_spp, args.depth, threads=threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": st["segments"] / dt / 1e6,
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"CornellBox1 {args.width}x{args.height} spp={args.cpu_spp} depth={args.depth} "
+                   f"(spp/{args.spp // max(args.cpu_spp, 1)} of the GPU frame), {dt:.2f} s wall, "
+                   f"{st['segments']} segments; ms/frame scaled to spp={args.spp}: "
+                   f"{dt * 1e3 * args.spp / args.cpu_spp:.0f}"),
+    }
+
+
+def load_pmc_traffic(workload: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        d = json.load(fh)
+    ent = d.get(workload)
+    return None if ent is None else float(ent["hbm_bytes_per_launch"])
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import raytracingthenextweekcuda_amd as rtmi
+
+    W, H = args.width, args.height
+    r = rtmi.Renderer(device=local)
+    rtmi.cornell_box1(r, W, H)
+    block = args.row_block
+    rows = rtmi.owned_rows(H, block, rank, world)
+    max_rows = max(rtmi.owned_rows(H, block, k, world) for k in range(world))
+    out = torch.zeros((max_rows, W, 3), dtype=torch.float32, device="cuda")
+    gather = [torch.empty_like(out) for _ in range(world)] if (rank == 0 and world > 1) else None
+    params = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, world)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        r.render_device(params, out.data_ptr(), stream.cuda_stream)
+        if world > 1:
+            dist.gather(out, gather, dst=0)
+        return r.stats()  # waits for the kernel's end event, reads counters
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kern_ms, segs, tri_tests, box_tests = [], 0, 0, 0
+    for _ in range(args.steps):
+        st = step()
+        kern_ms.append(st["kernel_ms"])
+        segs += st["segments"]
+        tri_tests += st["tri_tests"]
+        box_tests += st["box_tests"]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+
+    # max time over ranks, totals over ranks
+    agg = torch.tensor([dt, float(segs), float(tri_tests), float(box_tests), float(np.mean(kern_ms)),
+                        float(rows)], dtype=torch.float64, device="cuda")
+    if world > 1:
+        tmax = agg[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tot = agg[1:].clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dt = float(tmax.item())
+        segs, tri_tests, box_tests = (float(x) for x in tot[:3].tolist())
+        kmean_sum, rows_tot = float(tot[3].item()), float(tot[4].item())
+        kmean = kmean_sum / world
+    else:
+        kmean, rows_tot = float(np.mean(kern_ms)), float(rows)
+
+    if rank == 0:
+        K = args.steps
+        ms_frame = dt * 1e3 / K
+        mrays = segs / dt / 1e6
+        # Roofline of the megakernel: algorithmic record bytes per launch
+        # (rank 0's launch stands for the per-GPU launch).
+        seg_launch = segs / K / world
+        alg_bytes = (seg_launch * object_bytes_per_segment(r) + tri_tests / K / world * BYTES["tri"]
+                     + box_tests / K / world * BYTES["box"] + rows_tot / world * W * BYTES["pixel"])
+        achieved = alg_bytes / (kmean * 1e-3) / 1e9
+        workload = f"cornellbox1_{W}x{H}_spp{args.spp}_d{args.depth}_n{world}"
+        traffic = load_pmc_traffic(workload)
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            threads = min(16, os.cpu_count() or 1)
+            cpu = cpu_baseline(args, threads)
+        line = {
+            "metric": METRIC,
+            "value": round(mrays, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_frame, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (deterministic CornellBox1 scene from the reference's cornellbox1.yaml; "
+                    "Philox RNG seed 1984)",
+            "config": {
+                "workload": workload,
+                "scene": "CornellBox1 (6 planes + 2 cube_small.obj meshes, 24 triangles)",
+                "width": W, "height": H, "spp": args.spp, "depth": args.depth,
+                "row_block": block, "parallelism": f"row-tiles x{world} + RCCL gather" if world > 1 else "single GPU",
+                "segments_per_frame": int(segs / K),
+                "msamples_per_s": round(W * H * args.spp / (dt / K) / 1e6, 3),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel_ms": round(kmean, 4),
+                "algorithmic_bytes_per_launch": int(alg_bytes),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    r.close()
+
+
+if __name__ == "__main__":
+    main()

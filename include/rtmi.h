@@ -1,0 +1,147 @@
+/*
+ * rtmi.h — C ABI of the MI355X-native path tracer (librtmi.so).
+ *
+ * This is the drop-in boundary for the reference's per-pixel path-tracing
+ * hot path (erosnick/RayTracingTheNextWeekCUDA). Every entry point below names
+ * the reference interface it replaces (paths relative to
+ * RayTracingTheNextWeekCUDA/). Plain C types only: no HIP, no torch types.
+ *
+ * Ownership: the library owns every device buffer; the caller owns its host
+ * input arrays (copied during the call) and its output buffers.
+ * Errors: every export returns rt_status (0 = RT_OK). The message for the last
+ * failure on a context is rt_last_error(ctx). The library never calls exit()
+ * (replaces gpuErrorCheck -> cudaDeviceReset -> exit, Utils.h:125-133).
+ * Threading: one rt_ctx per HIP device; calls on one ctx are not thread-safe.
+ */
+#ifndef RTMI_H_
+#define RTMI_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTMI_ABI_VERSION 1
+
+typedef int32_t rt_status;
+enum {
+    RT_OK = 0,
+    RT_ERR_INVALID = 1,  /* bad argument / index / shape */
+    RT_ERR_HIP = 2,      /* HIP runtime failure */
+    RT_ERR_IO = 3,       /* file could not be read / parsed */
+    RT_ERR_STATE = 4,    /* call out of order (e.g. render before commit) */
+    RT_ERR_OOM = 5,      /* allocation failure */
+    RT_ERR_NODEV = 6,    /* no GPU / context created without a device */
+    RT_ERR_OVERFLOW = 7  /* BVH traversal stack overflow flagged by the kernel */
+};
+
+/* Material kinds (Material.h:8-13 MaterialType). */
+enum { RT_LAMBERTIAN = 0, RT_METAL = 1, RT_DIELECTRIC = 2, RT_EMISSION = 3 };
+/* Plane orientation (Plane.h:5-9 PlaneOrientation). */
+enum { RT_PLANE_XY = 0, RT_PLANE_YZ = 1, RT_PLANE_XZ = 2 };
+
+typedef struct rt_ctx rt_ctx;
+
+/* Render parameters. Replaces the compile-time knobs of renderKernel
+ * (main.cu:160-206: samplesPerPixel 165-169, BOUNCES 23, curand_init seed 1984
+ * at 127) and adds row tiling for multi-GPU sharding.
+ * Rows are numbered with y = 0 at the BOTTOM (reference convention,
+ * main.cu:183). Row tiling: global row y belongs to this call iff
+ * (y / row_block) % row_world == row_rank. Output holds only the owned rows,
+ * in increasing y, each width*3 floats. row_world = 1 renders the full frame. */
+typedef struct rt_render_params {
+    int32_t width;
+    int32_t height;
+    int32_t spp;            /* samples per pixel (reference: 32 offline, 1 realtime) */
+    int32_t max_depth;      /* reference BOUNCES (main.cu:23) */
+    uint32_t seed;          /* reference 1984 (main.cu:127) */
+    uint32_t sample_offset; /* first global sample index (progressive accumulation) */
+    int32_t row_block;      /* rows per tile block (>= 1) */
+    int32_t row_rank;       /* this shard's rank */
+    int32_t row_world;      /* number of shards (>= 1) */
+} rt_render_params;
+
+typedef struct rt_render_stats {
+    uint64_t segments;      /* closest-hit queries traced (camera ray = 1, +1 per scatter) */
+    uint64_t samples;       /* camera samples = owned pixels * spp */
+    uint64_t node_visits;   /* BVH node visits (0 for linear-scan scenes) */
+    uint64_t tri_tests;     /* triangle records tested */
+    uint64_t box_tests;     /* mesh bounding boxes tested */
+    double kernel_ms;       /* duration of the render kernel (hipEvent) */
+    uint32_t overflow;      /* 1 if any lane overflowed the traversal stack */
+} rt_render_stats;
+
+/* ---- context (replaces initialize()/cleanup(), main.cu:555-936) ---- */
+int32_t rt_abi_version(void);
+/* device >= 0: HIP ordinal. device = -1: scene-building only (no GPU calls). */
+rt_status rt_create(int32_t device, rt_ctx** out);
+void rt_destroy(rt_ctx* ctx);
+const char* rt_last_error(const rt_ctx* ctx);
+/* Drops every material, object and the camera (scene reset). */
+rt_status rt_clear_scene(rt_ctx* ctx);
+
+/* ---- materials (kernels.h:50-84 create*Material) ---- */
+rt_status rt_material_lambertian(rt_ctx* ctx, int32_t index, const float albedo[3], float absorb);
+rt_status rt_material_metal(rt_ctx* ctx, int32_t index, const float albedo[3], float fuzz);
+rt_status rt_material_dielectric(rt_ctx* ctx, int32_t index, float index_of_refraction);
+rt_status rt_material_emission(rt_ctx* ctx, int32_t index, const float albedo[3], float intensity);
+/* 1 if material slot `index` has been created (the `materials[id] == nullptr`
+ * guards of main.cu:714,723,733,743), else 0. */
+int32_t rt_material_defined(const rt_ctx* ctx, int32_t index);
+
+/* ---- hitables (kernels.h:99-154 create*; object slot = closest-hit scan
+ *      order of hit(), main.cu:43-57) ---- */
+rt_status rt_sphere(rt_ctx* ctx, int32_t index, const float center[3], float radius,
+                    int32_t material, int32_t shading);
+rt_status rt_moving_sphere(rt_ctx* ctx, int32_t index, const float center0[3],
+                           const float center1[3], float time0, float time1, float radius,
+                           int32_t material);
+rt_status rt_plane(rt_ctx* ctx, int32_t index, const float position[3], const float normal[3],
+                   const float extend[3], int32_t material, int32_t orientation,
+                   int32_t two_side);
+rt_status rt_cube(rt_ctx* ctx, int32_t index, const float center[3], const float extend[3],
+                  int32_t material);
+/* Triangle mesh from world-space vertices, 9 floats per triangle
+ * (createTriangleMeshData + createMesh, main.cu:384-401, kernels.h:126-133). */
+rt_status rt_mesh(rt_ctx* ctx, int32_t index, const float* tri_vertices, int32_t n_tris,
+                  int32_t material);
+/* OBJ mesh with the loadModel(file, scale, rotate, offset) transform
+ * (ModelLoader.cpp:418-448; tinyobjloader quad split, tiny_obj_loader.h:1397-1495). */
+rt_status rt_mesh_obj(rt_ctx* ctx, int32_t index, const char* path, const float scale[3],
+                      const float rotate[3], const float offset[3], int32_t material);
+/* Number of triangles of the mesh in slot `index` (0 if not a mesh). */
+int32_t rt_mesh_triangle_count(const rt_ctx* ctx, int32_t index);
+/* Copies the world-space vertices (9 floats/tri) of mesh slot `index`. */
+rt_status rt_mesh_vertices(const rt_ctx* ctx, int32_t index, float* out, int32_t max_tris);
+
+/* ---- camera (Camera.h:19-34 initialize, 86-103 updateViewMatrix) ---- */
+rt_status rt_camera(rt_ctx* ctx, const float eye[3], const float center[3], const float up[3],
+                    float aspect_ratio, float fov, float aperture, float focus_distance,
+                    float time0, float time1);
+
+/* Builds the device scene tables and uploads them (replaces the device-side
+ * `new` factories + cudaMemcpyToSymbol, main.cu:850-851). */
+rt_status rt_commit(rt_ctx* ctx);
+/* Committed scene census: out[0] planes (cube faces included), [1] spheres,
+ * [2] moving spheres, [3] meshes, [4] triangles, [5] material slots,
+ * [6] BVH nodes, [7] reserved. */
+rt_status rt_scene_info(const rt_ctx* ctx, int32_t out[8]);
+
+/* ---- render (renderKernel, main.cu:160-206, launched by pathTracing 875-898) ----
+ * Output: float32 RGB mean radiance (color / spp, BEFORE Canvas::gamma). */
+rt_status rt_render(rt_ctx* ctx, const rt_render_params* params, float* out_rgb_host);
+/* Same, into a caller-owned device buffer, enqueued on `hip_stream`
+ * (hipStream_t, NULL = default). Asynchronous: stats are valid after the
+ * stream has completed and rt_sync_stats() has been called. */
+rt_status rt_render_device(rt_ctx* ctx, const rt_render_params* params, float* out_rgb_device,
+                           void* hip_stream);
+rt_status rt_sync_stats(rt_ctx* ctx, rt_render_stats* out);
+
+/* Canvas::gamma (Canvas.h:198-200): u8 = uint(255.99 * clamp(sqrt(c), 0, 0.999)). */
+rt_status rt_gamma_u8(const float* rgb, int64_t n, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTMI_H_ */

@@ -1,0 +1,842 @@
+/*
+ * rt_oracle.c — CPU restatement of the reference path tracer's hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY. This file is the parity checker (and the
+ * `cpu_baseline` of bench.py). It is never linked into, loaded by or called
+ * from the product library (raytracingthenextweekcuda_amd/librtmi.so). Only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it.
+ *
+ * It restates, in plain C with the reference's object structure and evaluation
+ * order, the reference's `rayColor` integrator path (paths relative to
+ * /root/reference/RayTracingTheNextWeekCUDA/):
+ *   renderKernel sample loop ........ main.cu:160-206
+ *   rayColor ........................ main.cu:63-94
+ *   hit (closest over objects) ...... main.cu:43-57
+ *   Camera initialize/update/getRay . Camera.h:19-34, 86-103, 151-168
+ *   Ray ctor (inverse dir, signs) ... Ray.h:10-16
+ *   HitResult::setFaceNormal ........ HitResult.h:15-18
+ *   Sphere / MovingSphere ........... Sphere.cu:3-78
+ *   Plane ........................... Plane.cu:4-52
+ *   Cube (6 two-sided planes) ....... Cube.cu:10-23, kernels.h:139-154
+ *   TriangleMesh + AABBox ........... TriangleMesh.cu:34-117, AABBox.h:14-111
+ *   mesh data prep / mesh AABB ...... main.cu:261-281, 318-350
+ *   Lambertian/Metal/Dieletric/Emission Material.cu:3-19, Material.h:45-123
+ *   random helpers .................. Utils.h:44-121
+ *   OBJ load + transform ............ ModelLoader.cpp:418-448 with the
+ *                                     tinyobjloader v2.0 parser/quad split
+ *                                     (tinyobjloader/tiny_obj_loader.h:837-975,
+ *                                     1397-1495)
+ *   Canvas::gamma ................... Canvas.h:198-200
+ *
+ * Deliberate, documented deviations from the reference:
+ *  1. cuRAND XORWOW is replaced by Philox4x32-10 (key = (seed, pixel),
+ *     counter = (draw/4, sample, 0, 0)), mapped to (0,1] with curand's
+ *     x*2^-32 + 2^-33. cuRAND itself is not in this image: parity with the
+ *     reference's random stream is "unpinned" by construction.
+ *  2. randomInUnitDisk draws x before y (the reference's order is unspecified).
+ *  3. pow(x, 5) in Schlick's approximation is ((x*x)*(x*x))*x (the reference
+ *     used --use_fast_math __powf, which is not reproducible).
+ *  4. MovingSphere::hit sets its material (the reference leaves it stale, a bug,
+ *     Sphere.cu:70).
+ *  5. abs() in Plane::hit is the float abs (CUDA device semantics).
+ * Compile with -ffp-contract=off and without fast-math.
+ *
+ * Pinning: the reference ships no golden radiance, RNG or timing data for this
+ * path. The reference cannot be built here without writing
+ * stand-ins for CUDA headers, which this project does not do. The oracle is
+ * therefore pinned by (a) the reference's own data files (cube_small.obj
+ * triangulation and the scene YAMLs), (b) Random123 Philox4x32-10 known-answer
+ * vectors, and (c) hand-derived known answers for each hit/scatter function
+ * (tests/test_oracle.py). Parity of the integrator's full radiance with the
+ * reference's own binary is "parity partially pinned" (see DESIGN.md §2).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORC_FLT_EPSILON 1.19209290e-07f
+#define ORC_EPS 0.001f /* Math::epsilon, Constants.h:23 */
+
+/* ---------------- Vector3Df (LinearAlgebra.h) ---------------- */
+typedef struct { float x, y, z; } V3;
+
+static inline V3 v3(float x, float y, float z) { V3 r = {x, y, z}; return r; }
+static inline V3 vadd(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline V3 vsub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline V3 vmulv(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline V3 vmul(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }   /* v*s and s*v */
+static inline V3 vdiv(V3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
+static inline V3 vneg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+static inline V3 vaddf(V3 b, float a) { return v3(b.x + a, b.y + a, b.z + a); } /* a + b */
+static inline float vdot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline float vlensq(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+static inline float vlen(V3 a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }
+static inline V3 vcross(V3 a, V3 b) {
+    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+static inline V3 vnorm(V3 v) {
+    float n = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
+    return v3(v.x / n, v.y / n, v.z / n);
+}
+static inline V3 vrecip(V3 b) { return v3(1.0f / b.x, 1.0f / b.y, 1.0f / b.z); } /* float / Vector3Df */
+static inline float radians_f(float deg) { return 3.1415926535897932f / 180.0f * deg; }
+
+/* ---------------- RNG: Philox4x32-10 ---------------- */
+static void philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* Stand-in for curandState: a (seed, pixel, sample) stream. */
+typedef struct {
+    uint32_t key[2];
+    uint32_t sample;
+    uint32_t n;
+    uint32_t block[4];
+} RandState;
+
+static void rand_init(RandState* s, uint32_t seed, uint32_t pixel, uint32_t sample) {
+    s->key[0] = seed; s->key[1] = pixel; s->sample = sample; s->n = 0;
+}
+
+/* curand_uniform: (0, 1] (curand's _curand_uniform mapping). */
+static float curand_uniform_(RandState* s) {
+    if ((s->n & 3u) == 0u) {
+        uint32_t ctr[4] = {s->n >> 2, s->sample, 0u, 0u};
+        philox(ctr, s->key, s->block);
+    }
+    uint32_t x = s->block[s->n & 3u];
+    s->n++;
+    const float inv = 2.3283064e-10f;
+    return (float)x * inv + (inv / 2.0f);
+}
+
+/* Utils.h:44-121 */
+static float u_random(RandState* s) { return curand_uniform_(s); }
+static float u_random_range(RandState* s, float mn, float mx) { return mn + (mx - mn) * u_random(s); }
+static V3 u_random_vector(RandState* s) {
+    float x = curand_uniform_(s);
+    float y = curand_uniform_(s);
+    float z = curand_uniform_(s);
+    return v3(x, y, z);
+}
+static V3 u_random_vector_range(RandState* s, float mn, float mx) {
+    return vaddf(vmul(u_random_vector(s), mx - mn), mn);
+}
+static V3 u_random_in_unit_sphere(RandState* s) {
+    for (;;) {
+        V3 p = u_random_vector_range(s, -1.0f, 1.0f);
+        if (vlensq(p) >= 1.0f) continue;
+        return p;
+    }
+}
+static V3 u_random_unit_vector(RandState* s) { return vnorm(u_random_in_unit_sphere(s)); }
+static V3 u_random_in_unit_disk(RandState* s) {
+    for (;;) {
+        float x = u_random_range(s, -1.0f, 1.0f); /* pinned: x first */
+        float y = u_random_range(s, -1.0f, 1.0f);
+        V3 p = v3(x, y, 0.0f);
+        if (vlensq(p) >= 1.0f) continue;
+        return p;
+    }
+}
+static int u_near_zero(V3 v) {
+    const float s = 1e-8f;
+    return (fabsf(v.x) < s) && (fabsf(v.y) < s) && (fabsf(v.z) < s);
+}
+static V3 u_reflect(V3 v, V3 n) { return vsub(v, vmul(n, 2.0f * vdot(v, n))); }
+static V3 u_refract(V3 uv, V3 n, float eta) {
+    float cos_theta = fminf(vdot(vneg(uv), n), 1.0f);
+    V3 perp = vmul(vadd(uv, vmul(n, cos_theta)), eta);
+    V3 par = vmul(n, -sqrtf(fabsf(1.0f - vlensq(perp))));
+    return vadd(perp, par);
+}
+
+/* ---------------- Ray / HitResult ---------------- */
+typedef struct {
+    V3 origin, direction, inverse_direction;
+    int32_t signs[3];
+    float time;
+} Ray;
+
+static Ray make_ray(V3 o, V3 d, float time) {
+    Ray r;
+    r.origin = o;
+    r.direction = d;
+    r.time = time;
+    r.inverse_direction = vrecip(d);
+    r.signs[0] = r.inverse_direction.x < 0.0f;
+    r.signs[1] = r.inverse_direction.y < 0.0f;
+    r.signs[2] = r.inverse_direction.z < 0.0f;
+    return r;
+}
+static V3 ray_at(const Ray* r, float t) { return vadd(r->origin, vmul(r->direction, t)); }
+
+typedef struct {
+    float t;
+    V3 normal;
+    int front_face;
+    int material;
+} HitResult;
+
+static void set_face_normal(HitResult* h, const Ray* r, V3 outward) {
+    h->front_face = vdot(r->direction, outward) < ORC_FLT_EPSILON;
+    h->normal = h->front_face ? outward : vneg(outward);
+}
+
+/* ---------------- Scene objects ---------------- */
+enum { O_SPHERE = 0, O_MOVING = 1, O_PLANE = 2, O_MESH = 3, O_CUBE = 4 };
+
+typedef struct {
+    int defined;
+    int type;      /* MaterialType (Material.h:8-13) */
+    V3 albedo;
+    float param;   /* absorb | fuzz | ior | intensity */
+} Material;
+
+typedef struct {
+    V3 position, normal, extend;
+    int orientation, two_side, material;
+} Plane;
+
+typedef struct Object {
+    int defined, type, material;
+    V3 center, center1;
+    float radius, time0, time1;
+    Plane plane;
+    Plane faces[6];
+    /* mesh */
+    int tri_count;
+    float* tri_data;   /* 12 floats per tri: (v0, n.x), (E1, n.y), (E2, n.z) as main.cu:341-343 */
+    V3 bounds[2];
+} Object;
+
+typedef struct {
+    Material* mats;
+    int n_mats;
+    Object* objs;
+    int n_objs;
+    /* camera (Camera.h fields) */
+    int has_camera;
+    V3 origin, lower_left, horizontal, vertical, right, true_up;
+    float lens_radius, time0, time1;
+} Scene;
+
+/* Sphere::hit (Sphere.cu:3-37) / MovingSphere::hit (39-73). */
+static V3 moving_center(const Object* o, float time) {
+    return vadd(o->center, vmul(vsub(o->center1, o->center), (time - o->time0) / (o->time1 - o->time0)));
+}
+static int sphere_hit(const Object* o, V3 center, const Ray* ray, float tmin, float tmax, HitResult* hr) {
+    V3 oc = vsub(ray->origin, center);
+    float a = vdot(ray->direction, ray->direction);
+    float half_b = vdot(oc, ray->direction);
+    float c = vdot(oc, oc) - o->radius * o->radius;
+    float disc = half_b * half_b - a * c;
+    if (!(disc > ORC_FLT_EPSILON)) return 0;
+    float inva = 1.0f / a;
+    float sq = sqrtf(disc);
+    float root = (-half_b - sq) * inva;
+    if (root < tmin || tmax < root) {
+        root = (-half_b + sq) * inva;
+        if (root < tmin || tmax < root) return 0;
+    }
+    hr->t = root;
+    V3 p = ray_at(ray, hr->t);
+    V3 outward = vdiv(vsub(p, center), o->radius);
+    set_face_normal(hr, ray, outward);
+    hr->material = o->material;
+    return 1;
+}
+
+/* Plane::hit (Plane.cu:4-52). */
+static int plane_hit(const Plane* pl, const Ray* ray, float tmin, float tmax, HitResult* hr) {
+    float den = vdot(pl->normal, ray->direction);
+    int proceed = pl->two_side ? (fabsf(den) > ORC_EPS) : (den > ORC_EPS);
+    if (!proceed) return 0;
+    V3 po = vsub(pl->position, ray->origin);
+    hr->t = vdot(po, pl->normal) / den;
+    V3 p = ray_at(ray, hr->t);
+    set_face_normal(hr, ray, pl->normal);
+    hr->material = pl->material;
+    int in_range = 0;
+    V3 lb = vsub(pl->position, pl->extend), rb = vadd(pl->position, pl->extend);
+    switch (pl->orientation) {
+    case 0:
+        in_range = (p.x > lb.x) && (p.x < rb.x) && (p.y > lb.y) && (p.y < rb.y);
+        break;
+    case 1:
+        in_range = (p.y > pl->position.y - pl->extend.y) && (p.y < pl->position.y + pl->extend.y) &&
+                   (p.z > pl->position.z - pl->extend.z) && (p.z < pl->position.z + pl->extend.z);
+        break;
+    case 2:
+        in_range = (p.x > lb.x) && (p.x < rb.x) && (p.z > lb.z) && (p.z < rb.z);
+        break;
+    }
+    return ((hr->t >= tmin) && (hr->t < tmax)) && in_range;
+}
+
+/* AABBox::intersect (AABBox.h:14-111). */
+static int aabb_intersect(const V3 b[2], const Ray* r) {
+    float tminx = (b[r->signs[0]].x - r->origin.x) * r->inverse_direction.x;
+    float tmaxx = (b[1 - r->signs[0]].x - r->origin.x) * r->inverse_direction.x;
+    float tminy = (b[r->signs[1]].y - r->origin.y) * r->inverse_direction.y;
+    float tmaxy = (b[1 - r->signs[1]].y - r->origin.y) * r->inverse_direction.y;
+    if ((tminx > tmaxy) || (tminy > tmaxx)) return 0;
+    if (tminy > tminx) tminx = tminy;
+    if (tmaxy < tmaxx) tmaxx = tmaxy;
+    float tminz = (b[r->signs[2]].z - r->origin.z) * r->inverse_direction.z;
+    float tmaxz = (b[1 - r->signs[2]].z - r->origin.z) * r->inverse_direction.z;
+    if ((tminx > tmaxz) || (tminz > tmaxx)) return 0;
+    if (tminz > tminx) tminx = tminz;
+    if (tmaxz < tmaxx) tmaxx = tmaxz;
+    float t = tminx;
+    if (t < 0.0f) {
+        t = tmaxx;
+        if (t < 0.0f) return 0;
+    }
+    return 1;
+}
+
+/* TriangleMesh::hit (TriangleMesh.cu:34-117). */
+static int mesh_hit(const Object* o, const Ray* ray, float tmin, float tmax, HitResult* hr,
+                    uint64_t* tri_tests) {
+    if (!aabb_intersect(o->bounds, ray)) return 0;
+    int any = 0;
+    float closest = tmax;
+    *tri_tests += (uint64_t)o->tri_count;
+    for (int i = 0; i < o->tri_count; ++i) {
+        const float* e = o->tri_data + 12 * i;
+        V3 v0 = v3(e[0], e[1], e[2]);
+        V3 E1 = v3(e[4], e[5], e[6]);
+        V3 E2 = v3(e[8], e[9], e[10]);
+        V3 normal = vnorm(vcross(E1, E2));
+        if (vdot(ray->direction, normal) > ORC_FLT_EPSILON) continue;
+        V3 S = vsub(ray->origin, v0);
+        V3 S1 = vcross(ray->direction, E2);
+        V3 S2 = vcross(S, E1);
+        float coef = 1.0f / vdot(S1, E1);
+        float t = coef * vdot(S2, E2);
+        float b1 = coef * vdot(S1, S);
+        float b2 = coef * vdot(S2, ray->direction);
+        if (((t >= ORC_FLT_EPSILON) && ((t >= tmin) && (t < closest))) && (b1 >= ORC_FLT_EPSILON) &&
+            (b2 >= ORC_FLT_EPSILON) && ((1.0f - b1 - b2) >= ORC_FLT_EPSILON)) {
+            hr->t = t;
+            set_face_normal(hr, ray, normal);
+            hr->material = o->material;
+            any = 1;
+            closest = t;
+        }
+    }
+    return any;
+}
+
+static int object_hit(const Object* o, const Ray* ray, float tmin, float tmax, HitResult* hr,
+                      uint64_t* tri_tests) {
+    switch (o->type) {
+    case O_SPHERE: return sphere_hit(o, o->center, ray, tmin, tmax, hr);
+    case O_MOVING: return sphere_hit(o, moving_center(o, ray->time), ray, tmin, tmax, hr);
+    case O_PLANE: return plane_hit(&o->plane, ray, tmin, tmax, hr);
+    case O_MESH: return mesh_hit(o, ray, tmin, tmax, hr, tri_tests);
+    case O_CUBE: { /* Cube::hit (Cube.cu:10-23) */
+        HitResult tmp;
+        int any = 0;
+        float closest = tmax;
+        for (int f = 0; f < 6; ++f) {
+            if (plane_hit(&o->faces[f], ray, tmin, closest, &tmp)) {
+                any = 1;
+                closest = tmp.t;
+                *hr = tmp;
+            }
+        }
+        return any;
+    }
+    }
+    return 0;
+}
+
+/* hit (main.cu:43-57) */
+static int scene_hit(const Scene* s, const Ray* ray, float tmin, float tmax, HitResult* out,
+                     uint64_t* tri_tests) {
+    HitResult tmp;
+    memset(&tmp, 0, sizeof(tmp));
+    int any = 0;
+    float closest = tmax;
+    for (int i = 0; i < s->n_objs; ++i) {
+        const Object* o = &s->objs[i];
+        if (o->defined && object_hit(o, ray, tmin, closest, &tmp, tri_tests)) {
+            any = 1;
+            closest = tmp.t;
+            *out = tmp;
+        }
+    }
+    return any;
+}
+
+/* Material::scatter family. Returns 1 if scattered. */
+static int scatter(const Material* m, const Ray* in, const HitResult* h, V3* att, Ray* sc, RandState* rs) {
+    switch (m->type) {
+    case 0: { /* Lambertian (Material.cu:3-19) */
+        V3 dir = vadd(h->normal, u_random_unit_vector(rs));
+        if (u_near_zero(dir)) dir = h->normal;
+        *sc = make_ray(ray_at(in, h->t), vnorm(dir), in->time);
+        *att = m->albedo;
+        return 1;
+    }
+    case 1: { /* Metal (Material.h:45-51) */
+        float fuzz = m->param < 1.0f ? m->param : 1.0f;
+        V3 refl = u_reflect(vnorm(in->direction), h->normal);
+        *sc = make_ray(ray_at(in, h->t), vadd(refl, vmul(u_random_in_unit_sphere(rs), fuzz)), in->time);
+        int ok = vdot(sc->direction, h->normal) > 0;
+        *att = vmul(m->albedo, (float)ok);
+        return ok;
+    }
+    case 2: { /* Dieletric (Material.h:65-109) */
+        *att = v3(1.0f, 1.0f, 1.0f);
+        float ratio = h->front_face ? (1.0f / m->param) : m->param;
+        V3 ud = vnorm(in->direction);
+        float cos_t = fminf(vdot(vneg(ud), h->normal), 1.0f);
+        float sin_t = sqrtf(1.0f - cos_t * cos_t);
+        int cannot = ratio * sin_t > 1.0f;
+        V3 dir;
+        int refl = cannot;
+        if (!refl) {
+            float r0 = (1.0f - ratio) / (1.0f + ratio);
+            r0 = r0 * r0;
+            float x = 1.0f - cos_t;
+            float x2 = x * x;
+            float R = r0 + (1.0f - r0) * ((x2 * x2) * x);
+            refl = R > u_random(rs);
+        }
+        if (refl) dir = u_reflect(ud, h->normal);
+        else dir = u_refract(ud, h->normal, ratio);
+        *sc = make_ray(ray_at(in, h->t), vnorm(dir), in->time);
+        return 1;
+    }
+    default: /* Emission (Material.h:120-123) */
+        *att = vmul(m->albedo, m->param);
+        return 0;
+    }
+}
+
+/* rayColor (main.cu:63-94) */
+static V3 ray_color(const Scene* s, Ray ray, int bounces, RandState* rs, uint64_t* segs, uint64_t* tri_tests) {
+    V3 cur = v3(1.0f, 1.0f, 1.0f);
+    for (int i = 0; i < bounces; ++i) {
+        HitResult h;
+        memset(&h, 0, sizeof(h));
+        h.t = -INFINITY;
+        h.front_face = 1;
+        ++*segs;
+        if (scene_hit(s, &ray, ORC_EPS, INFINITY, &h, tri_tests)) {
+            V3 att;
+            Ray sc;
+            if (scatter(&s->mats[h.material], &ray, &h, &att, &sc, rs)) {
+                cur = vmulv(cur, att);
+                ray = sc;
+            } else {
+                return vmulv(cur, att);
+            }
+        } else {
+            V3 ud = vnorm(ray.direction);
+            float t = 0.5f * (ud.y + 1.0f);
+            V3 bg = vadd(vmul(v3(1.0f, 1.0f, 1.0f), 1.0f - t), vmul(v3(0.5f, 0.7f, 1.0f), t));
+            return vmulv(cur, bg);
+        }
+    }
+    return v3(0.0f, 0.0f, 0.0f);
+}
+
+/* Camera::getRay (Camera.h:151-168) */
+static Ray camera_get_ray(const Scene* s, float dx, float dy, RandState* rs) {
+    V3 rnd = vmul(u_random_in_unit_disk(rs), s->lens_radius);
+    V3 offset = vadd(vmul(s->right, rnd.x), vmul(s->true_up, rnd.y));
+    V3 new_origin = vadd(s->origin, offset);
+    V3 dir = vsub(vadd(vadd(s->lower_left, vmul(s->horizontal, dx)), vmul(s->vertical, dy)), new_origin);
+    dir = vnorm(dir);
+    return make_ray(vadd(s->origin, offset), dir, u_random_range(rs, s->time0, s->time1));
+}
+
+/* ====================== exported API (ctypes) ====================== */
+
+Scene* orc_scene_new(void) { return (Scene*)calloc(1, sizeof(Scene)); }
+
+void orc_scene_free(Scene* s) {
+    if (!s) return;
+    for (int i = 0; i < s->n_objs; ++i) free(s->objs[i].tri_data);
+    free(s->objs);
+    free(s->mats);
+    free(s);
+}
+
+static Material* mat_at(Scene* s, int idx) {
+    if (idx < 0) return NULL;
+    if (idx >= s->n_mats) {
+        s->mats = (Material*)realloc(s->mats, (size_t)(idx + 1) * sizeof(Material));
+        memset(s->mats + s->n_mats, 0, (size_t)(idx + 1 - s->n_mats) * sizeof(Material));
+        s->n_mats = idx + 1;
+    }
+    return &s->mats[idx];
+}
+
+static Object* obj_at(Scene* s, int idx) {
+    if (idx < 0) return NULL;
+    if (idx >= s->n_objs) {
+        s->objs = (Object*)realloc(s->objs, (size_t)(idx + 1) * sizeof(Object));
+        memset(s->objs + s->n_objs, 0, (size_t)(idx + 1 - s->n_objs) * sizeof(Object));
+        s->n_objs = idx + 1;
+    }
+    free(s->objs[idx].tri_data);
+    memset(&s->objs[idx], 0, sizeof(Object));
+    return &s->objs[idx];
+}
+
+/* type: 0 Lambertian(param=absorb), 1 Metal(fuzz), 2 Dieletric(ior), 3 Emission(intensity) */
+int orc_material(Scene* s, int idx, int type, const float albedo[3], float param) {
+    Material* m = mat_at(s, idx);
+    if (!m || type < 0 || type > 3) return 1;
+    m->defined = 1;
+    m->type = type;
+    m->albedo = albedo ? v3(albedo[0], albedo[1], albedo[2]) : v3(1.0f, 1.0f, 1.0f);
+    m->param = param;
+    return 0;
+}
+
+int orc_material_defined(const Scene* s, int idx) {
+    return idx >= 0 && idx < s->n_mats && s->mats[idx].defined;
+}
+
+int orc_sphere(Scene* s, int idx, const float c[3], float r, int mat) {
+    Object* o = obj_at(s, idx);
+    if (!o) return 1;
+    o->defined = 1; o->type = O_SPHERE; o->material = mat;
+    o->center = v3(c[0], c[1], c[2]); o->radius = r;
+    return 0;
+}
+
+int orc_moving_sphere(Scene* s, int idx, const float c0[3], const float c1[3], float t0, float t1, float r, int mat) {
+    Object* o = obj_at(s, idx);
+    if (!o) return 1;
+    o->defined = 1; o->type = O_MOVING; o->material = mat;
+    o->center = v3(c0[0], c0[1], c0[2]); o->center1 = v3(c1[0], c1[1], c1[2]);
+    o->time0 = t0; o->time1 = t1; o->radius = r;
+    return 0;
+}
+
+static Plane make_plane(V3 p, V3 n, V3 e, int mat, int orient, int two) {
+    Plane pl;
+    pl.position = p; pl.normal = n; pl.extend = e; pl.material = mat; pl.orientation = orient; pl.two_side = two;
+    return pl;
+}
+
+int orc_plane(Scene* s, int idx, const float p[3], const float n[3], const float e[3], int mat, int orient, int two) {
+    Object* o = obj_at(s, idx);
+    if (!o) return 1;
+    o->defined = 1; o->type = O_PLANE; o->material = mat;
+    o->plane = make_plane(v3(p[0], p[1], p[2]), v3(n[0], n[1], n[2]), v3(e[0], e[1], e[2]), mat, orient, two);
+    return 0;
+}
+
+int orc_cube(Scene* s, int idx, const float c[3], const float e[3], int mat) {
+    Object* o = obj_at(s, idx);
+    if (!o) return 1;
+    V3 C = v3(c[0], c[1], c[2]), E = v3(e[0], e[1], e[2]);
+    o->defined = 1; o->type = O_CUBE; o->material = mat; o->center = C;
+    o->faces[0] = make_plane(v3(C.x - E.x, C.y, C.z), v3(-1, 0, 0), E, mat, 1, 1);
+    o->faces[1] = make_plane(v3(C.x + E.x, C.y, C.z), v3(1, 0, 0), E, mat, 1, 1);
+    o->faces[2] = make_plane(v3(C.x, C.y + E.y, C.z), v3(0, 1, 0), E, mat, 2, 1);
+    o->faces[3] = make_plane(v3(C.x, C.y - E.y, C.z), v3(0, -1, 0), E, mat, 2, 1);
+    o->faces[4] = make_plane(v3(C.x, C.y, C.z + E.z), v3(0, 0, 1), E, mat, 0, 1);
+    o->faces[5] = make_plane(v3(C.x, C.y, C.z - E.z), v3(0, 0, -1), E, mat, 0, 1);
+    return 0;
+}
+
+/* createTriangleMeshData / prepareTriangleData / computeMeshAABB (main.cu:261-350, 384-401) */
+int orc_mesh(Scene* s, int idx, const float* verts, int n_tris, int mat) {
+    if (n_tris <= 0) return 0; /* empty meshes are not created (main.cu:777) */
+    Object* o = obj_at(s, idx);
+    if (!o) return 1;
+    o->defined = 1; o->type = O_MESH; o->material = mat; o->tri_count = n_tris;
+    o->tri_data = (float*)malloc((size_t)n_tris * 12 * sizeof(float));
+    V3 mn = v3(verts[0], verts[1], verts[2]), mx = mn;
+    for (int i = 0; i < n_tris * 3; ++i) {
+        const float* p = verts + 3 * i;
+        if (p[0] < mn.x) mn.x = p[0];
+        if (p[1] < mn.y) mn.y = p[1];
+        if (p[2] < mn.z) mn.z = p[2];
+        if (p[0] > mx.x) mx.x = p[0];
+        if (p[1] > mx.y) mx.y = p[1];
+        if (p[2] > mx.z) mx.z = p[2];
+    }
+    o->bounds[0] = mn; o->bounds[1] = mx;
+    for (int i = 0; i < n_tris; ++i) {
+        const float* p = verts + 9 * i;
+        V3 v0 = v3(p[0], p[1], p[2]), v1 = v3(p[3], p[4], p[5]), v2 = v3(p[6], p[7], p[8]);
+        V3 E1 = vsub(v1, v0), E2 = vsub(v2, v0);
+        V3 n = vnorm(vcross(E1, E2));
+        float* d = o->tri_data + 12 * i;
+        d[0] = v0.x; d[1] = v0.y; d[2] = v0.z; d[3] = n.x;
+        d[4] = E1.x; d[5] = E1.y; d[6] = E1.z; d[7] = n.y;
+        d[8] = E2.x; d[9] = E2.y; d[10] = E2.z; d[11] = n.z;
+    }
+    return 0;
+}
+
+/* tinyobjloader tryParseDouble (tiny_obj_loader.h:837-965) */
+static int obj_parse_double(const char* s, const char* e, double* result) {
+    if (s >= e) return 0;
+    double mantissa = 0.0;
+    int exponent = 0, read = 0, lead = 0;
+    char sign = '+', esign = '+';
+    const char* c = s;
+    if (*c == '+' || *c == '-') { sign = *c; c++; if (c != e && *c == '.') lead = 1; }
+    else if (*c >= '0' && *c <= '9') {}
+    else if (*c == '.') lead = 1;
+    else return 0;
+    if (!lead) {
+        while (c != e && *c >= '0' && *c <= '9') { mantissa *= 10; mantissa += (int)(*c - '0'); c++; read++; }
+        if (read == 0) return 0;
+    }
+    if (c == e) goto assemble;
+    if (*c == '.') {
+        static const double lut[] = {1.0, 0.1, 0.01, 0.001, 0.0001, 0.00001, 0.000001, 0.0000001};
+        c++; read = 1;
+        while (c != e && *c >= '0' && *c <= '9') {
+            mantissa += (int)(*c - '0') * (read < 8 ? lut[read] : pow(10.0, -read));
+            read++; c++;
+        }
+    } else if (*c == 'e' || *c == 'E') {
+    } else goto assemble;
+    if (c == e) goto assemble;
+    if (*c == 'e' || *c == 'E') {
+        c++;
+        if (c != e && (*c == '+' || *c == '-')) { esign = *c; c++; }
+        else if (c != e && *c >= '0' && *c <= '9') {}
+        else return 0;
+        read = 0;
+        while (c != e && *c >= '0' && *c <= '9') { exponent = exponent * 10 + (int)(*c - '0'); c++; read++; }
+        exponent *= (esign == '+' ? 1 : -1);
+        if (read == 0) return 0;
+    }
+assemble:
+    *result = (sign == '+' ? 1 : -1) * (exponent ? ldexp(mantissa * pow(5.0, exponent), exponent) : mantissa);
+    return 1;
+}
+
+static float obj_real(const char** p) {
+    *p += strspn(*p, " \t");
+    const char* end = *p + strcspn(*p, " \t\r\n");
+    double v = 0.0;
+    obj_parse_double(*p, end, &v);
+    *p = end;
+    return (float)v;
+}
+
+/* loadModel(file, scale, rotate, offset) (ModelLoader.cpp:418-448).
+ * Returns triangle count (>= 0) or -1 on error; *out is malloc'ed (9 floats/tri). */
+int orc_load_obj(const char* path, const float scale[3], const float rotate[3], const float offset[3], float** out) {
+    FILE* f = fopen(path, "rb");
+    if (!f) return -1;
+    float* pos = NULL; int npos = 0, cpos = 0;
+    int* idx = NULL; int nidx = 0, cidx = 0;
+    int shape_started = 0, first_done = 0;
+    char line[4096];
+    while (fgets(line, sizeof line, f)) {
+        const char* p = line + strspn(line, " \t");
+        if (p[0] == 'v' && (p[1] == ' ' || p[1] == '\t')) {
+            p += 2;
+            if (npos + 3 > cpos) { cpos = cpos ? 2 * cpos : 1024; pos = (float*)realloc(pos, (size_t)cpos * sizeof(float)); }
+            pos[npos++] = obj_real(&p); pos[npos++] = obj_real(&p); pos[npos++] = obj_real(&p);
+        } else if ((p[0] == 'o' || p[0] == 'g') && (p[1] == ' ' || p[1] == '\t')) {
+            if (shape_started && nidx > 0) first_done = 1;
+        } else if (p[0] == 'f' && (p[1] == ' ' || p[1] == '\t')) {
+            if (first_done) continue;
+            shape_started = 1;
+            p += 2;
+            int face[64], nf = 0, nv = npos / 3;
+            while (*p && *p != '\n' && *p != '\r') {
+                p += strspn(p, " \t");
+                if (!*p || *p == '\n' || *p == '\r') break;
+                int v = atoi(p);
+                if (v > 0) v -= 1; else if (v < 0) v = nv + v; else { fclose(f); free(pos); free(idx); return -1; }
+                if (v < 0 || v >= nv || nf >= 64) { fclose(f); free(pos); free(idx); return -1; }
+                face[nf++] = v;
+                p += strcspn(p, " \t\r\n");
+            }
+            if (nf < 3) continue;
+            if (nidx + 6 > cidx) { cidx = cidx ? 2 * cidx : 1024; idx = (int*)realloc(idx, (size_t)cidx * sizeof(int)); }
+            if (nf == 3) {
+                idx[nidx++] = face[0]; idx[nidx++] = face[1]; idx[nidx++] = face[2];
+            } else if (nf == 4) {
+                const float *v0 = pos + 3 * face[0], *v1 = pos + 3 * face[1], *v2 = pos + 3 * face[2], *v3p = pos + 3 * face[3];
+                float e02x = v2[0] - v0[0], e02y = v2[1] - v0[1], e02z = v2[2] - v0[2];
+                float e13x = v3p[0] - v1[0], e13y = v3p[1] - v1[1], e13z = v3p[2] - v1[2];
+                float s02 = e02x * e02x + e02y * e02y + e02z * e02z;
+                float s13 = e13x * e13x + e13y * e13y + e13z * e13z;
+                if (s02 < s13) {
+                    int t[6] = {face[0], face[1], face[2], face[0], face[2], face[3]};
+                    memcpy(idx + nidx, t, sizeof t);
+                } else {
+                    int t[6] = {face[0], face[1], face[3], face[1], face[2], face[3]};
+                    memcpy(idx + nidx, t, sizeof t);
+                }
+                nidx += 6;
+            } else {
+                fclose(f); free(pos); free(idx); return -1; /* n-gon ear clipping not restated */
+            }
+        }
+    }
+    fclose(f);
+    int ntri = nidx / 3;
+    float* v = (float*)malloc((size_t)(nidx > 0 ? nidx : 1) * 3 * sizeof(float));
+    float ry = radians_f(rotate[1]);
+    for (int i = 0; i < nidx; ++i) {
+        V3 q = v3(pos[3 * idx[i]], pos[3 * idx[i] + 1], pos[3 * idx[i] + 2]);
+        q = vmulv(q, v3(scale[0], scale[1], scale[2]));                            /* vertex *= scale */
+        q = v3(q.x * cosf(ry) + q.z * sinf(ry), q.y, -q.x * sinf(ry) + q.z * cosf(ry)); /* rotateY */
+        q = vadd(q, v3(offset[0], offset[1], offset[2]));                          /* += offset */
+        v[3 * i] = q.x; v[3 * i + 1] = q.y; v[3 * i + 2] = q.z;
+    }
+    free(pos); free(idx);
+    *out = v;
+    return ntri;
+}
+
+void orc_free(void* p) { free(p); }
+
+int orc_mesh_obj(Scene* s, int idx, const char* path, const float scale[3], const float rotate[3],
+                 const float offset[3], int mat) {
+    float* v = NULL;
+    int n = orc_load_obj(path, scale, rotate, offset, &v);
+    if (n < 0) return 1;
+    int r = orc_mesh(s, idx, v, n, mat);
+    free(v);
+    return r;
+}
+
+/* Camera::initialize + updateViewMatrix (Camera.h:19-34, 86-103) */
+int orc_camera(Scene* s, const float eye[3], const float center[3], const float up[3], float aspect,
+               float fov, float aperture, float focus, float t0, float t1) {
+    float scale_ = tanf(radians_f(fov / 2.0f));
+    float vh = 2.0f * scale_;
+    float vw = vh * aspect;
+    V3 E = v3(eye[0], eye[1], eye[2]), C = v3(center[0], center[1], center[2]), U = v3(up[0], up[1], up[2]);
+    V3 forward = vnorm(vsub(C, E));
+    V3 right = vnorm(vcross(forward, U));
+    V3 true_up = vcross(right, forward);
+    s->origin = E;
+    s->horizontal = vmul(vmul(right, vw), focus);
+    s->vertical = vmul(vmul(true_up, vh), focus);
+    s->lower_left = vadd(vsub(vsub(E, vdiv(s->horizontal, 2.0f)), vdiv(s->vertical, 2.0f)), vmul(forward, focus));
+    s->right = right;
+    s->true_up = true_up;
+    s->lens_radius = aperture / 2.0f;
+    s->time0 = t0;
+    s->time1 = t1;
+    s->has_camera = 1;
+    return 0;
+}
+
+/* Vector3Df::length, used by main.cu:635 for the focus distance. */
+float orc_length(const float v[3]) { return vlen(v3(v[0], v[1], v[2])); }
+
+static int owned_rows(int h, int blk, int rank, int world) {
+    int n = 0;
+    for (int b = rank; b * blk < h; b += world) {
+        int r0 = b * blk, r1 = r0 + blk < h ? r0 + blk : h;
+        n += r1 - r0;
+    }
+    return n;
+}
+
+/* renderKernel (main.cu:160-206) for the rows owned by (row_block, rank, world).
+ * out: owned_rows * width * 3 floats, mean radiance (color / spp).
+ * stats (may be NULL): [0] segments, [1] triangle tests. */
+int orc_render(const Scene* s, int width, int height, int spp, int bounces, uint32_t seed,
+               uint32_t sample_offset, int row_block, int row_rank, int row_world, int threads,
+               float* out, uint64_t* stats) {
+    if (!s->has_camera || width < 2 || height < 2 || spp < 1 || bounces < 0 || row_block < 1 ||
+        row_world < 1 || row_rank < 0 || row_rank >= row_world)
+        return 1;
+    for (int i = 0; i < s->n_objs; ++i) {
+        const Object* o = &s->objs[i];
+        if (!o->defined) continue;
+        if (o->material < 0 || o->material >= s->n_mats || !s->mats[o->material].defined) return 2;
+    }
+    int local_rows = owned_rows(height, row_block, row_rank, row_world);
+    uint64_t segs = 0, tris = 0;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : segs, tris)
+#endif
+    for (int lr = 0; lr < local_rows; ++lr) {
+        int lb = lr / row_block;
+        int y = (lb * row_world + row_rank) * row_block + (lr - lb * row_block);
+        for (int x = 0; x < width; ++x) {
+            uint32_t pixel = (uint32_t)y * (uint32_t)width + (uint32_t)x;
+            V3 color = v3(0.0f, 0.0f, 0.0f);
+            for (int i = 0; i < spp; ++i) {
+                RandState rs;
+                rand_init(&rs, seed, pixel, sample_offset + (uint32_t)i);
+                float rx = curand_uniform_(&rs);
+                float ry = curand_uniform_(&rs);
+                float dx = ((float)x + rx) / (float)(width - 1);
+                float dy = ((float)y + ry) / (float)(height - 1);
+                Ray ray = camera_get_ray(s, dx, dy, &rs);
+                color = vadd(color, ray_color(s, ray, bounces, &rs, &segs, &tris));
+            }
+            V3 m = vdiv(color, (float)spp);
+            float* o = out + ((size_t)lr * width + x) * 3;
+            o[0] = m.x; o[1] = m.y; o[2] = m.z;
+        }
+    }
+    if (stats) { stats[0] = segs; stats[1] = tris; }
+    return 0;
+}
+
+/* ---- known-answer hooks for tests ---- */
+void orc_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) { philox(ctr, key, out); }
+
+void orc_uniforms(uint32_t seed, uint32_t pixel, uint32_t sample, int n, float* out) {
+    RandState rs;
+    rand_init(&rs, seed, pixel, sample);
+    for (int i = 0; i < n; ++i) out[i] = curand_uniform_(&rs);
+}
+
+/* Single closest-hit query: returns 1 on hit, fills t, normal[3], front, material. */
+int orc_trace(const Scene* s, const float o[3], const float d[3], float time, float* t, float normal[3],
+              int* front, int* material) {
+    Ray r = make_ray(v3(o[0], o[1], o[2]), v3(d[0], d[1], d[2]), time);
+    HitResult h;
+    memset(&h, 0, sizeof h);
+    uint64_t tt = 0;
+    int hit = scene_hit(s, &r, ORC_EPS, INFINITY, &h, &tt);
+    if (hit) {
+        *t = h.t; normal[0] = h.normal.x; normal[1] = h.normal.y; normal[2] = h.normal.z;
+        *front = h.front_face; *material = h.material;
+    }
+    return hit;
+}
+
+/* Canvas::gamma (Canvas.h:198-200) */
+void orc_gamma_u8(const float* rgb, int64_t n, uint8_t* out) {
+    for (int64_t i = 0; i < n; ++i) {
+        float v = fmaxf(0.0f, fminf(sqrtf(rgb[i]), 0.999f));
+        out[i] = (uint8_t)(uint32_t)(255.99f * v);
+    }
+}

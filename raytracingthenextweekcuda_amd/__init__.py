@@ -1,0 +1,14 @@
+"""rtmi — MI355X-native path tracer with the scene model of
+erosnick/RayTracingTheNextWeekCUDA.
+
+The renderer is librtmi.so (hand-written HIP megakernel for gfx950 + C ABI,
+include/rtmi.h). This package is the host-side mirror of the reference's scene
+API (Camera / create* factories) over that ABI, plus scene ingestion.
+"""
+from ._lib import RTError, build  # noqa: F401
+from .renderer import (  # noqa: F401
+    Camera, MaterialHandle, Renderer, createCube, createDieletricMaterial,
+    createEmissionMaterial, createLambertianMaterial, createMesh, createMetalMaterial,
+    createMovingSphere, createPlane, createSphere, gamma_u8, owned_row_ids, owned_rows,
+)
+from .scene import cornell_box1, load_yaml_scene  # noqa: F401

@@ -1,0 +1,101 @@
+"""ctypes binding of librtmi.so (include/rtmi.h).
+
+The product path always goes through this native library: if librtmi.so is
+missing, importing the renderer raises instead of falling back to anything.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_PATH = os.path.join(PKG_DIR, "librtmi.so")
+
+RT_OK = 0
+STATUS_NAMES = {
+    0: "RT_OK", 1: "RT_ERR_INVALID", 2: "RT_ERR_HIP", 3: "RT_ERR_IO", 4: "RT_ERR_STATE",
+    5: "RT_ERR_OOM", 6: "RT_ERR_NODEV", 7: "RT_ERR_OVERFLOW",
+}
+
+# Every symbol include/rtmi.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "rt_abi_version", "rt_create", "rt_destroy", "rt_last_error", "rt_clear_scene",
+    "rt_material_lambertian", "rt_material_metal", "rt_material_dielectric",
+    "rt_material_emission", "rt_material_defined", "rt_sphere", "rt_moving_sphere", "rt_plane",
+    "rt_cube", "rt_mesh", "rt_mesh_obj", "rt_mesh_triangle_count", "rt_mesh_vertices",
+    "rt_camera", "rt_commit", "rt_scene_info", "rt_render", "rt_render_device", "rt_sync_stats", "rt_gamma_u8",
+]
+
+
+class RTError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+class RenderParams(C.Structure):
+    _fields_ = [
+        ("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32),
+        ("max_depth", C.c_int32), ("seed", C.c_uint32), ("sample_offset", C.c_uint32),
+        ("row_block", C.c_int32), ("row_rank", C.c_int32), ("row_world", C.c_int32),
+    ]
+
+
+class RenderStats(C.Structure):
+    _fields_ = [
+        ("segments", C.c_uint64), ("samples", C.c_uint64), ("node_visits", C.c_uint64),
+        ("tri_tests", C.c_uint64), ("box_tests", C.c_uint64), ("kernel_ms", C.c_double),
+        ("overflow", C.c_uint32),
+    ]
+
+
+def build(arch: str = "gfx950") -> str:
+    """Compile librtmi.so in-tree with hipcc (cross-compiles without a GPU)."""
+    subprocess.run(["make", "-s", "-C", CSRC, f"ARCH={arch}", "-j4"], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"librtmi.so not found at {LIB_PATH}: build it with __graft_entry__.build() "
+            "(the renderer has no fallback path)")
+    L = C.CDLL(LIB_PATH)
+    vp, fp, i32 = C.c_void_p, C.POINTER(C.c_float), C.c_int32
+    L.rt_abi_version.restype = i32
+    L.rt_create.argtypes = [i32, C.POINTER(vp)]
+    L.rt_destroy.argtypes = [vp]
+    L.rt_destroy.restype = None
+    L.rt_last_error.argtypes = [vp]
+    L.rt_last_error.restype = C.c_char_p
+    L.rt_clear_scene.argtypes = [vp]
+    L.rt_material_lambertian.argtypes = [vp, i32, fp, C.c_float]
+    L.rt_material_metal.argtypes = [vp, i32, fp, C.c_float]
+    L.rt_material_dielectric.argtypes = [vp, i32, C.c_float]
+    L.rt_material_emission.argtypes = [vp, i32, fp, C.c_float]
+    L.rt_material_defined.argtypes = [vp, i32]
+    L.rt_sphere.argtypes = [vp, i32, fp, C.c_float, i32, i32]
+    L.rt_moving_sphere.argtypes = [vp, i32, fp, fp, C.c_float, C.c_float, C.c_float, i32]
+    L.rt_plane.argtypes = [vp, i32, fp, fp, fp, i32, i32, i32]
+    L.rt_cube.argtypes = [vp, i32, fp, fp, i32]
+    L.rt_mesh.argtypes = [vp, i32, fp, i32, i32]
+    L.rt_mesh_obj.argtypes = [vp, i32, C.c_char_p, fp, fp, fp, i32]
+    L.rt_mesh_triangle_count.argtypes = [vp, i32]
+    L.rt_mesh_vertices.argtypes = [vp, i32, fp, i32]
+    L.rt_camera.argtypes = [vp, fp, fp, fp] + [C.c_float] * 6
+    L.rt_commit.argtypes = [vp]
+    L.rt_scene_info.argtypes = [vp, C.POINTER(C.c_int32)]
+    L.rt_render.argtypes = [vp, C.POINTER(RenderParams), fp]
+    L.rt_render_device.argtypes = [vp, C.POINTER(RenderParams), vp, vp]
+    L.rt_sync_stats.argtypes = [vp, C.POINTER(RenderStats)]
+    L.rt_gamma_u8.argtypes = [fp, C.c_int64, C.POINTER(C.c_uint8)]
+    _lib = L
+    return L

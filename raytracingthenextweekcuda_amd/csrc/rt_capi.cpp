@@ -1,0 +1,462 @@
+// rt_capi.cpp — the C ABI of include/rtmi.h.
+//
+// Replaces the reference's host driver (main.cu initialize/pathTracing/cleanup,
+// main.cu:555-936) and the device-side `new` factories of kernels.h with a
+// context that owns a host scene description and its device tables.
+#include "../../include/rtmi.h"
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "rt_kernel.h"
+#include "rt_scene.h"
+
+struct rt_ctx {
+    int device = -1;
+    std::string err;
+    rt::HostScene scene;
+    bool committed = false;
+
+    // device tables
+    rt::ObjRec* d_objs = nullptr;
+    rt::TriRec* d_tris = nullptr;
+    rt::MatRec* d_mats = nullptr;
+    int n_objs = 0;
+    int n_mats = 0;
+    unsigned long long* d_counters = nullptr;
+    float* d_out = nullptr;   // staging buffer for rt_render (host output)
+    size_t d_out_bytes = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool have_events = false;
+    rt_render_stats last{};
+    bool stats_pending = false;
+};
+
+namespace {
+
+rt_status fail(rt_ctx* c, rt_status s, const std::string& msg) {
+    if (c) c->err = msg;
+    return s;
+}
+
+rt_status hip_fail(rt_ctx* c, hipError_t e, const char* what) {
+    return fail(c, RT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define RT_HIP(c, call)                                 \
+    do {                                                \
+        hipError_t _e = (call);                         \
+        if (_e != hipSuccess) return hip_fail(c, _e, #call); \
+    } while (0)
+
+bool finite3(const float* v) { return v && isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2]); }
+
+rt::HostMaterial* mat_slot(rt_ctx* c, int32_t index) {
+    if (index < 0 || index > (1 << 24)) return nullptr;
+    if ((size_t)index >= c->scene.materials.size()) c->scene.materials.resize(index + 1);
+    c->committed = false;
+    return &c->scene.materials[index];
+}
+
+rt::HostObject* obj_slot(rt_ctx* c, int32_t index) {
+    if (index < 0 || index > (1 << 24)) return nullptr;
+    if ((size_t)index >= c->scene.objects.size()) c->scene.objects.resize(index + 1);
+    c->committed = false;
+    return &c->scene.objects[index];
+}
+
+void free_device(rt_ctx* c) {
+    if (c->device < 0) return;
+    (void)hipFree(c->d_objs);
+    (void)hipFree(c->d_tris);
+    (void)hipFree(c->d_mats);
+    c->d_objs = nullptr;
+    c->d_tris = nullptr;
+    c->d_mats = nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t rt_abi_version(void) { return RTMI_ABI_VERSION; }
+
+rt_status rt_create(int32_t device, rt_ctx** out) {
+    if (!out) return RT_ERR_INVALID;
+    *out = nullptr;
+    rt_ctx* c = new (std::nothrow) rt_ctx();
+    if (!c) return RT_ERR_OOM;
+    c->device = device;
+    if (device >= 0) {
+        int n = 0;
+        hipError_t e = hipGetDeviceCount(&n);
+        if (e != hipSuccess || n == 0) {
+            delete c;
+            return RT_ERR_NODEV;
+        }
+        if (device >= n) {
+            delete c;
+            return RT_ERR_INVALID;
+        }
+        if (hipSetDevice(device) != hipSuccess ||
+            hipMalloc(&c->d_counters, rt::kNumCounters * sizeof(unsigned long long)) != hipSuccess ||
+            hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+            delete c;
+            return RT_ERR_HIP;
+        }
+        c->have_events = true;
+    }
+    *out = c;
+    return RT_OK;
+}
+
+void rt_destroy(rt_ctx* c) {
+    if (!c) return;
+    if (c->device >= 0) {
+        (void)hipSetDevice(c->device);
+        free_device(c);
+        (void)hipFree(c->d_counters);
+        (void)hipFree(c->d_out);
+        if (c->have_events) {
+            (void)hipEventDestroy(c->ev0);
+            (void)hipEventDestroy(c->ev1);
+        }
+    }
+    delete c;
+}
+
+const char* rt_last_error(const rt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+rt_status rt_clear_scene(rt_ctx* c) {
+    if (!c) return RT_ERR_INVALID;
+    c->scene = rt::HostScene();
+    c->committed = false;
+    return RT_OK;
+}
+
+// ---- materials (kernels.h:50-84) ----
+rt_status rt_material_lambertian(rt_ctx* c, int32_t index, const float albedo[3], float absorb) {
+    (void)absorb;  // stored but unused by the reference's Lambertian::scatter (Material.h:35)
+    if (!c) return RT_ERR_INVALID;
+    if (!finite3(albedo)) return fail(c, RT_ERR_INVALID, "lambertian: albedo must be 3 finite floats");
+    rt::HostMaterial* m = mat_slot(c, index);
+    if (!m) return fail(c, RT_ERR_INVALID, "material index out of range");
+    m->defined = true;
+    m->rec = rt::MatRec{RT_LAMBERTIAN, albedo[0], albedo[1], albedo[2], 0.0f, 0, 0, 0};
+    return RT_OK;
+}
+
+rt_status rt_material_metal(rt_ctx* c, int32_t index, const float albedo[3], float fuzz) {
+    if (!c) return RT_ERR_INVALID;
+    if (!finite3(albedo) || !isfinite(fuzz))
+        return fail(c, RT_ERR_INVALID, "metal: albedo/fuzz must be finite");
+    rt::HostMaterial* m = mat_slot(c, index);
+    if (!m) return fail(c, RT_ERR_INVALID, "material index out of range");
+    m->defined = true;
+    // Metal ctor: fuzz(inFuzz < 1.0f ? inFuzz : 1.0f) (Material.h:40).
+    m->rec = rt::MatRec{RT_METAL, albedo[0], albedo[1], albedo[2], fuzz < 1.0f ? fuzz : 1.0f, 0, 0, 0};
+    return RT_OK;
+}
+
+rt_status rt_material_dielectric(rt_ctx* c, int32_t index, float ior) {
+    if (!c) return RT_ERR_INVALID;
+    if (!isfinite(ior) || ior <= 0.0f) return fail(c, RT_ERR_INVALID, "dielectric: ior must be > 0");
+    rt::HostMaterial* m = mat_slot(c, index);
+    if (!m) return fail(c, RT_ERR_INVALID, "material index out of range");
+    m->defined = true;
+    m->rec = rt::MatRec{RT_DIELECTRIC, 1.0f, 1.0f, 1.0f, ior, 0, 0, 0};
+    return RT_OK;
+}
+
+rt_status rt_material_emission(rt_ctx* c, int32_t index, const float albedo[3], float intensity) {
+    if (!c) return RT_ERR_INVALID;
+    if (!finite3(albedo) || !isfinite(intensity))
+        return fail(c, RT_ERR_INVALID, "emission: albedo/intensity must be finite");
+    rt::HostMaterial* m = mat_slot(c, index);
+    if (!m) return fail(c, RT_ERR_INVALID, "material index out of range");
+    m->defined = true;
+    // attenuation = albedo * intensity (Material.h:121), precomputed.
+    m->rec = rt::MatRec{RT_EMISSION, albedo[0] * intensity, albedo[1] * intensity,
+                        albedo[2] * intensity, intensity, 0, 0, 0};
+    return RT_OK;
+}
+
+int32_t rt_material_defined(const rt_ctx* c, int32_t index) {
+    if (!c || index < 0 || (size_t)index >= c->scene.materials.size()) return 0;
+    return c->scene.materials[index].defined ? 1 : 0;
+}
+
+// ---- hitables (kernels.h:99-154) ----
+rt_status rt_sphere(rt_ctx* c, int32_t index, const float center[3], float radius,
+                    int32_t material, int32_t shading) {
+    (void)shading;  // Sphere::bShading is stored but never read on the hot path
+    if (!c) return RT_ERR_INVALID;
+    if (!finite3(center) || !isfinite(radius)) return fail(c, RT_ERR_INVALID, "sphere: non-finite input");
+    rt::HostObject* o = obj_slot(c, index);
+    if (!o) return fail(c, RT_ERR_INVALID, "object index out of range");
+    *o = rt::HostObject();
+    o->defined = true;
+    o->type = rt::kObjSphere;
+    o->material = (uint32_t)material;
+    memcpy(o->f, center, 3 * sizeof(float));
+    o->f[3] = radius;
+    return RT_OK;
+}
+
+rt_status rt_moving_sphere(rt_ctx* c, int32_t index, const float c0[3], const float c1[3],
+                           float t0, float t1, float radius, int32_t material) {
+    if (!c) return RT_ERR_INVALID;
+    if (!finite3(c0) || !finite3(c1) || !isfinite(t0) || !isfinite(t1) || !isfinite(radius))
+        return fail(c, RT_ERR_INVALID, "moving sphere: non-finite input");
+    rt::HostObject* o = obj_slot(c, index);
+    if (!o) return fail(c, RT_ERR_INVALID, "object index out of range");
+    *o = rt::HostObject();
+    o->defined = true;
+    o->type = rt::kObjMovingSphere;
+    o->material = (uint32_t)material;
+    memcpy(o->f, c0, 3 * sizeof(float));
+    memcpy(o->f + 3, c1, 3 * sizeof(float));
+    o->f[6] = t0;
+    o->f[7] = t1;
+    o->f[8] = radius;
+    return RT_OK;
+}
+
+rt_status rt_plane(rt_ctx* c, int32_t index, const float pos[3], const float normal[3],
+                   const float extend[3], int32_t material, int32_t orientation, int32_t two_side) {
+    if (!c) return RT_ERR_INVALID;
+    if (!finite3(pos) || !finite3(normal) || !finite3(extend))
+        return fail(c, RT_ERR_INVALID, "plane: non-finite input");
+    if (orientation < 0 || orientation > 2) return fail(c, RT_ERR_INVALID, "plane: orientation must be 0..2");
+    rt::HostObject* o = obj_slot(c, index);
+    if (!o) return fail(c, RT_ERR_INVALID, "object index out of range");
+    *o = rt::HostObject();
+    o->defined = true;
+    o->type = rt::kObjPlane;
+    o->material = (uint32_t)material;
+    o->orientation = (uint32_t)orientation;
+    o->two_side = two_side ? 1u : 0u;
+    memcpy(o->f, pos, 3 * sizeof(float));
+    memcpy(o->f + 3, normal, 3 * sizeof(float));
+    memcpy(o->f + 6, extend, 3 * sizeof(float));
+    return RT_OK;
+}
+
+rt_status rt_cube(rt_ctx* c, int32_t index, const float center[3], const float extend[3],
+                  int32_t material) {
+    if (!c) return RT_ERR_INVALID;
+    if (!finite3(center) || !finite3(extend)) return fail(c, RT_ERR_INVALID, "cube: non-finite input");
+    rt::HostObject* o = obj_slot(c, index);
+    if (!o) return fail(c, RT_ERR_INVALID, "object index out of range");
+    *o = rt::HostObject();
+    o->defined = true;
+    o->type = rt::kHostCube;
+    o->material = (uint32_t)material;
+    memcpy(o->f, center, 3 * sizeof(float));
+    memcpy(o->f + 3, extend, 3 * sizeof(float));
+    return RT_OK;
+}
+
+rt_status rt_mesh(rt_ctx* c, int32_t index, const float* v, int32_t n_tris, int32_t material) {
+    if (!c) return RT_ERR_INVALID;
+    if (n_tris < 0 || (n_tris > 0 && !v)) return fail(c, RT_ERR_INVALID, "mesh: bad vertex array");
+    for (int64_t i = 0; i < (int64_t)n_tris * 9; ++i)
+        if (!isfinite(v[i])) return fail(c, RT_ERR_INVALID, "mesh: non-finite vertex");
+    rt::HostObject* o = obj_slot(c, index);
+    if (!o) return fail(c, RT_ERR_INVALID, "object index out of range");
+    *o = rt::HostObject();
+    o->defined = true;
+    o->type = rt::kObjMesh;
+    o->material = (uint32_t)material;
+    o->tri_vertices.assign(v, v + (size_t)n_tris * 9);
+    return RT_OK;
+}
+
+rt_status rt_mesh_obj(rt_ctx* c, int32_t index, const char* path, const float scale[3],
+                      const float rotate[3], const float offset[3], int32_t material) {
+    if (!c) return RT_ERR_INVALID;
+    if (!path || !finite3(scale) || !finite3(rotate) || !finite3(offset))
+        return fail(c, RT_ERR_INVALID, "mesh_obj: bad arguments");
+    std::vector<float> verts;
+    std::string e = rt::load_obj_transformed(path, rt::v3{scale[0], scale[1], scale[2]},
+                                             rt::v3{rotate[0], rotate[1], rotate[2]},
+                                             rt::v3{offset[0], offset[1], offset[2]}, verts);
+    if (!e.empty()) return fail(c, RT_ERR_IO, e);
+    return rt_mesh(c, index, verts.data(), (int32_t)(verts.size() / 9), material);
+}
+
+int32_t rt_mesh_triangle_count(const rt_ctx* c, int32_t index) {
+    if (!c || index < 0 || (size_t)index >= c->scene.objects.size()) return 0;
+    const rt::HostObject& o = c->scene.objects[index];
+    if (!o.defined || o.type != rt::kObjMesh) return 0;
+    return (int32_t)(o.tri_vertices.size() / 9);
+}
+
+rt_status rt_mesh_vertices(const rt_ctx* c, int32_t index, float* out, int32_t max_tris) {
+    int32_t n = rt_mesh_triangle_count(c, index);
+    if (!c || !out || n == 0) return RT_ERR_INVALID;
+    if (max_tris < n) return RT_ERR_INVALID;
+    memcpy(out, c->scene.objects[index].tri_vertices.data(), (size_t)n * 9 * sizeof(float));
+    return RT_OK;
+}
+
+rt_status rt_camera(rt_ctx* c, const float eye[3], const float center[3], const float up[3],
+                    float aspect, float fov, float aperture, float focus, float t0, float t1) {
+    if (!c) return RT_ERR_INVALID;
+    if (!finite3(eye) || !finite3(center) || !finite3(up) || !isfinite(aspect) || !isfinite(fov) ||
+        !isfinite(aperture) || !isfinite(focus) || !isfinite(t0) || !isfinite(t1))
+        return fail(c, RT_ERR_INVALID, "camera: non-finite input");
+    c->scene.camera = rt::make_camera(rt::v3{eye[0], eye[1], eye[2]},
+                                      rt::v3{center[0], center[1], center[2]},
+                                      rt::v3{up[0], up[1], up[2]}, aspect, fov, aperture, focus,
+                                      t0, t1);
+    c->scene.has_camera = true;
+    return RT_OK;
+}
+
+rt_status rt_commit(rt_ctx* c) {
+    if (!c) return RT_ERR_INVALID;
+    std::string e = c->scene.flatten();
+    if (!e.empty()) return fail(c, RT_ERR_INVALID, e);
+    if (c->device < 0) {
+        c->committed = true;
+        return RT_OK;
+    }
+    RT_HIP(c, hipSetDevice(c->device));
+    free_device(c);
+    const auto& S = c->scene;
+    auto up = [&](auto** dst, const auto& vec) -> hipError_t {
+        size_t bytes = vec.size() * sizeof(vec[0]);
+        if (bytes == 0) bytes = 64;  // keep a valid pointer for empty tables
+        hipError_t err = hipMalloc((void**)dst, bytes);
+        if (err != hipSuccess) return err;
+        if (!vec.empty()) err = hipMemcpy(*dst, vec.data(), vec.size() * sizeof(vec[0]), hipMemcpyHostToDevice);
+        return err;
+    };
+    RT_HIP(c, up(&c->d_objs, S.objs));
+    RT_HIP(c, up(&c->d_tris, S.tris));
+    RT_HIP(c, up(&c->d_mats, S.mats));
+    c->n_objs = (int)S.objs.size();
+    c->n_mats = (int)S.mats.size();
+    c->committed = true;
+    return RT_OK;
+}
+
+rt_status rt_scene_info(const rt_ctx* c, int32_t out[8]) {
+    if (!c || !out) return RT_ERR_INVALID;
+    if (!c->committed) return RT_ERR_STATE;
+    for (int i = 0; i < 8; ++i) out[i] = 0;
+    for (const rt::ObjRec& o : c->scene.objs) {
+        if (o.type == rt::kObjPlane) ++out[0];
+        else if (o.type == rt::kObjSphere) ++out[1];
+        else if (o.type == rt::kObjMovingSphere) ++out[2];
+        else ++out[3];
+    }
+    out[4] = (int32_t)c->scene.tris.size();
+    out[5] = (int32_t)c->scene.mats.size();
+    return RT_OK;
+}
+
+static rt_status validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& L) {
+    if (!p) return fail(c, RT_ERR_INVALID, "null params");
+    if (c->device < 0) return fail(c, RT_ERR_NODEV, "context has no device");
+    if (!c->committed) return fail(c, RT_ERR_STATE, "scene not committed (call rt_commit)");
+    if (!c->scene.has_camera) return fail(c, RT_ERR_STATE, "camera not set");
+    if (p->width < 2 || p->height < 2) return fail(c, RT_ERR_INVALID, "width/height must be >= 2");
+    if ((int64_t)p->width * p->height > (int64_t)1 << 31) return fail(c, RT_ERR_INVALID, "frame too large");
+    if (p->spp < 1 || p->max_depth < 0) return fail(c, RT_ERR_INVALID, "spp must be >= 1, max_depth >= 0");
+    if (p->row_block < 1 || p->row_world < 1 || p->row_rank < 0 || p->row_rank >= p->row_world)
+        return fail(c, RT_ERR_INVALID, "bad row tiling");
+    L.width = p->width;
+    L.height = p->height;
+    L.spp = p->spp;
+    L.max_depth = p->max_depth;
+    L.seed = p->seed;
+    L.sample_offset = p->sample_offset;
+    L.row_block = p->row_block;
+    L.row_rank = p->row_rank;
+    L.row_world = p->row_world;
+    L.local_rows = rt::owned_rows(p->height, p->row_block, p->row_rank, p->row_world);
+    return RT_OK;
+}
+
+rt_status rt_render_device(rt_ctx* c, const rt_render_params* p, float* out, void* stream) {
+    if (!c) return RT_ERR_INVALID;
+    rt::RenderLaunch L;
+    rt_status s = validate(c, p, L);
+    if (s != RT_OK) return s;
+    if (!out && L.local_rows > 0) return fail(c, RT_ERR_INVALID, "null output");
+    hipStream_t st = (hipStream_t)stream;
+    RT_HIP(c, hipSetDevice(c->device));
+    RT_HIP(c, hipMemsetAsync(c->d_counters, 0, rt::kNumCounters * sizeof(unsigned long long), st));
+    RT_HIP(c, hipEventRecord(c->ev0, st));
+    rt::KernelScene sc{c->d_objs, c->d_tris, c->d_mats, c->n_objs, c->n_mats};
+    RT_HIP(c, rt::launch_render(sc, c->scene.camera, L, out, c->d_counters, st));
+    RT_HIP(c, hipEventRecord(c->ev1, st));
+    c->last = rt_render_stats{};
+    c->last.samples = (uint64_t)L.local_rows * (uint64_t)L.width * (uint64_t)L.spp;
+    c->stats_pending = true;
+    return RT_OK;
+}
+
+rt_status rt_sync_stats(rt_ctx* c, rt_render_stats* out) {
+    if (!c) return RT_ERR_INVALID;
+    if (c->stats_pending) {
+        RT_HIP(c, hipSetDevice(c->device));
+        RT_HIP(c, hipEventSynchronize(c->ev1));
+        unsigned long long h[rt::kNumCounters];
+        RT_HIP(c, hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
+        float ms = 0.0f;
+        RT_HIP(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        c->last.segments = h[0];
+        c->last.tri_tests = h[1];
+        c->last.box_tests = h[2];
+        c->last.node_visits = h[3];
+        c->last.overflow = h[4] ? 1u : 0u;
+        c->last.kernel_ms = ms;
+        c->stats_pending = false;
+    }
+    if (out) *out = c->last;
+    return RT_OK;
+}
+
+rt_status rt_render(rt_ctx* c, const rt_render_params* p, float* out_host) {
+    if (!c) return RT_ERR_INVALID;
+    rt::RenderLaunch L;
+    rt_status s = validate(c, p, L);
+    if (s != RT_OK) return s;
+    size_t bytes = (size_t)L.local_rows * L.width * 3 * sizeof(float);
+    if (!out_host && bytes) return fail(c, RT_ERR_INVALID, "null output");
+    RT_HIP(c, hipSetDevice(c->device));
+    if (bytes > c->d_out_bytes) {
+        (void)hipFree(c->d_out);
+        c->d_out = nullptr;
+        c->d_out_bytes = 0;
+        RT_HIP(c, hipMalloc(&c->d_out, bytes));
+        c->d_out_bytes = bytes;
+    }
+    s = rt_render_device(c, p, c->d_out, nullptr);
+    if (s != RT_OK) return s;
+    RT_HIP(c, hipStreamSynchronize(nullptr));
+    if (bytes) RT_HIP(c, hipMemcpy(out_host, c->d_out, bytes, hipMemcpyDeviceToHost));
+    s = rt_sync_stats(c, nullptr);
+    if (s != RT_OK) return s;
+    if (c->last.overflow) return fail(c, RT_ERR_OVERFLOW, "BVH traversal stack overflow");
+    return RT_OK;
+}
+
+rt_status rt_gamma_u8(const float* rgb, int64_t n, uint8_t* out) {
+    if (n < 0 || (n > 0 && (!rgb || !out))) return RT_ERR_INVALID;
+    for (int64_t i = 0; i < n; ++i) {
+        // Canvas::gamma (Canvas.h:198-200) with clamp = fmaxf(a, fminf(f, b)) (cutil_math.h:1100-1103).
+        float v = fmaxf(0.0f, fminf(sqrtf(rgb[i]), 0.999f));
+        out[i] = (uint8_t)(uint32_t)(255.99f * v);
+    }
+    return RT_OK;
+}
+
+}  // extern "C"

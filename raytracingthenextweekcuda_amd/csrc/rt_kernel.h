@@ -1,0 +1,36 @@
+// rt_kernel.h — launch interface between the C ABI (rt_capi.cpp) and the HIP
+// megakernel (rt_kernel.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "rt_scene.h"
+
+namespace rt {
+
+// Per-launch parameters (rt_render_params after validation).
+struct RenderLaunch {
+    int32_t width, height, spp, max_depth;
+    uint32_t seed, sample_offset;
+    int32_t row_block, row_rank, row_world;
+    int32_t local_rows;  // rows owned by this shard (output has local_rows * width pixels)
+};
+
+// counters[0] = segments, [1] = triangle tests, [2] = mesh-box tests,
+// [3] = BVH node visits, [4] = traversal overflow flag.
+constexpr int kNumCounters = 8;
+
+hipError_t launch_render(const KernelScene& sc, const CamRec& cam, const RenderLaunch& L,
+                         float* out, unsigned long long* counters, hipStream_t stream);
+
+// Rows of [0, height) owned by (row_block, row_rank, row_world).
+inline int32_t owned_rows(int32_t height, int32_t block, int32_t rank, int32_t world) {
+    int32_t n = 0;
+    for (int32_t b = rank; b * block < height; b += world) {
+        int32_t r0 = b * block, r1 = r0 + block < height ? r0 + block : height;
+        n += r1 - r0;
+    }
+    return n;
+}
+
+}  // namespace rt

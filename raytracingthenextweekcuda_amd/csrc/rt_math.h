@@ -1,0 +1,167 @@
+// rt_math.h — float3 arithmetic and the counter-based RNG used by the render
+// kernel and by the host-side scene preparation.
+//
+// Every operation keeps the reference's evaluation order so that results are
+// bit-identical to a literal restatement of the reference (LinearAlgebra.h
+// Vector3Df, Utils.h helpers). The whole library is compiled with
+// -ffp-contract=off and IEEE division/sqrt (no fast-math), which is what makes
+// host and device results identical.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define RT_HD __host__ __device__ __forceinline__
+#else
+#include <math.h>
+#define RT_HD static inline
+#endif
+
+namespace rt {
+
+constexpr float kFltEpsilon = 1.19209290e-07f;  // FLT_EPSILON (HitResult.h:16, TriangleMesh.cu:72)
+constexpr float kTMin = 0.001f;                 // Math::epsilon (Constants.h:23), rayColor tMin (main.cu:69)
+
+struct v3 {
+    float x, y, z;
+};
+
+RT_HD v3 mk(float x, float y, float z) { return v3{x, y, z}; }
+// Vector3Df operators (LinearAlgebra.h:26-45): component-wise, left to right.
+RT_HD v3 add(v3 a, v3 b) { return v3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+RT_HD v3 sub(v3 a, v3 b) { return v3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+RT_HD v3 mul(v3 a, v3 b) { return v3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+// v * s and s * v are both evaluated as (v.x*s, v.y*s, v.z*s) (LinearAlgebra.h:35,61-63).
+RT_HD v3 scale(v3 a, float s) { return v3{a.x * s, a.y * s, a.z * s}; }
+RT_HD v3 divs(v3 a, float s) { return v3{a.x / s, a.y / s, a.z / s}; }
+RT_HD v3 neg(v3 a) { return v3{-a.x, -a.y, -a.z}; }
+// float + Vector3Df -> (b.x + a, ...) (LinearAlgebra.h:65-67, 39).
+RT_HD v3 adds(v3 a, float s) { return v3{a.x + s, a.y + s, a.z + s}; }
+RT_HD float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+RT_HD float lengthsq(v3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+RT_HD v3 cross(v3 a, v3 b) {
+    return v3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+// normalize(v): norm = sqrtf(x*x+y*y+z*z); (x/norm, y/norm, z/norm) (LinearAlgebra.h:69-72).
+RT_HD v3 normalize(v3 a) {
+    float n = sqrtf(a.x * a.x + a.y * a.y + a.z * a.z);
+    return v3{a.x / n, a.y / n, a.z / n};
+}
+RT_HD v3 rcp(v3 a) { return v3{1.0f / a.x, 1.0f / a.y, 1.0f / a.z}; }
+RT_HD float minf_(float a, float b) { return a < b ? a : b; }
+RT_HD float maxf_(float a, float b) { return a > b ? a : b; }
+
+// ---------------------------------------------------------------------------
+// Counter-based RNG: Philox4x32-10 (Salmon et al., SC'11; Random123 constants).
+// Replaces cuRAND XORWOW (curand_init main.cu:127, curand_uniform Utils.h:44-51).
+// Stream: key = (seed, pixel), counter = (block, sample, 0, 0); draw n of a
+// sample is word (n & 3) of block (n >> 2). Uniform in (0, 1] with curand's
+// mapping x * 2^-32 + 2^-33.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPhiloxM0 = 0xD2511F53u;
+constexpr uint32_t kPhiloxM1 = 0xCD9E8D57u;
+constexpr uint32_t kPhiloxW0 = 0x9E3779B9u;
+constexpr uint32_t kPhiloxW1 = 0xBB67AE85u;
+
+struct u4 {
+    uint32_t x, y, z, w;
+};
+
+RT_HD void mulhilo(uint32_t a, uint32_t b, uint32_t& hi, uint32_t& lo) {
+    uint64_t p = (uint64_t)a * (uint64_t)b;
+    hi = (uint32_t)(p >> 32);
+    lo = (uint32_t)p;
+}
+
+RT_HD u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
+#if defined(__HIPCC__)
+#pragma unroll
+#endif
+    for (int r = 0; r < 10; ++r) {
+        uint32_t hi0, lo0, hi1, lo1;
+        mulhilo(kPhiloxM0, c.x, hi0, lo0);
+        mulhilo(kPhiloxM1, c.z, hi1, lo1);
+        c = u4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += kPhiloxW0;
+        k1 += kPhiloxW1;
+    }
+    return c;
+}
+
+// curand's _curand_uniform: x * CURAND_2POW32_INV + CURAND_2POW32_INV/2 -> (0, 1].
+RT_HD float u01(uint32_t x) {
+    const float inv = 2.3283064e-10f;  // 2^-32
+    return (float)x * inv + (inv / 2.0f);
+}
+
+// Per-lane stream state: one Philox block (4 words) cached in registers.
+struct Rng {
+    uint32_t key0, key1;  // seed, pixel
+    uint32_t sample;      // global sample index
+    uint32_t n;           // draws consumed in this sample
+    u4 buf;
+
+    RT_HD void begin(uint32_t seed, uint32_t pixel, uint32_t s) {
+        key0 = seed;
+        key1 = pixel;
+        sample = s;
+        n = 0;
+    }
+    RT_HD float next() {
+        uint32_t lane = n & 3u;
+        if (lane == 0u) buf = philox4x32_10(u4{n >> 2, sample, 0u, 0u}, key0, key1);
+        uint32_t w = lane == 0u ? buf.x : lane == 1u ? buf.y : lane == 2u ? buf.z : buf.w;
+        ++n;
+        return u01(w);
+    }
+};
+
+// Utils::random(min,max) = min + (max - min) * u (Utils.h:49-51).
+RT_HD float random_range(Rng& r, float lo, float hi) { return lo + (hi - lo) * r.next(); }
+
+// randomInUnitSphere (Utils.h:69-78): x, y, z drawn in order, each 2u + (-1)
+// (randomVector(min,max) = min + (max-min)*v, Utils.h:64-66 -> v*(2) + (-1)).
+RT_HD v3 random_in_unit_sphere(Rng& r) {
+    for (;;) {
+        float x = r.next();
+        float y = r.next();
+        float z = r.next();
+        v3 p = adds(scale(v3{x, y, z}, 2.0f), -1.0f);
+        if (lengthsq(p) >= 1.0f) continue;
+        return p;
+    }
+}
+
+// randomInUnitDisk (Utils.h:96-104). The reference's argument evaluation order
+// is unspecified; this build pins x before y.
+RT_HD v3 random_in_unit_disk(Rng& r) {
+    for (;;) {
+        float x = random_range(r, -1.0f, 1.0f);
+        float y = random_range(r, -1.0f, 1.0f);
+        v3 p = v3{x, y, 0.0f};
+        if (lengthsq(p) >= 1.0f) continue;
+        return p;
+    }
+}
+
+// reflect (Utils.h:112-114): v - 2*dot(v,n)*n, i.e. v - n*((2*dot(v,n))).
+RT_HD v3 reflect(v3 v, v3 n) { return sub(v, scale(n, 2.0f * dot(v, n))); }
+
+// refract (Utils.h:116-121).
+RT_HD v3 refract(v3 uv, v3 n, float eta) {
+    float c = fminf(dot(neg(uv), n), 1.0f);
+    v3 perp = scale(add(uv, scale(n, c)), eta);
+    v3 par = scale(n, -sqrtf(fabsf(1.0f - lengthsq(perp))));
+    return add(perp, par);
+}
+
+// pow(x, 5.0f) in Dieletric::reflectance (Material.h:108). The reference
+// compiled it with --use_fast_math (__powf); this build evaluates the exact
+// product chain ((x*x)*(x*x))*x on host and device alike.
+RT_HD float pow5(float x) {
+    float x2 = x * x;
+    return (x2 * x2) * x;
+}
+
+}  // namespace rt

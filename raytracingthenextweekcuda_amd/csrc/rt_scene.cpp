@@ -1,0 +1,303 @@
+// rt_scene.cpp — host-side scene preparation: camera, triangle records, OBJ
+// ingestion and flattening of the reference's Hitable list into the device
+// tables of rt_scene.h. Compiled with -ffp-contract=off (see Makefile).
+#include "rt_scene.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <fstream>
+#include <sstream>
+
+namespace rt {
+
+namespace {
+// Math::radians (Constants.h:29-31): pi / 180.0f * degree.
+inline float radians(float deg) { return 3.1415926535897932f / 180.0f * deg; }
+
+// rotateY (LinearAlgebra.h:74-77) with the float cos/sin of CUDATypes.h:23-24.
+inline v3 rotate_y(v3 v, float r) {
+    return v3{v.x * cosf(r) + v.z * sinf(r), v.y, -v.x * sinf(r) + v.z * cosf(r)};
+}
+}  // namespace
+
+CamRec make_camera(v3 eye, v3 center, v3 up, float aspect, float fov, float aperture,
+                   float focus, float time0, float time1) {
+    // Camera::updateViewMatrix (Camera.h:86-103).
+    float sc = tanf(radians(fov / 2.0f));
+    float vh = 2.0f * sc;
+    float vw = vh * aspect;
+    v3 forward = normalize(sub(center, eye));
+    v3 right = normalize(cross(forward, up));
+    v3 true_up = cross(right, forward);
+    CamRec c;
+    c.origin = eye;
+    c.horizontal = scale(scale(right, vw), focus);   // viewportWidth * right * focusDistance
+    c.vertical = scale(scale(true_up, vh), focus);   // viewportHeight * trueUp * focusDistance
+    // origin - horizontal/2 - vertical/2 + forward*focusDistance, left to right.
+    c.lower_left = add(sub(sub(eye, divs(c.horizontal, 2.0f)), divs(c.vertical, 2.0f)),
+                       scale(forward, focus));
+    c.right = right;
+    c.true_up = true_up;
+    c.lens_radius = aperture / 2.0f;  // updateLensRadius (Camera.h:110-113)
+    c.time0 = time0;
+    c.time1 = time1;
+    return c;
+}
+
+TriRec make_triangle(v3 p0, v3 p1, v3 p2) {
+    v3 e1 = sub(p1, p0);
+    v3 e2 = sub(p2, p0);
+    v3 n = normalize(cross(e1, e2));
+    TriRec t;
+    t.v0x = p0.x; t.v0y = p0.y; t.v0z = p0.z; t.nx = n.x;
+    t.e1x = e1.x; t.e1y = e1.y; t.e1z = e1.z; t.ny = n.y;
+    t.e2x = e2.x; t.e2y = e2.y; t.e2z = e2.z; t.nz = n.z;
+    return t;
+}
+
+// ---------------------------------------------------------------------------
+// OBJ ingestion. Restates the parts of tinyobjloader v2.0 (vendored by the
+// reference as tinyobjloader/tiny_obj_loader.h) that decide triangle output:
+// its decimal parser (tryParseDouble, :837-965, cast to float in parseReal
+// :967-975), 1-based / negative index fix-up, and the quad split on the
+// shorter diagonal (:1397-1495). n-gons (> 4 vertices) use tinyobjloader's
+// ear clipping, which this loader does not restate: they are rejected.
+// ---------------------------------------------------------------------------
+namespace {
+
+bool parse_obj_double(const char* s, const char* e, double* out) {
+    if (s >= e) return false;
+    double mant = 0.0;
+    int expo = 0;
+    char sign = '+', esign = '+';
+    const char* c = s;
+    int read = 0;
+    bool lead_dot = false;
+    if (*c == '+' || *c == '-') {
+        sign = *c++;
+        if (c != e && *c == '.') lead_dot = true;
+    } else if (*c >= '0' && *c <= '9') {
+    } else if (*c == '.') {
+        lead_dot = true;
+    } else {
+        return false;
+    }
+    if (!lead_dot) {
+        while (c != e && *c >= '0' && *c <= '9') {
+            mant *= 10;
+            mant += (int)(*c - '0');
+            ++c;
+            ++read;
+        }
+        if (read == 0) return false;
+    }
+    if (c != e) {
+        if (*c == '.') {
+            ++c;
+            read = 1;
+            static const double lut[] = {1.0, 0.1, 0.01, 0.001, 0.0001, 0.00001, 0.000001, 0.0000001};
+            while (c != e && *c >= '0' && *c <= '9') {
+                mant += (int)(*c - '0') * (read < 8 ? lut[read] : pow(10.0, -read));
+                ++read;
+                ++c;
+            }
+        }
+        if (c != e && (*c == 'e' || *c == 'E')) {
+            ++c;
+            if (c != e && (*c == '+' || *c == '-')) {
+                esign = *c++;
+            } else if (!(c != e && *c >= '0' && *c <= '9')) {
+                return false;
+            }
+            read = 0;
+            while (c != e && *c >= '0' && *c <= '9') {
+                expo = expo * 10 + (int)(*c - '0');
+                ++c;
+                ++read;
+            }
+            expo *= (esign == '+' ? 1 : -1);
+            if (read == 0) return false;
+        }
+    }
+    *out = (sign == '+' ? 1 : -1) * (expo ? ldexp(mant * pow(5.0, expo), expo) : mant);
+    return true;
+}
+
+float parse_obj_real(const char*& p) {
+    p += strspn(p, " \t");
+    const char* end = p + strcspn(p, " \t\r");
+    double v = 0.0;
+    parse_obj_double(p, end, &v);
+    p = end;
+    return (float)v;
+}
+
+}  // namespace
+
+std::string load_obj_transformed(const std::string& path, v3 scl, v3 rot, v3 off,
+                                 std::vector<float>& out) {
+    std::ifstream in(path);
+    if (!in) return "cannot open OBJ file: " + path;
+    std::vector<float> pos;  // raw positions
+    std::vector<int> idx;    // triangulated position indices
+    std::string line;
+    int lineno = 0;
+    bool first_shape_done = false;
+    bool in_shape = false;
+    while (std::getline(in, line)) {
+        ++lineno;
+        if (!line.empty() && line.back() == '\r') line.pop_back();
+        const char* p = line.c_str();
+        p += strspn(p, " \t");
+        if (p[0] == 'v' && (p[1] == ' ' || p[1] == '\t')) {
+            p += 2;
+            float x = parse_obj_real(p);
+            float y = parse_obj_real(p);
+            float z = parse_obj_real(p);
+            pos.push_back(x);
+            pos.push_back(y);
+            pos.push_back(z);
+        } else if ((p[0] == 'o' || p[0] == 'g') && (p[1] == ' ' || p[1] == '\t')) {
+            // loadModel(file, scale, rotate, offset) keeps only the first mesh
+            // (getMeshes()[0], ModelLoader.cpp:421).
+            if (in_shape && !idx.empty()) first_shape_done = true;
+        } else if (p[0] == 'f' && (p[1] == ' ' || p[1] == '\t')) {
+            if (first_shape_done) continue;
+            in_shape = true;
+            p += 2;
+            std::vector<int> face;
+            const int nv = (int)(pos.size() / 3);
+            while (*p) {
+                p += strspn(p, " \t");
+                if (!*p) break;
+                int v = atoi(p);
+                if (v > 0) v -= 1;
+                else if (v < 0) v = nv + v;
+                else return "OBJ face index 0 at line " + std::to_string(lineno);
+                face.push_back(v);
+                p += strcspn(p, " \t");
+            }
+            if (face.size() < 3) continue;  // degenerate face: skipped (tiny_obj_loader.h:1389-1395)
+            for (int v : face)
+                if (v < 0 || v >= nv) return "OBJ vertex index out of range at line " + std::to_string(lineno);
+            if (face.size() == 3) {
+                idx.insert(idx.end(), face.begin(), face.end());
+            } else if (face.size() == 4) {
+                const float* a = &pos[3 * face[0]];
+                const float* b = &pos[3 * face[1]];
+                const float* c = &pos[3 * face[2]];
+                const float* d = &pos[3 * face[3]];
+                float e02x = c[0] - a[0], e02y = c[1] - a[1], e02z = c[2] - a[2];
+                float e13x = d[0] - b[0], e13y = d[1] - b[1], e13z = d[2] - b[2];
+                float s02 = e02x * e02x + e02y * e02y + e02z * e02z;
+                float s13 = e13x * e13x + e13y * e13y + e13z * e13z;
+                if (s02 < s13) {
+                    int t[6] = {face[0], face[1], face[2], face[0], face[2], face[3]};
+                    idx.insert(idx.end(), t, t + 6);
+                } else {
+                    int t[6] = {face[0], face[1], face[3], face[1], face[2], face[3]};
+                    idx.insert(idx.end(), t, t + 6);
+                }
+            } else {
+                return "OBJ n-gon with " + std::to_string(face.size()) +
+                       " vertices is not supported (line " + std::to_string(lineno) + ")";
+            }
+        }
+    }
+    // ModelLoader.cpp:438-445: vertex *= scale; rotateY(radians(rotate.y)); += offset.
+    out.clear();
+    out.reserve(idx.size() * 3);
+    const float ry = radians(rot.y);
+    for (int i : idx) {
+        v3 v{pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]};
+        v = mul(v, scl);
+        v = rotate_y(v, ry);
+        v = add(v, off);
+        out.push_back(v.x);
+        out.push_back(v.y);
+        out.push_back(v.z);
+    }
+    return "";
+}
+
+std::string HostScene::flatten() {
+    objs.clear();
+    tris.clear();
+    mats.clear();
+    for (size_t i = 0; i < materials.size(); ++i) {
+        MatRec m = materials[i].rec;
+        if (!materials[i].defined) m.type = 0xFFFFFFFFu;  // never referenced by a defined object
+        mats.push_back(m);
+    }
+    auto check_mat = [&](uint32_t m) -> bool {
+        return m < materials.size() && materials[m].defined;
+    };
+    for (size_t i = 0; i < objects.size(); ++i) {
+        const HostObject& o = objects[i];
+        if (!o.defined) continue;  // null slots are skipped (main.cu:49)
+        if (!check_mat(o.material))
+            return "object " + std::to_string(i) + " references undefined material " +
+                   std::to_string(o.material);
+        if (o.type == kHostCube) {
+            // createCube (kernels.h:139-154): six two-sided planes.
+            v3 c{o.f[0], o.f[1], o.f[2]};
+            v3 e{o.f[3], o.f[4], o.f[5]};
+            struct Face { v3 p, n; uint32_t orient; };
+            const Face faces[6] = {
+                {{c.x - e.x, c.y, c.z}, {-1.0f, 0.0f, 0.0f}, 1},
+                {{c.x + e.x, c.y, c.z}, {1.0f, 0.0f, 0.0f}, 1},
+                {{c.x, c.y + e.y, c.z}, {0.0f, 1.0f, 0.0f}, 2},
+                {{c.x, c.y - e.y, c.z}, {0.0f, -1.0f, 0.0f}, 2},
+                {{c.x, c.y, c.z + e.z}, {0.0f, 0.0f, 1.0f}, 0},
+                {{c.x, c.y, c.z - e.z}, {0.0f, 0.0f, -1.0f}, 0},
+            };
+            for (const Face& f : faces) {
+                ObjRec r{};
+                r.type = kObjPlane;
+                r.material = o.material;
+                r.u0 = f.orient;
+                r.u1 = 1;
+                r.f[0] = f.p.x; r.f[1] = f.p.y; r.f[2] = f.p.z;
+                r.f[3] = f.n.x; r.f[4] = f.n.y; r.f[5] = f.n.z;
+                r.f[6] = e.x; r.f[7] = e.y; r.f[8] = e.z;
+                objs.push_back(r);
+            }
+            continue;
+        }
+        ObjRec r{};
+        r.type = o.type;
+        r.material = o.material;
+        memcpy(r.f, o.f, sizeof(r.f));
+        if (o.type == kObjPlane) {
+            r.u0 = o.orientation;
+            r.u1 = o.two_side;
+        } else if (o.type == kObjMesh) {
+            const size_t nt = o.tri_vertices.size() / 9;
+            if (nt == 0) continue;  // empty meshes are not created (main.cu:777)
+            r.u0 = (uint32_t)tris.size();
+            r.u1 = (uint32_t)nt;
+            // computeMeshAABB (main.cu:261-281): per-axis min / max of all vertices.
+            v3 lo{o.tri_vertices[0], o.tri_vertices[1], o.tri_vertices[2]}, hi = lo;
+            for (size_t k = 0; k < nt * 3; ++k) {
+                const float* p = &o.tri_vertices[3 * k];
+                lo.x = std::min(lo.x, p[0]); lo.y = std::min(lo.y, p[1]); lo.z = std::min(lo.z, p[2]);
+                hi.x = std::max(hi.x, p[0]); hi.y = std::max(hi.y, p[1]); hi.z = std::max(hi.z, p[2]);
+            }
+            r.f[0] = lo.x; r.f[1] = lo.y; r.f[2] = lo.z;
+            r.f[3] = hi.x; r.f[4] = hi.y; r.f[5] = hi.z;
+            for (size_t t = 0; t < nt; ++t) {
+                const float* p = &o.tri_vertices[9 * t];
+                tris.push_back(make_triangle(v3{p[0], p[1], p[2]}, v3{p[3], p[4], p[5]},
+                                             v3{p[6], p[7], p[8]}));
+            }
+        }
+        objs.push_back(r);
+    }
+    return "";
+}
+
+}  // namespace rt

@@ -1,0 +1,118 @@
+// rt_scene.h — device scene layout (what lives in HBM) and the host-side scene
+// builder behind the C ABI.
+//
+// Layout rationale: the closest-hit scan walks the object table
+// in the same order for every lane of a wave, so object and triangle records
+// are wave-uniform reads. They are packed AoS records sized for one scalar
+// s_load_dwordx16 / x12 each (64 B / 48 B), which the SMEM path broadcasts to
+// all 64 lanes. Materials are read per lane (divergent) and are 32 B records.
+// BVH nodes (per-lane divergent traversal) are SoA-friendly 32 B records.
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "rt_math.h"
+
+namespace rt {
+
+enum ObjType : uint32_t { kObjSphere = 0, kObjMovingSphere = 1, kObjPlane = 2, kObjMesh = 3 };
+
+// One hitable (Sphere.h, Plane.h, TriangleMesh.h). Cube is flattened into its
+// six planes at build time: Cube::hit (Cube.cu:10-23) is a closest scan over its
+// faces with the caller's closestSoFar, identical to scanning them inline.
+struct alignas(16) ObjRec {
+    uint32_t type;
+    uint32_t material;
+    uint32_t u0;  // plane: orientation | mesh: first triangle
+    uint32_t u1;  // plane: twoSide     | mesh: triangle count
+    // sphere: center xyz, radius
+    // moving sphere: center0 xyz, center1 xyz, time0, time1, radius
+    // plane: position xyz, normal xyz, extend xyz
+    // mesh: boundsMin xyz, boundsMax xyz
+    float f[12];
+};
+static_assert(sizeof(ObjRec) == 64, "ObjRec must be 64 B");
+
+// Triangle as prepared by prepareTriangleData (main.cu:334-349): v0, E1, E2.
+// The per-triangle normal normalize(cross(E1,E2)) that TriangleMesh::hit
+// recomputes for every ray (TriangleMesh.cu:42) is ray-independent and is
+// precomputed here with the same float operations.
+struct alignas(16) TriRec {
+    float v0x, v0y, v0z, nx;
+    float e1x, e1y, e1z, ny;
+    float e2x, e2y, e2z, nz;
+};
+static_assert(sizeof(TriRec) == 48, "TriRec must be 48 B");
+
+struct alignas(16) MatRec {
+    uint32_t type;  // RT_LAMBERTIAN..RT_EMISSION
+    float a0, a1, a2;  // albedo (emission: albedo * intensity, Material.h:121)
+    float p0;          // metal: fuzz (clamped to 1, Material.h:40) | dielectric: ior
+    float pad0, pad1, pad2;
+};
+static_assert(sizeof(MatRec) == 32, "MatRec must be 32 B");
+
+// Camera after updateViewMatrix (Camera.h:86-103), as read by getRay (151-168).
+struct CamRec {
+    v3 origin, lower_left, horizontal, vertical, right, true_up;
+    float lens_radius, time0, time1;
+};
+
+struct KernelScene {
+    const ObjRec* objs;
+    const TriRec* tris;
+    const MatRec* mats;
+    int32_t n_objs;
+    int32_t n_mats;
+};
+
+// ----------------------------------------------------------------------------
+// Host-side scene (built by the C ABI, uploaded by commit()).
+// ----------------------------------------------------------------------------
+struct HostMaterial {
+    bool defined = false;
+    MatRec rec{};
+};
+
+struct HostObject {
+    bool defined = false;
+    uint32_t type = 0;        // kObj* or kHostCube
+    uint32_t material = 0;
+    uint32_t orientation = 0;
+    uint32_t two_side = 1;
+    float f[12] = {0};
+    std::vector<float> tri_vertices;  // mesh: 9 floats / triangle
+};
+constexpr uint32_t kHostCube = 100;
+
+struct HostScene {
+    std::vector<HostMaterial> materials;
+    std::vector<HostObject> objects;
+    bool has_camera = false;
+    CamRec camera{};
+
+    // Flattened tables (valid after flatten()).
+    std::vector<ObjRec> objs;
+    std::vector<TriRec> tris;
+    std::vector<MatRec> mats;
+
+    // Returns "" on success or an error message.
+    std::string flatten();
+};
+
+// Camera::initialize + updateViewMatrix (Camera.h:19-34, 86-103) on the host.
+CamRec make_camera(v3 eye, v3 center, v3 up, float aspect, float fov, float aperture,
+                   float focus, float time0, float time1);
+
+// TriRec from three world-space vertices (prepareTriangleData, main.cu:334-343).
+TriRec make_triangle(v3 p0, v3 p1, v3 p2);
+
+// OBJ loading with loadModel(file, scale, rotate, offset) semantics
+// (ModelLoader.cpp:418-448). Returns "" on success.
+std::string load_obj_transformed(const std::string& path, v3 scale, v3 rotate, v3 offset,
+                                 std::vector<float>& out_tri_vertices);
+
+}  // namespace rt

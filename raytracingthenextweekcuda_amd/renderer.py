@@ -1,0 +1,276 @@
+"""Host-side mirror of the reference's scene API over the C ABI.
+
+The reference builds scenes with device-side factories that take a pointer
+table and a slot index (kernels.h:50-154), a Camera (Camera.h) and a Canvas
+(Canvas.h). This module keeps those names and argument meanings so scene code
+written like main.cu:592-848 ports line by line:
+
+    r = Renderer(device=0)
+    materials, spheres = r.materials, r.objects          # createObjectPtrArray
+    createLambertianMaterial(materials, 0, (1, 0, 0))    # kernels.h:54
+    createSphere(spheres, 0, (-1, 0, -1), 0.5, materials[0])
+    r.set_camera(Camera(eye, center, up, aspect, fov, aperture, focus, 0, 1))
+    img = r.render(width, height, spp, depth)            # pathTracing()
+
+`materials[i]` is None until slot i is created, so the reference's
+`if (materials[id] == nullptr)` guards (main.cu:714-744) read the same.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import RT_OK, RenderParams, RenderStats, RTError, lib
+
+_f3 = C.c_float * 3
+
+
+def _v(x):
+    return _f3(*[float(c) for c in x])
+
+
+@dataclass(frozen=True)
+class MaterialHandle:
+    """Opaque non-null stand-in for a device `Material*`."""
+    index: int
+
+
+class _Table:
+    def __init__(self, renderer: "Renderer"):
+        self._r = renderer
+
+
+class MaterialTable(_Table):
+    """createObjectPtrArray<Material*>(n) (kernels.h:26-31)."""
+
+    def __getitem__(self, i: int):
+        return MaterialHandle(i) if lib().rt_material_defined(self._r.ctx, i) else None
+
+
+class ObjectTable(_Table):
+    """createObjectPtrArray<Hitable*>(n): slot order = closest-hit scan order."""
+
+
+def _mat_index(m) -> int:
+    if m is None:
+        raise ValueError("material is nullptr (slot not created)")
+    return m.index if isinstance(m, MaterialHandle) else int(m)
+
+
+class Camera:
+    """Camera(eye, center, up, aspectRatio, fov=90, aperture=2, focusDistance=1,
+    time0=0, time1=0) — Camera.h:14-17 defaults."""
+
+    def __init__(self, eye, center, up, aspectRatio, fov=90.0, aperture=2.0,
+                 focusDistance=1.0, time0=0.0, time1=0.0):
+        self.initialize(eye, center, up, aspectRatio, fov, aperture, focusDistance, time0, time1)
+
+    def initialize(self, eye, center, up, aspectRatio, fov=90.0, aperture=2.0,
+                   focusDistance=1.0, time0=0.0, time1=0.0):
+        self.eye, self.center, self.up = tuple(eye), tuple(center), tuple(up)
+        self.aspectRatio, self.fov, self.aperture = float(aspectRatio), float(fov), float(aperture)
+        self.focusDistance, self.time0, self.time1 = float(focusDistance), float(time0), float(time1)
+        self.bIsDirty = True
+
+    def setAperture(self, a):
+        self.aperture = float(a)
+        self.bIsDirty = True
+
+    def isDirty(self):
+        return self.bIsDirty
+
+    def resetDiryFlag(self):  # reference spelling (Camera.h:147)
+        self.bIsDirty = False
+
+
+class Renderer:
+    """One rt_ctx on one HIP device (replaces initialize()/cleanup(), main.cu:555-936)."""
+
+    def __init__(self, device: int = 0):
+        self.L = lib()
+        h = C.c_void_p()
+        st = self.L.rt_create(device, C.byref(h))
+        if st != RT_OK:
+            raise RTError(st, f"rt_create(device={device}) failed")
+        self.ctx = h
+        self.device = device
+        self.materials = MaterialTable(self)
+        self.objects = ObjectTable(self)
+        self._camera = None
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.L.rt_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, st):
+        if st != RT_OK:
+            raise RTError(st, self.L.rt_last_error(self.ctx).decode(errors="replace"))
+
+    # ---- scene ----
+    def clear(self):
+        self._check(self.L.rt_clear_scene(self.ctx))
+
+    def lambertian(self, index, albedo, absorb=1.0):
+        self._check(self.L.rt_material_lambertian(self.ctx, index, _v(albedo), absorb))
+
+    def metal(self, index, albedo, fuzz=1.0):
+        self._check(self.L.rt_material_metal(self.ctx, index, _v(albedo), fuzz))
+
+    def dielectric(self, index, ior=1.5):
+        self._check(self.L.rt_material_dielectric(self.ctx, index, ior))
+
+    def emission(self, index, albedo, intensity=1.0):
+        self._check(self.L.rt_material_emission(self.ctx, index, _v(albedo), intensity))
+
+    def sphere(self, index, center, radius, material, shading=True):
+        self._check(self.L.rt_sphere(self.ctx, index, _v(center), radius, _mat_index(material), int(shading)))
+
+    def moving_sphere(self, index, c0, c1, t0, t1, radius, material):
+        self._check(self.L.rt_moving_sphere(self.ctx, index, _v(c0), _v(c1), t0, t1, radius,
+                                            _mat_index(material)))
+
+    def plane(self, index, position, normal, extend, material, orientation=2, two_side=True):
+        self._check(self.L.rt_plane(self.ctx, index, _v(position), _v(normal), _v(extend),
+                                    _mat_index(material), int(orientation), int(bool(two_side))))
+
+    def cube(self, index, center, extend, material):
+        self._check(self.L.rt_cube(self.ctx, index, _v(center), _v(extend), _mat_index(material)))
+
+    def mesh(self, index, tri_vertices, material):
+        v = np.ascontiguousarray(tri_vertices, np.float32).reshape(-1)
+        if v.size % 9:
+            raise ValueError("mesh vertices must be 9 floats per triangle")
+        self._check(self.L.rt_mesh(self.ctx, index, v.ctypes.data_as(C.POINTER(C.c_float)),
+                                   v.size // 9, _mat_index(material)))
+
+    def mesh_obj(self, index, path, scale=(1, 1, 1), rotate=(0, 0, 0), offset=(0, 0, 0), material=3):
+        self._check(self.L.rt_mesh_obj(self.ctx, index, str(path).encode(), _v(scale), _v(rotate),
+                                       _v(offset), _mat_index(material)))
+
+    def mesh_vertices(self, index) -> np.ndarray:
+        n = self.L.rt_mesh_triangle_count(self.ctx, index)
+        out = np.zeros((n, 9), np.float32)
+        if n:
+            self._check(self.L.rt_mesh_vertices(self.ctx, index, out.ctypes.data_as(C.POINTER(C.c_float)), n))
+        return out
+
+    def set_camera(self, cam: Camera):
+        self._camera = cam
+        self._check(self.L.rt_camera(self.ctx, _v(cam.eye), _v(cam.center), _v(cam.up),
+                                     cam.aspectRatio, cam.fov, cam.aperture, cam.focusDistance,
+                                     cam.time0, cam.time1))
+        cam.resetDiryFlag()
+
+    def commit(self):
+        self._check(self.L.rt_commit(self.ctx))
+
+    def object_counts(self) -> dict:
+        """Census of the committed device tables (rt_scene_info)."""
+        out = (C.c_int32 * 8)()
+        self._check(self.L.rt_scene_info(self.ctx, out))
+        keys = ["plane", "sphere", "moving_sphere", "mesh", "triangle", "material", "bvh_node"]
+        return {k: int(out[i]) for i, k in enumerate(keys)}
+
+    # ---- render ----
+    @staticmethod
+    def params(width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,
+               row_rank=0, row_world=1) -> RenderParams:
+        return RenderParams(width, height, spp, max_depth, seed, sample_offset, row_block,
+                            row_rank, row_world)
+
+    def render(self, width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,
+               row_rank=0, row_world=1) -> np.ndarray:
+        """Mean radiance of the owned rows, shape (rows, width, 3), y = 0 bottom."""
+        p = self.params(width, height, spp, max_depth, seed, sample_offset, row_block, row_rank, row_world)
+        rows = owned_rows(height, row_block, row_rank, row_world)
+        out = np.zeros((rows, width, 3), np.float32)
+        self._check(self.L.rt_render(self.ctx, C.byref(p), out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out
+
+    def render_device(self, params: RenderParams, out_ptr: int, stream_ptr: int = 0):
+        """Enqueue a render into a caller-owned device buffer (e.g. a torch tensor's
+        data_ptr()) on a HIP stream (torch.cuda.Stream.cuda_stream)."""
+        self._check(self.L.rt_render_device(self.ctx, C.byref(params), C.c_void_p(out_ptr),
+                                            C.c_void_p(stream_ptr)))
+
+    def stats(self) -> dict:
+        s = RenderStats()
+        self._check(self.L.rt_sync_stats(self.ctx, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in RenderStats._fields_}
+
+
+def owned_rows(height, block, rank, world) -> int:
+    n, b = 0, rank
+    while b * block < height:
+        r0 = b * block
+        n += min(r0 + block, height) - r0
+        b += world
+    return n
+
+
+def owned_row_ids(height, block, rank, world) -> np.ndarray:
+    ids, b = [], rank
+    while b * block < height:
+        ids.extend(range(b * block, min(b * block + block, height)))
+        b += world
+    return np.asarray(ids, np.int64)
+
+
+def gamma_u8(rgb: np.ndarray) -> np.ndarray:
+    """Canvas::gamma (Canvas.h:198-200) through the native library."""
+    rgb = np.ascontiguousarray(rgb, np.float32)
+    out = np.zeros(rgb.shape, np.uint8)
+    st = lib().rt_gamma_u8(rgb.ctypes.data_as(C.POINTER(C.c_float)), rgb.size,
+                           out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    if st != RT_OK:
+        raise RTError(st, "rt_gamma_u8")
+    return out
+
+
+# ---- kernels.h factory names (reference signatures) ----
+def createLambertianMaterial(materials: MaterialTable, index, albedo, absorb=1.0):
+    materials._r.lambertian(index, albedo, absorb)
+
+
+def createMetalMaterial(materials: MaterialTable, index, albedo, fuzz=1.0):
+    materials._r.metal(index, albedo, fuzz)
+
+
+def createDieletricMaterial(materials: MaterialTable, index, indexOfRefraction=1.5):
+    materials._r.dielectric(index, indexOfRefraction)
+
+
+def createEmissionMaterial(materials: MaterialTable, index, albedo, intensity=1.0):
+    materials._r.emission(index, albedo, intensity)
+
+
+def createSphere(spheres: ObjectTable, index, center, radius, material, bShading=True):
+    spheres._r.sphere(index, center, radius, material, bShading)
+
+
+def createMovingSphere(spheres: ObjectTable, index, center0, center1, time0, time1, radius, material):
+    spheres._r.moving_sphere(index, center0, center1, time0, time1, radius, material)
+
+
+def createPlane(planes: ObjectTable, index, position, normal, extend, material, orientation, bTwoSide=True):
+    planes._r.plane(index, position, normal, extend, material, orientation, bTwoSide)
+
+
+def createCube(cubes: ObjectTable, index, center, extend, material):
+    cubes._r.cube(index, center, extend, material)
+
+
+def createMesh(meshes: ObjectTable, index, tri_vertices, material):
+    meshes._r.mesh(index, tri_vertices, material)

@@ -1,0 +1,89 @@
+"""Scene ingestion with the reference's semantics.
+
+load_yaml_scene restates initialize() for SCENE == 1 (main.cu:623-786):
+  * camera from the `camera:` map, focus distance = |center - eye|, aspect =
+    Float(width)/height, shutter [0, 1] (main.cu:632-638);
+  * materials 0-8 are pre-created BEFORE the objects (main.cu:643-651), so a
+    YAML material with an already-used id is ignored (the `== nullptr` guards);
+    e.g. the Cornell-box light (id 8) is Emission(1,1,1)x5 whatever the YAML says;
+  * the primitive type is the FIRST key of each object map (main.cu:706, 749);
+  * meshes always use materials[3] (main.cu:781); empty meshes are skipped.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from .renderer import Camera, Renderer
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+ASSETS = os.path.join(REPO_DIR, "assets")
+SCENES_DIR = os.path.join(ASSETS, "scenes")
+MODELS_DIR = os.path.join(ASSETS, "models")
+
+
+def preseed_materials(r: Renderer):
+    """main.cu:643-651."""
+    r.lambertian(0, (1.0, 0.0, 0.0))
+    r.lambertian(1, (0.0, 1.0, 0.0))
+    r.lambertian(2, (0.0, 0.0, 1.0))
+    r.lambertian(3, (1.0, 1.0, 1.0))
+    r.lambertian(4, (0.75, 0.25, 0.25))
+    r.lambertian(5, (0.25, 0.25, 0.75))
+    r.metal(6, (1.0, 1.0, 1.0), 0.0)
+    r.dielectric(7, 1.5)
+    r.emission(8, (1.0, 1.0, 1.0), 5.0)
+
+
+def load_yaml_scene(r: Renderer, path: str, width: int, height: int, models_dir: str = MODELS_DIR,
+                    commit: bool = True) -> Camera:
+    import yaml
+
+    with open(path) as fh:
+        cfg = yaml.safe_load(fh)
+    cam = cfg["camera"]
+    eye = np.float32(cam["eye"])
+    center = np.float32(cam["center"])
+    d = center - eye
+    focus = np.sqrt(np.float32(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]), dtype=np.float32)
+    aspect = np.float32(width) / np.float32(height)
+    camera = Camera(cam["eye"], cam["center"], cam["up"], float(aspect), float(cam["fov"]),
+                    float(cam["aperture"]), float(focus), 0.0, 1.0)
+    r.set_camera(camera)
+    preseed_materials(r)
+    for i, entry in enumerate(cfg["objects"]):
+        key = next(iter(entry))
+        obj = entry[key]
+        mat = obj["material"]
+        mid = int(obj["materialId"])
+        mtype = int(mat["type"])
+        if r.materials[mid] is None:
+            if mtype == 0:
+                r.lambertian(mid, mat["albedo"])
+            elif mtype == 2:
+                r.dielectric(mid, float(mat["indexOfRefraction"]))
+            elif mtype == 1:
+                r.metal(mid, mat["albedo"], float(mat["fuzz"]))
+            elif mtype == 3:
+                r.emission(mid, mat["albedo"], float(mat["intensity"]))
+        ptype = int(next(iter(obj.values())))
+        if ptype == 0:
+            r.sphere(i, obj["center"], float(obj["radius"]), r.materials[mid])
+        elif ptype == 1:
+            r.plane(i, obj["position"], obj["normal"], obj["extend"], r.materials[mid],
+                    int(obj["orientation"]), bool(obj["twoSide"]))
+        elif ptype == 2:
+            r.mesh_obj(i, os.path.join(models_dir, obj["model"]), obj["scale"], obj["rotate"],
+                       obj["offset"], r.materials[3])
+        else:
+            raise ValueError(f"unknown primitive type {ptype} in {path}")
+    if commit:
+        r.commit()
+    return camera
+
+
+def cornell_box1(r: Renderer, width: int, height: int, commit: bool = True) -> Camera:
+    """BASELINE configs 1-2: resources/scenes/cornellbox1.yaml."""
+    return load_yaml_scene(r, os.path.join(SCENES_DIR, "cornellbox1.yaml"), width, height, commit=commit)

@@ -1,0 +1,151 @@
+"""GPU parity: the HIP megakernel (through the C ABI) against the CPU
+restatement on identical scenes and seeds.
+
+Tolerance (BASELINE.json north_star): per-channel L_inf <= 1e-4 on the float
+mean-radiance buffer. Both sides follow the reference's float evaluation order
+with -ffp-contract=off and IEEE div/sqrt, so the expected result is bit-exact;
+the tests also require identical traced-segment counts (same paths)."""
+import os
+
+import numpy as np
+import pytest
+
+from tests import scenes as S
+
+TOL = 1e-4
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rtmi():
+    import raytracingthenextweekcuda_amd as m
+
+    return m
+
+
+def _oracle_yaml(name, w, h):
+    from oracle import oracle as orc
+
+    return orc.yaml_scene(os.path.join(S.SCENES, name), S.MODELS, w, h)
+
+
+def _check(img, ref, st, ref_st, tag):
+    assert img.shape == ref.shape, tag
+    err = float(np.max(np.abs(img.astype(np.float64) - ref)))
+    exact = float(np.mean(img == ref))
+    assert np.isfinite(img).all(), tag
+    assert err <= TOL, f"{tag}: L_inf {err} (bit-exact fraction {exact:.4f})"
+    assert st["segments"] == ref_st["segments"], (tag, st["segments"], ref_st["segments"])
+    return err, exact
+
+
+@pytest.mark.parametrize("w,h,spp,depth", [(64, 64, 4, 4), (96, 64, 8, 8), (33, 17, 3, 10)])
+def test_cornellbox1_parity(rtmi, w, h, spp, depth):
+    with rtmi.Renderer(0) as r:
+        rtmi.cornell_box1(r, w, h)
+        img = r.render(w, h, spp, depth)
+        st = r.stats()
+    ref, ref_st = _oracle_yaml("cornellbox1.yaml", w, h).render(w, h, spp, depth)
+    err, exact = _check(img, ref, st, ref_st, f"cb1 {w}x{h} spp{spp} d{depth}")
+    assert exact == 1.0, f"expected bit-exact, got {exact}"
+    assert st["tri_tests"] == ref_st["tri_tests"]
+    assert st["samples"] == w * h * spp
+
+
+@pytest.mark.parametrize("name", ["cornellbox0.yaml", "cornellbox2.yaml", "cornellbox_empty.yaml"])
+def test_yaml_scenes_parity(rtmi, name):
+    w, h, spp, depth = 48, 48, 4, 10
+    with rtmi.Renderer(0) as r:
+        rtmi.load_yaml_scene(r, os.path.join(S.SCENES, name), w, h)
+        img = r.render(w, h, spp, depth)
+        st = r.stats()
+    ref, ref_st = _oracle_yaml(name, w, h).render(w, h, spp, depth)
+    _check(img, ref, st, ref_st, name)
+
+
+@pytest.mark.parametrize("maker", [S.spheres_scene, S.mixed_scene])
+def test_spec_scenes_parity(rtmi, maker):
+    spec = maker()
+    w, h, spp, depth = 64, 48, 4, 10
+    with rtmi.Renderer(0) as r:
+        S.build_product(r, spec)
+        img = r.render(w, h, spp, depth, seed=7, sample_offset=3)
+        st = r.stats()
+    ref, ref_st = S.build_oracle(spec).render(w, h, spp, depth, seed=7, sample_offset=3)
+    _check(img, ref, st, ref_st, maker.__name__)
+
+
+@pytest.mark.parametrize("world,block", [(2, 8), (3, 5), (8, 1)])
+def test_row_tiling_is_bit_identical(rtmi, world, block):
+    """Frames sharded by pixel-row tiles reassemble to the single-GPU frame
+    bit for bit (RNG keyed by the global pixel index)."""
+    w, h, spp, depth = 40, 37, 2, 6
+    with rtmi.Renderer(0) as r:
+        rtmi.cornell_box1(r, w, h)
+        full = r.render(w, h, spp, depth)
+        tiles = np.zeros_like(full)
+        seg = 0
+        for rank in range(world):
+            part = r.render(w, h, spp, depth, row_block=block, row_rank=rank, row_world=world)
+            rows = rtmi.owned_row_ids(h, block, rank, world)
+            assert part.shape[0] == len(rows)
+            tiles[rows] = part
+            seg += r.stats()["segments"]
+        r.render(w, h, spp, depth)
+        assert seg == r.stats()["segments"]
+    assert np.array_equal(full, tiles)
+
+
+def test_zero_depth_is_black(rtmi):
+    with rtmi.Renderer(0) as r:
+        rtmi.cornell_box1(r, 16, 16)
+        img = r.render(16, 16, 2, 0)
+        assert r.stats()["segments"] == 0
+    assert not img.any()
+
+
+def test_progressive_accumulation_matches_single_pass(rtmi):
+    """Realtime mode (spp batches with sample_offset, Canvas running mean) equals
+    one pass at the total spp up to float summation order."""
+    from raytracingthenextweekcuda_amd.canvas import Canvas
+
+    w = h = 32
+    with rtmi.Renderer(0) as r:
+        rtmi.cornell_box1(r, w, h)
+        one = r.render(w, h, 8, 6)
+        cv = Canvas(w, h)
+        for k in range(4):
+            cv.accumulate(r.render(w, h, 2, 6, sample_offset=2 * k), 2)
+    assert np.max(np.abs(cv.mean() - one)) <= 1e-5
+
+
+def test_render_errors(rtmi):
+    from raytracingthenextweekcuda_amd._lib import RTError
+
+    with rtmi.Renderer(0) as r:
+        with pytest.raises(RTError, match="RT_ERR_STATE"):
+            r.render(8, 8, 1, 1)
+        rtmi.cornell_box1(r, 8, 8)
+        with pytest.raises(RTError, match="RT_ERR_INVALID"):
+            r.render(1, 8, 1, 1)
+        with pytest.raises(RTError, match="RT_ERR_INVALID"):
+            r.render(8, 8, 0, 1)
+        with pytest.raises(RTError, match="RT_ERR_INVALID"):
+            r.render(8, 8, 1, 1, row_rank=2, row_world=2)
+
+
+def test_render_into_torch_buffer(rtmi):
+    """rt_render_device writes into a caller-owned HBM buffer on a torch stream."""
+    torch = pytest.importorskip("torch")
+    w = h = 24
+    with rtmi.Renderer(0) as r:
+        rtmi.cornell_box1(r, w, h)
+        host = r.render(w, h, 2, 4)
+        buf = torch.empty((h, w, 3), dtype=torch.float32, device="cuda:0")
+        s = torch.cuda.Stream()
+        r.render_device(r.params(w, h, 2, 4), buf.data_ptr(), s.cuda_stream)
+        s.synchronize()
+        st = r.stats()
+    assert st["kernel_ms"] > 0
+    assert np.array_equal(buf.cpu().numpy(), host)
