@@ -64,6 +64,13 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: if torch (which bundles its own
+    # libamdhip64) is importable, load it first so librtmi.so binds to the
+    # already-loaded runtime instead of a second copy from /opt/rocm.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"librtmi.so not found at {LIB_PATH}: build it with __graft_entry__.build() "
