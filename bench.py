@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--spp", type=int, default=128)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--row-block", type=int, default=8)
+    ap.add_argument("--lanes", type=int, default=0, help="lanes per pixel (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-spp", type=int, default=32)
     return ap.parse_args()
@@ -112,7 +113,7 @@ def main():
     max_rows = max(rtmi.owned_rows(H, block, k, world) for k in range(world))
     out = torch.zeros((max_rows, W, 3), dtype=torch.float32, device="cuda")
     gather = [torch.empty_like(out) for _ in range(world)] if (rank == 0 and world > 1) else None
-    params = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, world)
+    params = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, world, args.lanes)
     stream = torch.cuda.current_stream()
 
     def step():
@@ -188,7 +189,7 @@ def main():
                 "workload": workload,
                 "scene": "CornellBox1 (6 planes + 2 cube_small.obj meshes, 24 triangles)",
                 "width": W, "height": H, "spp": args.spp, "depth": args.depth,
-                "row_block": block, "parallelism": f"row-tiles x{world} + RCCL gather" if world > 1 else "single GPU",
+                "row_block": block, "lanes_per_pixel": int(st["lanes_per_pixel"]), "parallelism": f"row-tiles x{world} + RCCL gather" if world > 1 else "single GPU",
                 "segments_per_frame": int(segs / K),
                 "msamples_per_s": round(W * H * args.spp / (dt / K) / 1e6, 3),
             },

@@ -60,6 +60,10 @@ typedef struct rt_render_params {
     int32_t row_block;      /* rows per tile block (>= 1) */
     int32_t row_rank;       /* this shard's rank */
     int32_t row_world;      /* number of shards (>= 1) */
+    int32_t lanes_per_pixel;/* lanes that split one pixel's samples: 0 = auto, or a
+                               power of two <= 64. Partial sums are combined in a
+                               fixed order, so results are deterministic for a
+                               given value; 1 = the reference's sequential sum. */
 } rt_render_params;
 
 typedef struct rt_render_stats {
@@ -70,6 +74,7 @@ typedef struct rt_render_stats {
     uint64_t box_tests;     /* mesh bounding boxes tested */
     double kernel_ms;       /* duration of the render kernel (hipEvent) */
     uint32_t overflow;      /* 1 if any lane overflowed the traversal stack */
+    uint32_t lanes_per_pixel; /* lane layout used by the last render */
 } rt_render_stats;
 
 /* ---- context (replaces initialize()/cleanup(), main.cu:555-936) ---- */

@@ -53,7 +53,7 @@ def lib():
         L.orc_length.argtypes = [fp]
         L.orc_length.restype = C.c_float
         L.orc_render.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_uint32,
-                                 C.c_int, C.c_int, C.c_int, C.c_int, fp, C.POINTER(C.c_uint64)]
+                                 C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, fp, C.POINTER(C.c_uint64)]
         L.orc_philox.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.orc_uniforms.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, fp]
         L.orc_trace.argtypes = [vp, fp, fp, C.c_float, fp, fp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
@@ -147,12 +147,12 @@ class OracleScene:
         return float(t.value), tuple(n), bool(front.value), int(mat.value)
 
     def render(self, width, height, spp, depth, seed=1984, sample_offset=0, row_block=1,
-               row_rank=0, row_world=1, threads=0):
+               row_rank=0, row_world=1, threads=0, lanes_per_pixel=1):
         rows = owned_rows(height, row_block, row_rank, row_world)
         out = np.zeros((rows, width, 3), np.float32)
         stats = (C.c_uint64 * 2)()
         rc = self.L.orc_render(self.h, width, height, spp, depth, seed, sample_offset, row_block,
-                               row_rank, row_world, threads,
+                               row_rank, row_world, lanes_per_pixel, threads,
                                out.ctypes.data_as(C.POINTER(C.c_float)), stats)
         if rc != 0:
             raise RuntimeError(f"orc_render failed with {rc}")

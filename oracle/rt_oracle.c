@@ -768,10 +768,11 @@ static int owned_rows(int h, int blk, int rank, int world) {
  * out: owned_rows * width * 3 floats, mean radiance (color / spp).
  * stats (may be NULL): [0] segments, [1] triangle tests. */
 int orc_render(const Scene* s, int width, int height, int spp, int bounces, uint32_t seed,
-               uint32_t sample_offset, int row_block, int row_rank, int row_world, int threads,
-               float* out, uint64_t* stats) {
+               uint32_t sample_offset, int row_block, int row_rank, int row_world,
+               int lanes_per_pixel, int threads, float* out, uint64_t* stats) {
+    const int S = lanes_per_pixel;
     if (!s->has_camera || width < 2 || height < 2 || spp < 1 || bounces < 0 || row_block < 1 ||
-        row_world < 1 || row_rank < 0 || row_rank >= row_world)
+        row_world < 1 || row_rank < 0 || row_rank >= row_world || S < 1 || S > 64 || (S & (S - 1)))
         return 1;
     for (int i = 0; i < s->n_objs; ++i) {
         const Object* o = &s->objs[i];
@@ -789,16 +790,24 @@ int orc_render(const Scene* s, int width, int height, int spp, int bounces, uint
         int y = (lb * row_world + row_rank) * row_block + (lr - lb * row_block);
         for (int x = 0; x < width; ++x) {
             uint32_t pixel = (uint32_t)y * (uint32_t)width + (uint32_t)x;
+            /* renderKernel's `color += rayColor(...)` over samples in order. With
+             * S > 1 (the product's lanes_per_pixel) sub-stream c sums samples
+             * c, c+S, ... in order and the partials combine as ((p0+p1)+p2)+...;
+             * S = 1 is exactly the reference's sequential sum. */
             V3 color = v3(0.0f, 0.0f, 0.0f);
-            for (int i = 0; i < spp; ++i) {
-                RandState rs;
-                rand_init(&rs, seed, pixel, sample_offset + (uint32_t)i);
-                float rx = curand_uniform_(&rs);
-                float ry = curand_uniform_(&rs);
-                float dx = ((float)x + rx) / (float)(width - 1);
-                float dy = ((float)y + ry) / (float)(height - 1);
-                Ray ray = camera_get_ray(s, dx, dy, &rs);
-                color = vadd(color, ray_color(s, ray, bounces, &rs, &segs, &tris));
+            for (int c = 0; c < S; ++c) {
+                V3 part = v3(0.0f, 0.0f, 0.0f);
+                for (int i = c; i < spp; i += S) {
+                    RandState rs;
+                    rand_init(&rs, seed, pixel, sample_offset + (uint32_t)i);
+                    float rx = curand_uniform_(&rs);
+                    float ry = curand_uniform_(&rs);
+                    float dx = ((float)x + rx) / (float)(width - 1);
+                    float dy = ((float)y + ry) / (float)(height - 1);
+                    Ray ray = camera_get_ray(s, dx, dy, &rs);
+                    part = vadd(part, ray_color(s, ray, bounces, &rs, &segs, &tris));
+                }
+                color = c == 0 ? part : vadd(color, part);
             }
             V3 m = vdiv(color, (float)spp);
             float* o = out + ((size_t)lr * width + x) * 3;

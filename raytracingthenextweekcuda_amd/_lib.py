@@ -40,6 +40,7 @@ class RenderParams(C.Structure):
         ("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32),
         ("max_depth", C.c_int32), ("seed", C.c_uint32), ("sample_offset", C.c_uint32),
         ("row_block", C.c_int32), ("row_rank", C.c_int32), ("row_world", C.c_int32),
+        ("lanes_per_pixel", C.c_int32),
     ]
 
 
@@ -47,7 +48,7 @@ class RenderStats(C.Structure):
     _fields_ = [
         ("segments", C.c_uint64), ("samples", C.c_uint64), ("node_visits", C.c_uint64),
         ("tri_tests", C.c_uint64), ("box_tests", C.c_uint64), ("kernel_ms", C.c_double),
-        ("overflow", C.c_uint32),
+        ("overflow", C.c_uint32), ("lanes_per_pixel", C.c_uint32),
     ]
 
 

@@ -381,6 +381,10 @@ static rt_status validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch
     L.row_rank = p->row_rank;
     L.row_world = p->row_world;
     L.local_rows = rt::owned_rows(p->height, p->row_block, p->row_rank, p->row_world);
+    const int32_t s = p->lanes_per_pixel;
+    if (s < 0 || s > 64 || (s & (s - 1)) != 0)
+        return fail(c, RT_ERR_INVALID, "lanes_per_pixel must be 0 (auto) or a power of two <= 64");
+    rt::choose_layout(L, s);
     return RT_OK;
 }
 
@@ -399,6 +403,7 @@ rt_status rt_render_device(rt_ctx* c, const rt_render_params* p, float* out, voi
     RT_HIP(c, hipEventRecord(c->ev1, st));
     c->last = rt_render_stats{};
     c->last.samples = (uint64_t)L.local_rows * (uint64_t)L.width * (uint64_t)L.spp;
+    c->last.lanes_per_pixel = (uint32_t)L.lanes_per_pixel;
     c->stats_pending = true;
     return RT_OK;
 }

@@ -14,7 +14,25 @@ struct RenderLaunch {
     uint32_t seed, sample_offset;
     int32_t row_block, row_rank, row_world;
     int32_t local_rows;  // rows owned by this shard (output has local_rows * width pixels)
+    int32_t lanes_per_pixel;  // S: power of two in [1, 64]
+    int32_t tile_w, tile_h;   // per-wave pixel tile, tile_w * tile_h = 64 / S
 };
+
+// Lane-layout choice: S = lanes_per_pixel (0 = auto). Auto raises S (power of
+// two, <= spp, <= 16) until the launch has >= 2^19 lanes (8192 waves, 8 per
+// SIMD on 256 CUs x 4 SIMDs) so small shards still fill the chip.
+inline void choose_layout(RenderLaunch& L, int32_t requested) {
+    int32_t s = requested;
+    if (s <= 0) {
+        s = 1;
+        const int64_t px = (int64_t)L.local_rows * L.width;
+        while (s < 16 && 2 * s <= L.spp && px * s < (int64_t(1) << 19)) s *= 2;
+    }
+    L.lanes_per_pixel = s;
+    const int32_t p = 64 / s;
+    L.tile_w = p >= 8 ? 8 : p;
+    L.tile_h = p / L.tile_w;
+}
 
 // counters[0] = segments, [1] = triangle tests, [2] = mesh-box tests,
 // [3] = BVH node visits, [4] = traversal overflow flag.

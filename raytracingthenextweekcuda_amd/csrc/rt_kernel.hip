@@ -86,6 +86,54 @@ __device__ __forceinline__ v3 moving_center(const float* f, float time) {
     return add(c0, scale(sub(c1, c0), (time - f[6]) / (f[7] - f[6])));
 }
 
+// In-rectangle test of Plane::hit for the plane's orientation.
+__device__ __forceinline__ bool plane_in_range(v3 p, const float* f, uint32_t orient) {
+    if (orient == 0u)
+        return (p.x > f[0] - f[6]) && (p.x < f[0] + f[6]) && (p.y > f[1] - f[7]) && (p.y < f[1] + f[7]);
+    if (orient == 1u)
+        return (p.y > f[1] - f[7]) && (p.y < f[1] + f[7]) && (p.z > f[2] - f[8]) && (p.z < f[2] + f[8]);
+    return (p.x > f[0] - f[6]) && (p.x < f[0] + f[6]) && (p.z > f[2] - f[8]) && (p.z < f[2] + f[8]);
+}
+
+// Relative slack that bounds the error of the screening arithmetic: v_rcp_f32
+// is within 1 ulp, each further rounding adds 0.5 ulp, so screened values are
+// within ~4 ulp (4.8e-7 relative) of the exact ones; 1e-5 leaves > 20x room.
+constexpr float kScreen = 1e-5f;
+
+// True only if the exact Plane::hit test is certain to fail.
+__device__ __forceinline__ bool plane_surely_missed(float num, float den, v3 o, v3 d, v3 pos,
+                                                    const float* f, uint32_t orient, float tmax) {
+    const float tq = num * __builtin_amdgcn_rcpf(den);
+    const float mt = fabsf(tq) * kScreen;
+    if (tq + mt < kTMin || tq - mt >= tmax) return true;
+    const v3 pq = add(o, scale(d, tq));
+    // |p - pq| <= |d| |t| 4.8e-7 + rounding of p: covered by slack on |d||tq| and |pq|.
+    auto out = [&](float pa, float da, float lo, float hi) {
+        const float m = (fabsf(da) * fabsf(tq) + fabsf(pa)) * kScreen + 1e-30f;
+        return (pa + m <= lo) || (pa - m >= hi);
+    };
+    if (orient == 0u)
+        return out(pq.x, d.x, f[0] - f[6], f[0] + f[6]) || out(pq.y, d.y, f[1] - f[7], f[1] + f[7]);
+    if (orient == 1u)
+        return out(pq.y, d.y, f[1] - f[7], f[1] + f[7]) || out(pq.z, d.z, f[2] - f[8], f[2] + f[8]);
+    return out(pq.x, d.x, f[0] - f[6], f[0] + f[6]) || out(pq.z, d.z, f[2] - f[8], f[2] + f[8]);
+}
+
+// True only if the exact TriangleMesh::hit acceptance test is certain to fail.
+// NaN/inf screened values compare false and fall through to the exact path.
+__device__ __forceinline__ bool tri_surely_missed(float det, float n_t, float n_b1, float n_b2,
+                                                  float tmax) {
+    if (!(fabsf(det) > 1e-30f)) return false;
+    const float cq = __builtin_amdgcn_rcpf(det);
+    const float tq = cq * n_t, b1 = cq * n_b1, b2 = cq * n_b2;
+    const float mt = fabsf(tq) * kScreen;
+    if (tq + mt < kTMin || tq - mt >= tmax) return true;
+    const float m1 = fabsf(b1) * kScreen, m2 = fabsf(b2) * kScreen;
+    if (b1 + m1 < kFltEpsilon || b2 + m2 < kFltEpsilon) return true;
+    const float r = 1.0f - b1 - b2;
+    return r + (m1 + m2 + 4e-7f) < kFltEpsilon;
+}
+
 struct Hit {
     float t;
     int32_t obj;   // object table index of the closest hit (-1: none)
@@ -108,24 +156,18 @@ __device__ __forceinline__ Hit closest_hit(const ObjRec* __restrict__ objs, int 
             float den = dot(n, d);
             bool proceed = objs[i].u1 ? (fabsf(den) > kTMin) : (den > kTMin);
             if (proceed) {
-                v3 po = sub(v3{f[0], f[1], f[2]}, o);
-                float t = dot(po, n) / den;
-                v3 p = add(o, scale(d, t));
-                bool in;
-                const uint32_t orient = objs[i].u0;
-                if (orient == 0u) {
-                    in = (p.x > f[0] - f[6]) && (p.x < f[0] + f[6]) && (p.y > f[1] - f[7]) &&
-                         (p.y < f[1] + f[7]);
-                } else if (orient == 1u) {
-                    in = (p.y > f[1] - f[7]) && (p.y < f[1] + f[7]) && (p.z > f[2] - f[8]) &&
-                         (p.z < f[2] + f[8]);
-                } else {
-                    in = (p.x > f[0] - f[6]) && (p.x < f[0] + f[6]) && (p.z > f[2] - f[8]) &&
-                         (p.z < f[2] + f[8]);
-                }
-                if ((t >= kTMin) && (t < h.t) && in) {
-                    h.t = t;
-                    h.obj = i;
+                v3 pos{f[0], f[1], f[2]};
+                float num = dot(sub(pos, o), n);
+                // Screening with v_rcp_f32 (<= 1 ulp): only lanes that are not
+                // clearly rejected evaluate the IEEE division, so every accepted
+                // hit and every close call is decided by the exact arithmetic.
+                if (!plane_surely_missed(num, den, o, d, pos, f, objs[i].u0, h.t)) {
+                    float t = num / den;
+                    v3 p = add(o, scale(d, t));
+                    if ((t >= kTMin) && (t < h.t) && plane_in_range(p, f, objs[i].u0)) {
+                        h.t = t;
+                        h.obj = i;
+                    }
                 }
             }
         } else if (type == kObjSphere) {
@@ -155,10 +197,13 @@ __device__ __forceinline__ Hit closest_hit(const ObjRec* __restrict__ objs, int 
                     v3 s = sub(o, v3{tr.v0x, tr.v0y, tr.v0z});
                     v3 s1 = cross(d, e2);
                     v3 s2 = cross(s, e1);
-                    float coef = 1.0f / dot(s1, e1);
-                    float t = coef * dot(s2, e2);
-                    float b1 = coef * dot(s1, s);
-                    float b2 = coef * dot(s2, d);
+                    const float det = dot(s1, e1);
+                    const float n_t = dot(s2, e2), n_b1 = dot(s1, s), n_b2 = dot(s2, d);
+                    if (tri_surely_missed(det, n_t, n_b1, n_b2, h.t)) continue;
+                    float coef = 1.0f / det;
+                    float t = coef * n_t;
+                    float b1 = coef * n_b1;
+                    float b2 = coef * n_b2;
                     if (((t >= kFltEpsilon) && ((t >= kTMin) && (t < h.t))) &&
                         (b1 >= kFltEpsilon) && (b2 >= kFltEpsilon) &&
                         ((1.0f - b1 - b2) >= kFltEpsilon)) {
@@ -186,8 +231,15 @@ __global__ __launch_bounds__(256) void render_kernel(
     float* __restrict__ out, unsigned long long* __restrict__ counters) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int px = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int lrow = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    // Lane layout: S = lanes_per_pixel adjacent lanes share one pixel and split
+    // its samples (sub-lane c takes samples c, c+S, c+2S, ...). A wave covers
+    // 64/S pixels as a tw x th tile; a 4-wave workgroup covers 2tw x 2th.
+    const int S = L.lanes_per_pixel;
+    const int c = lane & (S - 1);
+    const int pix = lane / S;
+    const int tw = L.tile_w, th = L.tile_h;
+    const int px = blockIdx.x * (2 * tw) + (wave & 1) * tw + (pix % tw);
+    const int lrow = blockIdx.y * (2 * th) + (wave >> 1) * th + (pix / tw);
     // Row tiling: local row -> global row (y = 0 is the bottom row).
     const int lb = lrow / L.row_block;
     const int y = (lb * L.row_world + L.row_rank) * L.row_block + (lrow - lb * L.row_block);
@@ -196,8 +248,8 @@ __global__ __launch_bounds__(256) void render_kernel(
 
     v3 sum{0.0f, 0.0f, 0.0f};
     uint32_t segs = 0, tri_tests = 0, box_tests = 0;
-    int s = 0;
-    bool alive = valid && L.spp > 0;
+    int s = c;
+    bool alive = valid && s < L.spp;
     bool need_cam = true;
     int depth = 0;
     Ray ray{};
@@ -228,7 +280,8 @@ __global__ __launch_bounds__(256) void render_kernel(
             need_cam = false;
             if (L.max_depth <= 0) {  // rayColor with BOUNCES = 0 returns black
                 need_cam = true;
-                if (++s == L.spp) alive = false;
+                s += S;
+                if (s >= L.spp) alive = false;
                 continue;
             }
         }
@@ -322,11 +375,23 @@ __global__ __launch_bounds__(256) void render_kernel(
         if (done) {
             sum = add(sum, contrib);
             need_cam = true;
-            if (++s == L.spp) alive = false;
+            s += S;
+            if (s >= L.spp) alive = false;
         }
     }
 
-    if (valid) {
+    // Fixed-order combination of the S partial sums: ((p0 + p1) + p2) + ...
+    if (S > 1) {
+        const int base = lane - c;
+        v3 acc = sum;
+        for (int j = 1; j < S; ++j) {
+            v3 pj{__shfl(sum.x, base + j, 64), __shfl(sum.y, base + j, 64), __shfl(sum.z, base + j, 64)};
+            acc = add(acc, pj);
+        }
+        sum = acc;
+    }
+
+    if (valid && c == 0) {
         const float fs = (float)L.spp;
         const size_t o = ((size_t)lrow * (size_t)L.width + (size_t)px) * 3;
         out[o + 0] = sum.x / fs;
@@ -347,7 +412,8 @@ __global__ __launch_bounds__(256) void render_kernel(
 hipError_t launch_render(const KernelScene& sc, const CamRec& cam, const RenderLaunch& L,
                          float* out, unsigned long long* counters, hipStream_t stream) {
     dim3 block(256);
-    dim3 grid((L.width + 15) / 16, (L.local_rows + 15) / 16);
+    dim3 grid((L.width + 2 * L.tile_w - 1) / (2 * L.tile_w),
+              (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
     hipLaunchKernelGGL(render_kernel, grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
                        sc.n_objs, cam, L, out, counters);

@@ -186,14 +186,17 @@ class Renderer:
     # ---- render ----
     @staticmethod
     def params(width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,
-               row_rank=0, row_world=1) -> RenderParams:
+               row_rank=0, row_world=1, lanes_per_pixel=1) -> RenderParams:
         return RenderParams(width, height, spp, max_depth, seed, sample_offset, row_block,
-                            row_rank, row_world)
+                            row_rank, row_world, lanes_per_pixel)
 
     def render(self, width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,
-               row_rank=0, row_world=1) -> np.ndarray:
-        """Mean radiance of the owned rows, shape (rows, width, 3), y = 0 bottom."""
-        p = self.params(width, height, spp, max_depth, seed, sample_offset, row_block, row_rank, row_world)
+               row_rank=0, row_world=1, lanes_per_pixel=1) -> np.ndarray:
+        """Mean radiance of the owned rows, shape (rows, width, 3), y = 0 bottom.
+        lanes_per_pixel=1 keeps the reference's sequential per-pixel sample sum;
+        0 lets the library pick a lane layout that fills the GPU."""
+        p = self.params(width, height, spp, max_depth, seed, sample_offset, row_block, row_rank,
+                        row_world, lanes_per_pixel)
         rows = owned_rows(height, row_block, row_rank, row_world)
         out = np.zeros((rows, width, 3), np.float32)
         self._check(self.L.rt_render(self.ctx, C.byref(p), out.ctypes.data_as(C.POINTER(C.c_float))))

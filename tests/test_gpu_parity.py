@@ -149,3 +149,29 @@ def test_render_into_torch_buffer(rtmi):
         st = r.stats()
     assert st["kernel_ms"] > 0
     assert np.array_equal(buf.cpu().numpy(), host)
+
+
+@pytest.mark.parametrize("lanes", [2, 4, 16, 64])
+def test_lanes_per_pixel_parity(rtmi, lanes):
+    """Samples of one pixel split over `lanes` lanes, partial sums combined in a
+    fixed order: bit-exact against the restatement using the same order, and
+    within float summation-order noise of the sequential (reference) order."""
+    w, h, spp, depth = 40, 24, 64, 6
+    with rtmi.Renderer(0) as r:
+        rtmi.cornell_box1(r, w, h)
+        img = r.render(w, h, spp, depth, lanes_per_pixel=lanes)
+        st = r.stats()
+        assert st["lanes_per_pixel"] == lanes
+    sc = _oracle_yaml("cornellbox1.yaml", w, h)
+    ref, ref_st = sc.render(w, h, spp, depth, lanes_per_pixel=lanes)
+    _check(img, ref, st, ref_st, f"lanes{lanes}")
+    assert np.array_equal(img, ref)
+    seq, _ = sc.render(w, h, spp, depth)
+    assert np.max(np.abs(img - seq)) <= 1e-5
+
+
+def test_auto_lane_layout_fills_small_shards(rtmi):
+    with rtmi.Renderer(0) as r:
+        rtmi.cornell_box1(r, 64, 64)
+        r.render(64, 64, 32, 4, lanes_per_pixel=0)
+        assert r.stats()["lanes_per_pixel"] == 16
