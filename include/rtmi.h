@@ -120,6 +120,19 @@ int32_t rt_mesh_triangle_count(const rt_ctx* ctx, int32_t index);
 /* Copies the world-space vertices (9 floats/tri) of mesh slot `index`. */
 rt_status rt_mesh_vertices(const rt_ctx* ctx, int32_t index, float* out, int32_t max_tris);
 
+/* PLY mesh with loadObject + processTriangleData semantics (Loader.cpp:207-319,
+ * 98-205): centred, scaled so max |coord| = max_coord (reference 1.0,
+ * MaxCoordAfterRescale Loader.cpp:58), then offset. The mesh is accelerated
+ * by the reference's binned-SAH BVH (BVH.cpp:94-497). */
+rt_status rt_mesh_ply(rt_ctx* ctx, int32_t index, const char* path, const float offset[3],
+                      float max_coord, int32_t material);
+/* The reference's `.bvh` cache image for a PLY file (BVH.cpp:500-554 with
+ * UpdateBoundingVolumeHierarchy's writer, 537-540): u32 node count, u32 index
+ * count, 32 B CacheFriendlyBVHNode[], int32 triangle indices. Writes up to
+ * `capacity` bytes to `out` (may be NULL) and the full size to *size. */
+rt_status rt_ply_bvh_image(const char* path, const float offset[3], float max_coord,
+                           uint8_t* out, int64_t capacity, int64_t* size);
+
 /* ---- camera (Camera.h:19-34 initialize, 86-103 updateViewMatrix) ---- */
 rt_status rt_camera(rt_ctx* ctx, const float eye[3], const float center[3], const float up[3],
                     float aspect_ratio, float fov, float aperture, float focus_distance,

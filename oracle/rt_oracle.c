@@ -29,10 +29,11 @@
  *   Canvas::gamma ................... Canvas.h:198-200
  *
  * Deliberate, documented deviations from the reference:
- *  1. cuRAND XORWOW is replaced by Philox4x32-10 (key = (seed, pixel),
- *     counter = (draw/4, sample, 0, 0)), mapped to (0,1] with curand's
- *     x*2^-32 + 2^-33. cuRAND itself is not in this image: parity with the
- *     reference's random stream is "unpinned" by construction.
+ *  1. cuRAND XORWOW is replaced by a counter-based stream per (pixel, sample):
+ *     Philox4x32-10 (key = (seed, pixel), counter = (sample, 0, 0, 0)) seeds
+ *     xoshiro128** 1.1; uniforms use curand's (0,1] mapping x*2^-32 + 2^-33.
+ *     cuRAND itself is not in this image: parity with the reference's random
+ *     stream is "unpinned" by construction.
  *  2. randomInUnitDisk draws x before y (the reference's order is unspecified).
  *  3. pow(x, 5) in Schlick's approximation is ((x*x)*(x*x))*x (the reference
  *     used --use_fast_math __powf, which is not reproducible).
@@ -103,26 +104,37 @@ static void philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-/* Stand-in for curandState: a (seed, pixel, sample) stream. */
+/* Stand-in for curandState: one stream per (seed, pixel, sample).
+ * Philox4x32-10(key = (seed, pixel), counter = (sample, 0, 0, 0)) seeds a
+ * xoshiro128** 1.1 generator (Blackman & Vigna, 2018) for the sample's draws. */
 typedef struct {
-    uint32_t key[2];
-    uint32_t sample;
-    uint32_t n;
-    uint32_t block[4];
+    uint32_t s[4];
 } RandState;
 
-static void rand_init(RandState* s, uint32_t seed, uint32_t pixel, uint32_t sample) {
-    s->key[0] = seed; s->key[1] = pixel; s->sample = sample; s->n = 0;
+static uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+
+static void rand_init(RandState* st, uint32_t seed, uint32_t pixel, uint32_t sample) {
+    uint32_t ctr[4] = {sample, 0u, 0u, 0u}, key[2] = {seed, pixel};
+    philox(ctr, key, st->s);
+    if ((st->s[0] | st->s[1] | st->s[2] | st->s[3]) == 0u) st->s[0] = 0x9E3779B9u;
+}
+
+static uint32_t xoshiro128ss(RandState* st) {
+    uint32_t* s = st->s;
+    const uint32_t result = rotl32(s[1] * 5u, 7) * 9u;
+    const uint32_t t = s[1] << 9;
+    s[2] ^= s[0];
+    s[3] ^= s[1];
+    s[1] ^= s[2];
+    s[0] ^= s[3];
+    s[2] ^= t;
+    s[3] = rotl32(s[3], 11);
+    return result;
 }
 
 /* curand_uniform: (0, 1] (curand's _curand_uniform mapping). */
 static float curand_uniform_(RandState* s) {
-    if ((s->n & 3u) == 0u) {
-        uint32_t ctr[4] = {s->n >> 2, s->sample, 0u, 0u};
-        philox(ctr, s->key, s->block);
-    }
-    uint32_t x = s->block[s->n & 3u];
-    s->n++;
+    uint32_t x = xoshiro128ss(s);
     const float inv = 2.3283064e-10f;
     return (float)x * inv + (inv / 2.0f);
 }

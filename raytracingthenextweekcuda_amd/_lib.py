@@ -12,6 +12,9 @@ import subprocess
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "librtmi.so")
+# Experiments only (A/B builds of the same sources, tools/variants.sh).
+if os.environ.get("RTMI_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["RTMI_LIB"])
 
 RT_OK = 0
 STATUS_NAMES = {
@@ -25,6 +28,7 @@ EXPORTS = [
     "rt_material_lambertian", "rt_material_metal", "rt_material_dielectric",
     "rt_material_emission", "rt_material_defined", "rt_sphere", "rt_moving_sphere", "rt_plane",
     "rt_cube", "rt_mesh", "rt_mesh_obj", "rt_mesh_triangle_count", "rt_mesh_vertices",
+    "rt_mesh_ply", "rt_ply_bvh_image",
     "rt_camera", "rt_commit", "rt_scene_info", "rt_render", "rt_render_device", "rt_sync_stats", "rt_gamma_u8",
 ]
 
@@ -98,6 +102,9 @@ def lib():
     L.rt_mesh_obj.argtypes = [vp, i32, C.c_char_p, fp, fp, fp, i32]
     L.rt_mesh_triangle_count.argtypes = [vp, i32]
     L.rt_mesh_vertices.argtypes = [vp, i32, fp, i32]
+    L.rt_mesh_ply.argtypes = [vp, i32, C.c_char_p, fp, C.c_float, i32]
+    L.rt_ply_bvh_image.argtypes = [C.c_char_p, fp, C.c_float, C.POINTER(C.c_uint8), C.c_int64,
+                                   C.POINTER(C.c_int64)]
     L.rt_camera.argtypes = [vp, fp, fp, fp] + [C.c_float] * 6
     L.rt_commit.argtypes = [vp]
     L.rt_scene_info.argtypes = [vp, C.POINTER(C.c_int32)]

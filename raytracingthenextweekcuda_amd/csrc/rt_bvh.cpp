@@ -1,0 +1,269 @@
+// rt_bvh.cpp — see rt_bvh.h. Compiled with -ffp-contract=off: the split search
+// must round exactly like the reference build to reproduce its trees.
+#include "rt_bvh.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <fstream>
+#include <memory>
+
+namespace rt {
+
+namespace {
+
+// min3 / max3 (LinearAlgebra.h:48-49): component-wise with a strict compare.
+inline v3 min3v(v3 a, v3 b) {
+    return v3{a.x < b.x ? a.x : b.x, a.y < b.y ? a.y : b.y, a.z < b.z ? a.z : b.z};
+}
+inline v3 max3v(v3 a, v3 b) {
+    return v3{a.x > b.x ? a.x : b.x, a.y > b.y ? a.y : b.y, a.z > b.z ? a.z : b.z};
+}
+inline float axis_of(v3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+
+struct Entry {  // BBoxTmp (BVH.cpp:61-76)
+    v3 bottom, top, center;
+    int32_t tri;
+};
+
+struct BNode {
+    v3 bottom{0, 0, 0}, top{0, 0, 0};
+    int left = -1, right = -1;    // inner node children (pool indices)
+    std::vector<int32_t> tris;    // leaf triangle list (work order)
+    bool leaf() const { return left < 0; }
+};
+
+struct Builder {
+    std::vector<BNode> pool;
+
+    int make_leaf(const std::vector<Entry>& work) {
+        pool.emplace_back();
+        for (const Entry& e : work) pool.back().tris.push_back(e.tri);
+        return (int)pool.size() - 1;
+    }
+
+    // Recurse (BVH.cpp:94-333).
+    int recurse(std::vector<Entry>& work, int depth) {
+        if (work.size() < 4) return make_leaf(work);
+
+        v3 bottom{FLT_MAX, FLT_MAX, FLT_MAX}, top{-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (const Entry& v : work) {
+            bottom = min3v(bottom, v.bottom);
+            top = max3v(top, v.top);
+        }
+        const float side1 = top.x - bottom.x, side2 = top.y - bottom.y, side3 = top.z - bottom.z;
+        float min_cost = (float)work.size() * (side1 * side2 + side2 * side3 + side3 * side1);
+        float best_split = FLT_MAX;
+        int best_axis = -1;
+
+        for (int axis = 0; axis < 3; ++axis) {
+            const float start = axis_of(bottom, axis), stop = axis_of(top, axis);
+            // fabsf(stop - start) < 1e-4 compares in double (BVH.cpp:164).
+            if ((double)fabsf(stop - start) < 1e-4) continue;
+            const float step = (stop - start) / (1024.0f / ((float)depth + 1.0f));
+            for (float split = start + step; split < stop - step; split += step) {
+                v3 lb{FLT_MAX, FLT_MAX, FLT_MAX}, lt{-FLT_MAX, -FLT_MAX, -FLT_MAX};
+                v3 rb{FLT_MAX, FLT_MAX, FLT_MAX}, rtp{-FLT_MAX, -FLT_MAX, -FLT_MAX};
+                int nl = 0, nr = 0;
+                for (const Entry& v : work) {
+                    if (axis_of(v.center, axis) < split) {
+                        lb = min3v(lb, v.bottom);
+                        lt = max3v(lt, v.top);
+                        ++nl;
+                    } else {
+                        rb = min3v(rb, v.bottom);
+                        rtp = max3v(rtp, v.top);
+                        ++nr;
+                    }
+                }
+                if (nl <= 1 || nr <= 1) continue;
+                const float l1 = lt.x - lb.x, l2 = lt.y - lb.y, l3 = lt.z - lb.z;
+                const float r1 = rtp.x - rb.x, r2 = rtp.y - rb.y, r3 = rtp.z - rb.z;
+                const float sl = l1 * l2 + l2 * l3 + l3 * l1;
+                const float sr = r1 * r2 + r2 * r3 + r3 * r1;
+                const float cost = sl * (float)nl + sr * (float)nr;
+                if (cost < min_cost) {
+                    min_cost = cost;
+                    best_split = split;
+                    best_axis = axis;
+                }
+            }
+        }
+        if (best_axis == -1) return make_leaf(work);
+
+        std::vector<Entry> left, right;
+        v3 lb{FLT_MAX, FLT_MAX, FLT_MAX}, lt{-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        v3 rb{FLT_MAX, FLT_MAX, FLT_MAX}, rtp{-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (const Entry& v : work) {
+            if (axis_of(v.center, best_axis) < best_split) {
+                left.push_back(v);
+                lb = min3v(lb, v.bottom);
+                lt = max3v(lt, v.top);
+            } else {
+                right.push_back(v);
+                rb = min3v(rb, v.bottom);
+                rtp = max3v(rtp, v.top);
+            }
+        }
+        work.clear();
+        work.shrink_to_fit();
+        pool.emplace_back();
+        const int me = (int)pool.size() - 1;
+        const int l = recurse(left, depth + 1);
+        pool[l].bottom = lb;
+        pool[l].top = lt;
+        const int r = recurse(right, depth + 1);
+        pool[r].bottom = rb;
+        pool[r].top = rtp;
+        pool[me].left = l;
+        pool[me].right = r;
+        return me;
+    }
+
+    // PopulateCacheFriendlyBVH (BVH.cpp:432-465): depth first, left first.
+    void populate(int n, uint32_t& idx_boxes, CFBvh& out, int depth) {
+        if (depth > out.max_depth) out.max_depth = depth;
+        const uint32_t cur = idx_boxes;
+        CFNode& c = out.nodes[cur];
+        const BNode& b = pool[n];
+        c.bottom[0] = b.bottom.x; c.bottom[1] = b.bottom.y; c.bottom[2] = b.bottom.z;
+        c.top[0] = b.top.x; c.top[1] = b.top.y; c.top[2] = b.top.z;
+        if (!b.leaf()) {
+            const uint32_t il = ++idx_boxes;
+            populate(b.left, idx_boxes, out, depth + 1);
+            const uint32_t ir = ++idx_boxes;
+            populate(b.right, idx_boxes, out, depth + 1);
+            out.nodes[cur].u0 = il;
+            out.nodes[cur].u1 = ir;
+        } else {
+            out.nodes[cur].u0 = 0x80000000u | (uint32_t)b.tris.size();
+            out.nodes[cur].u1 = (uint32_t)out.tri_index.size();
+            for (int32_t t : b.tris) out.tri_index.push_back(t);
+        }
+    }
+};
+
+}  // namespace
+
+std::string load_ply(const std::string& path, PlyMesh& out) {
+    std::ifstream in(path);
+    if (!in) return "cannot open PLY file: " + path;
+    out.vertices.clear();
+    out.indices.clear();
+    std::string line;
+    unsigned nv = 0, nf = 0;
+    bool inside = false;
+    while (std::getline(in, line)) {
+        if (!inside) {
+            if (line.compare(0, 14, "element vertex") == 0) {
+                nv = (unsigned)strtoul(line.c_str() + 14, nullptr, 10);
+            } else if (line.compare(0, 12, "element face") == 0) {
+                nf = (unsigned)strtoul(line.c_str() + 12, nullptr, 10);
+            } else if (line.compare(0, 10, "end_header") == 0) {
+                inside = true;
+                out.vertices.reserve(nv);
+                out.indices.reserve((size_t)nf * 3);
+            }
+        } else if (nv) {
+            --nv;
+            // str_in >> x >> y >> z (Loader.cpp:258-259): correctly rounded strtof.
+            const char* p = line.c_str();
+            char* e;
+            float x = strtof(p, &e);
+            float y = strtof(e, &e);
+            float z = strtof(e, &e);
+            out.vertices.push_back(v3{x, y, z});
+        } else if (nf) {
+            --nf;
+            // `dummy idx1 idx2 idx3` (Loader.cpp:276-277): only the first three
+            // indices of a face are used.
+            unsigned long v[4];
+            const char* p = line.c_str();
+            char* e;
+            int k = 0;
+            for (; k < 4; ++k) {
+                v[k] = strtoul(p, &e, 10);
+                if (e == p) break;
+                p = e;
+            }
+            if (k < 4) continue;  // malformed line: skipped like a failed `>>`
+            const size_t n = out.vertices.size();
+            if (v[1] >= n || v[2] >= n || v[3] >= n) return "PLY face index out of range in " + path;
+            out.indices.push_back((uint32_t)v[1]);
+            out.indices.push_back((uint32_t)v[2]);
+            out.indices.push_back((uint32_t)v[3]);
+        }
+    }
+    if (!inside) return "PLY header without end_header: " + path;
+    return "";
+}
+
+void process_ply_vertices(PlyMesh& m, v3 offset, float max_coord) {
+    v3 minp{FLT_MAX, FLT_MAX, FLT_MAX}, maxp{-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (size_t i = 0; i < m.indices.size(); i += 3) {
+        for (int k = 0; k < 3; ++k) minp = min3v(minp, m.vertices[m.indices[i + k]]);
+        for (int k = 0; k < 3; ++k) maxp = max3v(maxp, m.vertices[m.indices[i + k]]);
+    }
+    const v3 c{(maxp.x + minp.x) * 0.5f, (maxp.y + minp.y) * 0.5f, (maxp.z + minp.z) * 0.5f};
+    minp = sub(minp, c);
+    maxp = sub(maxp, c);
+    float maxi = 0.0f;  // std::max(maxi, (float)fabs(.)) keeps the first on ties
+    const float cand[6] = {fabsf(minp.x), fabsf(minp.y), fabsf(minp.z),
+                           fabsf(maxp.x), fabsf(maxp.y), fabsf(maxp.z)};
+    for (float f : cand) maxi = (maxi < f) ? f : maxi;
+    const float s = max_coord / maxi;
+    for (v3& v : m.vertices) {
+        v = sub(v, c);
+        v = scale(v, s);
+        v = add(v, offset);
+    }
+}
+
+void build_cf_bvh(const std::vector<v3>& vertices, const std::vector<uint32_t>& indices,
+                  CFBvh& out) {
+    // CreateBVH (BVH.cpp:335-392).
+    const size_t nt = indices.size() / 3;
+    std::vector<Entry> work;
+    work.reserve(nt);
+    v3 bottom{FLT_MAX, FLT_MAX, FLT_MAX}, top{-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (size_t j = 0; j < nt; ++j) {
+        Entry b;
+        b.tri = (int32_t)j;
+        b.bottom = v3{FLT_MAX, FLT_MAX, FLT_MAX};
+        b.top = v3{-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (int k = 0; k < 3; ++k) b.bottom = min3v(b.bottom, vertices[indices[3 * j + k]]);
+        for (int k = 0; k < 3; ++k) b.top = max3v(b.top, vertices[indices[3 * j + k]]);
+        bottom = min3v(bottom, b.bottom);
+        top = max3v(top, b.top);
+        b.center = scale(add(b.top, b.bottom), 0.5f);
+        work.push_back(b);
+    }
+    Builder B;
+    B.pool.reserve(nt);
+    const int root = B.recurse(work, 0);
+    B.pool[root].bottom = bottom;
+    B.pool[root].top = top;
+    // CreateCFBVH (BVH.cpp:467-497).
+    size_t nboxes = B.pool.size();
+    out.nodes.assign(nboxes, CFNode{});
+    out.tri_index.clear();
+    out.tri_index.reserve(nt);
+    out.max_depth = 0;
+    uint32_t idx = 0;
+    B.populate(root, idx, out, 0);
+}
+
+std::vector<uint8_t> bvh_image(const CFBvh& b) {
+    const uint32_t nn = (uint32_t)b.nodes.size(), ni = (uint32_t)b.tri_index.size();
+    std::vector<uint8_t> img(8 + (size_t)nn * sizeof(CFNode) + (size_t)ni * 4);
+    memcpy(img.data(), &nn, 4);
+    memcpy(img.data() + 4, &ni, 4);
+    memcpy(img.data() + 8, b.nodes.data(), (size_t)nn * sizeof(CFNode));
+    memcpy(img.data() + 8 + (size_t)nn * sizeof(CFNode), b.tri_index.data(), (size_t)ni * 4);
+    return img;
+}
+
+}  // namespace rt

@@ -1,0 +1,56 @@
+// rt_bvh.h — PLY ingestion and the binned-SAH BVH builder.
+//
+// Restates, for byte-exact agreement with the reference's `.bvh` cache files
+// (paths relative to RayTracingTheNextWeekCUDA/):
+//   loadObject (ASCII PLY) ............. Loader.cpp:207-319
+//   processTriangleData (centre/scale, Kuchkuda planes) Loader.cpp:98-205
+//   CreateBVH / Recurse (binned SAH) .... BVH.cpp:94-392
+//   CreateCFBVH / PopulateCacheFriendlyBVH (DFS, 32 B nodes) BVH.cpp:432-497
+//   .bvh cache image .................... BVH.cpp:537-540
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "rt_math.h"
+
+namespace rt {
+
+struct PlyMesh {
+    std::vector<v3> vertices;
+    std::vector<uint32_t> indices;  // 3 per triangle, as read (idx1, idx2, idx3)
+};
+
+// Loader.cpp:207-319 (ASCII "element vertex / element face / end_header").
+std::string load_ply(const std::string& path, PlyMesh& out);
+
+// processTriangleData (Loader.cpp:98-205) vertex transform: centre the
+// triangles' bounding box, scale so max |coord| = max_coord, add offset.
+void process_ply_vertices(PlyMesh& m, v3 offset, float max_coord);
+
+// CacheFriendlyBVHNode (BVH.h:46-67): bottom, top, {idxLeft, idxRight} or
+// {0x80000000 | count, startIndexInTriIndexList}.
+struct CFNode {
+    float bottom[3];
+    float top[3];
+    uint32_t u0;
+    uint32_t u1;
+};
+static_assert(sizeof(CFNode) == 32, "CFNode must be 32 B");
+
+struct CFBvh {
+    std::vector<CFNode> nodes;
+    std::vector<int32_t> tri_index;  // leaf triangle lists (indices into the mesh)
+    int max_depth = 0;
+};
+
+// CreateBVH + CreateCFBVH over triangles given by vertex index triples.
+void build_cf_bvh(const std::vector<v3>& vertices, const std::vector<uint32_t>& indices,
+                  CFBvh& out);
+
+// The `.bvh` cache image: u32 nodes, u32 indices, nodes, int32 indices.
+std::vector<uint8_t> bvh_image(const CFBvh& b);
+
+}  // namespace rt

@@ -9,9 +9,11 @@
 #include <math.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
+#include "rt_bvh.h"
 #include "rt_kernel.h"
 #include "rt_scene.h"
 
@@ -287,6 +289,39 @@ rt_status rt_mesh_obj(rt_ctx* c, int32_t index, const char* path, const float sc
                                              rt::v3{offset[0], offset[1], offset[2]}, verts);
     if (!e.empty()) return fail(c, RT_ERR_IO, e);
     return rt_mesh(c, index, verts.data(), (int32_t)(verts.size() / 9), material);
+}
+
+rt_status rt_mesh_ply(rt_ctx* c, int32_t index, const char* path, const float offset[3],
+                      float max_coord, int32_t material) {
+    if (!c) return RT_ERR_INVALID;
+    if (!path || !finite3(offset) || !isfinite(max_coord) || max_coord <= 0.0f)
+        return fail(c, RT_ERR_INVALID, "mesh_ply: bad arguments");
+    rt::PlyMesh m;
+    std::string e = rt::load_ply(path, m);
+    if (!e.empty()) return fail(c, RT_ERR_IO, e);
+    rt::process_ply_vertices(m, rt::v3{offset[0], offset[1], offset[2]}, max_coord);
+    std::vector<float> verts;
+    verts.reserve(m.indices.size() * 3);
+    for (uint32_t i : m.indices) {
+        verts.push_back(m.vertices[i].x);
+        verts.push_back(m.vertices[i].y);
+        verts.push_back(m.vertices[i].z);
+    }
+    return rt_mesh(c, index, verts.data(), (int32_t)(verts.size() / 9), material);
+}
+
+rt_status rt_ply_bvh_image(const char* path, const float offset[3], float max_coord,
+                           uint8_t* out, int64_t capacity, int64_t* size) {
+    if (!path || !finite3(offset) || !size || !(max_coord > 0.0f)) return RT_ERR_INVALID;
+    rt::PlyMesh m;
+    if (!rt::load_ply(path, m).empty()) return RT_ERR_IO;
+    rt::process_ply_vertices(m, rt::v3{offset[0], offset[1], offset[2]}, max_coord);
+    rt::CFBvh b;
+    rt::build_cf_bvh(m.vertices, m.indices, b);
+    std::vector<uint8_t> img = rt::bvh_image(b);
+    *size = (int64_t)img.size();
+    if (out && capacity > 0) memcpy(out, img.data(), (size_t)std::min<int64_t>(capacity, *size));
+    return RT_OK;
 }
 
 int32_t rt_mesh_triangle_count(const rt_ctx* c, int32_t index) {

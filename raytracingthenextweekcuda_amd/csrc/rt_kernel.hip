@@ -31,6 +31,10 @@ namespace {
 
 constexpr float kInf = __builtin_huge_valf();
 
+#ifndef RT_SCREEN
+#define RT_SCREEN 1  // rcp-screened plane/triangle tests (exact fallback)
+#endif
+
 struct Ray {
     v3 o, d;
     float time;
@@ -161,7 +165,7 @@ __device__ __forceinline__ Hit closest_hit(const ObjRec* __restrict__ objs, int 
                 // Screening with v_rcp_f32 (<= 1 ulp): only lanes that are not
                 // clearly rejected evaluate the IEEE division, so every accepted
                 // hit and every close call is decided by the exact arithmetic.
-                if (!plane_surely_missed(num, den, o, d, pos, f, objs[i].u0, h.t)) {
+                if (!RT_SCREEN || !plane_surely_missed(num, den, o, d, pos, f, objs[i].u0, h.t)) {
                     float t = num / den;
                     v3 p = add(o, scale(d, t));
                     if ((t >= kTMin) && (t < h.t) && plane_in_range(p, f, objs[i].u0)) {
@@ -199,7 +203,7 @@ __device__ __forceinline__ Hit closest_hit(const ObjRec* __restrict__ objs, int 
                     v3 s2 = cross(s, e1);
                     const float det = dot(s1, e1);
                     const float n_t = dot(s2, e2), n_b1 = dot(s1, s), n_b2 = dot(s2, d);
-                    if (tri_surely_missed(det, n_t, n_b1, n_b2, h.t)) continue;
+                    if (RT_SCREEN && tri_surely_missed(det, n_t, n_b1, n_b2, h.t)) continue;
                     float coef = 1.0f / det;
                     float t = coef * n_t;
                     float b1 = coef * n_b1;

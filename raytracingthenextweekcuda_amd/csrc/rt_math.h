@@ -53,11 +53,14 @@ RT_HD float minf_(float a, float b) { return a < b ? a : b; }
 RT_HD float maxf_(float a, float b) { return a > b ? a : b; }
 
 // ---------------------------------------------------------------------------
-// Counter-based RNG: Philox4x32-10 (Salmon et al., SC'11; Random123 constants).
-// Replaces cuRAND XORWOW (curand_init main.cu:127, curand_uniform Utils.h:44-51).
-// Stream: key = (seed, pixel), counter = (block, sample, 0, 0); draw n of a
-// sample is word (n & 3) of block (n >> 2). Uniform in (0, 1] with curand's
-// mapping x * 2^-32 + 2^-33.
+// RNG, replacing cuRAND XORWOW (curand_init main.cu:127, curand_uniform
+// Utils.h:44-51). Counter-based at sample granularity: Philox4x32-10 (Salmon
+// et al., SC'11; Random123 constants) with key = (seed, pixel) and counter =
+// (sample, 0, 0, 0) yields 128 bits that seed a xoshiro128** 1.1 stream
+// (Blackman & Vigna) for that sample's draws. Every (pixel, sample) stream is
+// random-access and independent of launch geometry; a draw costs ~12 full-rate
+// integer ops, so divergent call sites (rejection loops) stay cheap. Uniforms
+// use curand's (0, 1] mapping x * 2^-32 + 2^-33.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kPhiloxM0 = 0xD2511F53u;
 constexpr uint32_t kPhiloxM1 = 0xCD9E8D57u;
@@ -95,26 +98,32 @@ RT_HD float u01(uint32_t x) {
     return (float)x * inv + (inv / 2.0f);
 }
 
-// Per-lane stream state: one Philox block (4 words) cached in registers.
-struct Rng {
-    uint32_t key0, key1;  // seed, pixel
-    uint32_t sample;      // global sample index
-    uint32_t n;           // draws consumed in this sample
-    u4 buf;
+RT_HD uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
 
-    RT_HD void begin(uint32_t seed, uint32_t pixel, uint32_t s) {
-        key0 = seed;
-        key1 = pixel;
-        sample = s;
-        n = 0;
+// Per-lane stream state (4 registers).
+struct Rng {
+    uint32_t s0, s1, s2, s3;
+
+    RT_HD void begin(uint32_t seed, uint32_t pixel, uint32_t sample) {
+        u4 b = philox4x32_10(u4{sample, 0u, 0u, 0u}, seed, pixel);
+        s0 = b.x;
+        s1 = b.y;
+        s2 = b.z;
+        s3 = b.w;
+        if ((s0 | s1 | s2 | s3) == 0u) s0 = kPhiloxW0;  // xoshiro's all-zero state is invalid
     }
-    RT_HD float next() {
-        uint32_t lane = n & 3u;
-        if (lane == 0u) buf = philox4x32_10(u4{n >> 2, sample, 0u, 0u}, key0, key1);
-        uint32_t w = lane == 0u ? buf.x : lane == 1u ? buf.y : lane == 2u ? buf.z : buf.w;
-        ++n;
-        return u01(w);
+    RT_HD uint32_t next_u32() {
+        const uint32_t r = rotl32(s1 * 5u, 7) * 9u;
+        const uint32_t t = s1 << 9;
+        s2 ^= s0;
+        s3 ^= s1;
+        s1 ^= s2;
+        s0 ^= s3;
+        s2 ^= t;
+        s3 = rotl32(s3, 11);
+        return r;
     }
+    RT_HD float next() { return u01(next_u32()); }
 };
 
 // Utils::random(min,max) = min + (max - min) * u (Utils.h:49-51).

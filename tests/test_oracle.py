@@ -24,11 +24,29 @@ def test_philox_kat(ctr, key, out):
     assert orc.philox(ctr, key) == out
 
 
+def _xoshiro128ss(state, n):
+    """xoshiro128** 1.1 (Blackman & Vigna), restated in Python."""
+    s = list(state)
+    M = 0xFFFFFFFF
+    rotl = lambda x, k: ((x << k) | (x >> (32 - k))) & M
+    out = []
+    for _ in range(n):
+        out.append((rotl((s[1] * 5) & M, 7) * 9) & M)
+        t = (s[1] << 9) & M
+        s[2] ^= s[0]
+        s[3] ^= s[1]
+        s[1] ^= s[2]
+        s[0] ^= s[3]
+        s[2] ^= t
+        s[3] = rotl(s[3], 11)
+    return out
+
+
 def test_uniform_stream_layout_and_range():
+    """Stream of (seed, pixel, sample): Philox4x32-10(counter=(sample,0,0,0),
+    key=(seed,pixel)) seeds xoshiro128**; uniforms use curand's (0,1] map."""
     u = orc.uniforms(1984, 12345, 7, 9)
-    blk0 = orc.philox([0, 7, 0, 0], [1984, 12345])
-    blk1 = orc.philox([1, 7, 0, 0], [1984, 12345])
-    words = blk0 + blk1 + orc.philox([2, 7, 0, 0], [1984, 12345])[:1]
+    words = _xoshiro128ss(orc.philox([7, 0, 0, 0], [1984, 12345]), 9)
     inv = np.float32(2.0 ** -32)
     expect = np.float32(words) * inv + inv / np.float32(2)
     assert np.array_equal(u, expect.astype(np.float32))
@@ -36,6 +54,9 @@ def test_uniform_stream_layout_and_range():
     # extremes of curand's mapping
     assert np.float32(0) * inv + inv / 2 > 0
     assert np.float32(0xFFFFFFFF) * inv + inv / 2 == np.float32(1.0)
+    # distinct samples / pixels give distinct streams
+    assert not np.array_equal(u, orc.uniforms(1984, 12345, 8, 9))
+    assert not np.array_equal(u, orc.uniforms(1984, 12346, 7, 9))
 
 
 def test_cube_small_triangulation():
