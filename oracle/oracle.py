@@ -49,6 +49,7 @@ def lib():
         L.orc_mesh_obj.argtypes = [vp, C.c_int, C.c_char_p, fp, fp, fp, C.c_int]
         L.orc_load_obj.argtypes = [C.c_char_p, fp, fp, fp, C.POINTER(fp)]
         L.orc_free.argtypes = [vp]
+        L.orc_load_ply.argtypes = [C.c_char_p, fp, C.c_float, C.POINTER(fp)]
         L.orc_camera.argtypes = [vp, fp, fp, fp] + [C.c_float] * 6
         L.orc_length.argtypes = [fp]
         L.orc_length.restype = C.c_float
@@ -83,6 +84,16 @@ def load_obj(path, scale=(1, 1, 1), rotate=(0, 0, 0), offset=(0, 0, 0)) -> np.nd
     n = lib().orc_load_obj(path.encode(), f3(scale), f3(rotate), f3(offset), C.byref(p))
     if n < 0:
         raise IOError(f"oracle OBJ load failed: {path}")
+    arr = np.ctypeslib.as_array(p, shape=(max(n, 1) * 9,)).copy()[: n * 9]
+    lib().orc_free(p)
+    return arr.reshape(n, 9)
+
+
+def load_ply(path, offset=(0, 0, 0), max_coord=1.0) -> np.ndarray:
+    p = C.POINTER(C.c_float)()
+    n = lib().orc_load_ply(path.encode(), f3(offset), max_coord, C.byref(p))
+    if n < 0:
+        raise IOError(f"oracle PLY load failed: {path}")
     arr = np.ctypeslib.as_array(p, shape=(max(n, 1) * 9,)).copy()[: n * 9]
     lib().orc_free(p)
     return arr.reshape(n, 9)
@@ -219,7 +230,10 @@ def yaml_scene(path: str, models_dir: str, width: int, height: int) -> OracleSce
         elif ptype == 1:
             sc.plane(i, obj["position"], obj["normal"], obj["extend"], mid, int(obj["orientation"]),
                      bool(obj["twoSide"]))
-        elif ptype == 2:
-            sc.mesh_obj(i, os.path.join(models_dir, obj["model"]), obj["scale"], obj["rotate"],
-                        obj["offset"], 3)  # meshes always use materials[3] (main.cu:781)
+        elif ptype == 2:  # meshes always use materials[3] (main.cu:781)
+            model = os.path.join(models_dir, obj["model"])
+            if model.lower().endswith(".ply"):  # build extension (PLY placement)
+                sc.mesh(i, load_ply(model, obj.get("offset", (0, 0, 0)), float(obj.get("maxCoord", 1.0))), 3)
+            else:
+                sc.mesh_obj(i, model, obj["scale"], obj["rotate"], obj["offset"], 3)
     return sc

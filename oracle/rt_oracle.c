@@ -62,6 +62,7 @@
 
 #define ORC_FLT_EPSILON 1.19209290e-07f
 #define ORC_EPS 0.001f /* Math::epsilon, Constants.h:23 */
+#define FLT_MAX_ 3.40282347e+38f
 
 /* ---------------- Vector3Df (LinearAlgebra.h) ---------------- */
 typedef struct { float x, y, z; } V3;
@@ -730,6 +731,82 @@ int orc_load_obj(const char* path, const float scale[3], const float rotate[3], 
 }
 
 void orc_free(void* p) { free(p); }
+
+/* loadObject (ASCII PLY, Loader.cpp:207-319) + the vertex transform of
+ * processTriangleData (Loader.cpp:98-144): centre the triangles' bounds, scale
+ * to max |coord| = max_coord (MaxCoordAfterRescale, :58), add offset.
+ * Returns triangle count or -1; *out (malloc'ed) holds 9 floats per triangle
+ * in (idx1, idx2, idx3) vertex order. */
+int orc_load_ply(const char* path, const float offset[3], float max_coord, float** out) {
+    FILE* f = fopen(path, "rb");
+    if (!f) return -1;
+    char line[1024];
+    unsigned nv = 0, nf = 0;
+    int inside = 0;
+    float* v = NULL;
+    unsigned* ix = NULL;
+    unsigned cv = 0, ct = 0;
+    while (fgets(line, sizeof line, f)) {
+        if (!inside) {
+            if (!strncmp(line, "element vertex", 14)) nv = (unsigned)strtoul(line + 14, NULL, 10);
+            else if (!strncmp(line, "element face", 12)) nf = (unsigned)strtoul(line + 12, NULL, 10);
+            else if (!strncmp(line, "end_header", 10)) {
+                inside = 1;
+                v = (float*)malloc((size_t)(nv ? nv : 1) * 3 * sizeof(float));
+                ix = (unsigned*)malloc((size_t)(nf ? nf : 1) * 3 * sizeof(unsigned));
+            }
+        } else if (nv) {
+            char* e;
+            nv--;
+            v[3 * cv] = strtof(line, &e);
+            v[3 * cv + 1] = strtof(e, &e);
+            v[3 * cv + 2] = strtof(e, &e);
+            cv++;
+        } else if (nf) {
+            unsigned long a[4];
+            const char* p = line;
+            char* e;
+            int k;
+            nf--;
+            for (k = 0; k < 4; ++k) {
+                a[k] = strtoul(p, &e, 10);
+                if (e == p) break;
+                p = e;
+            }
+            if (k < 4) continue;
+            if (a[1] >= cv || a[2] >= cv || a[3] >= cv) { fclose(f); free(v); free(ix); return -1; }
+            ix[3 * ct] = (unsigned)a[1]; ix[3 * ct + 1] = (unsigned)a[2]; ix[3 * ct + 2] = (unsigned)a[3];
+            ct++;
+        }
+    }
+    fclose(f);
+    if (!inside) { free(v); free(ix); return -1; }
+    V3 mn = v3(FLT_MAX_, FLT_MAX_, FLT_MAX_), mx = v3(-FLT_MAX_, -FLT_MAX_, -FLT_MAX_);
+    for (unsigned i = 0; i < 3 * ct; ++i) {
+        V3 q = v3(v[3 * ix[i]], v[3 * ix[i] + 1], v[3 * ix[i] + 2]);
+        mn = v3(mn.x < q.x ? mn.x : q.x, mn.y < q.y ? mn.y : q.y, mn.z < q.z ? mn.z : q.z);
+        mx = v3(mx.x > q.x ? mx.x : q.x, mx.y > q.y ? mx.y : q.y, mx.z > q.z ? mx.z : q.z);
+    }
+    V3 c = v3((mx.x + mn.x) * 0.5f, (mx.y + mn.y) * 0.5f, (mx.z + mn.z) * 0.5f);
+    mn = vsub(mn, c);
+    mx = vsub(mx, c);
+    float maxi = 0.0f, cand[6] = {fabsf(mn.x), fabsf(mn.y), fabsf(mn.z), fabsf(mx.x), fabsf(mx.y), fabsf(mx.z)};
+    for (int k = 0; k < 6; ++k) maxi = (maxi < cand[k]) ? cand[k] : maxi;
+    float sc = max_coord / maxi;
+    V3 off = v3(offset[0], offset[1], offset[2]);
+    for (unsigned i = 0; i < cv; ++i) {
+        V3 q = v3(v[3 * i], v[3 * i + 1], v[3 * i + 2]);
+        q = vadd(vmul(vsub(q, c), sc), off);
+        v[3 * i] = q.x; v[3 * i + 1] = q.y; v[3 * i + 2] = q.z;
+    }
+    float* t = (float*)malloc((size_t)(ct ? ct : 1) * 9 * sizeof(float));
+    for (unsigned i = 0; i < 3 * ct; ++i) {
+        t[3 * i] = v[3 * ix[i]]; t[3 * i + 1] = v[3 * ix[i] + 1]; t[3 * i + 2] = v[3 * ix[i] + 2];
+    }
+    free(v); free(ix);
+    *out = t;
+    return (int)ct;
+}
 
 int orc_mesh_obj(Scene* s, int idx, const char* path, const float scale[3], const float rotate[3],
                  const float offset[3], int mat) {

@@ -27,6 +27,8 @@ struct rt_ctx {
     rt::ObjRec* d_objs = nullptr;
     rt::TriRec* d_tris = nullptr;
     rt::MatRec* d_mats = nullptr;
+    rt::BvhNode* d_nodes = nullptr;
+    uint32_t* d_tri_orig = nullptr;
     int n_objs = 0;
     int n_mats = 0;
     unsigned long long* d_counters = nullptr;
@@ -76,9 +78,13 @@ void free_device(rt_ctx* c) {
     (void)hipFree(c->d_objs);
     (void)hipFree(c->d_tris);
     (void)hipFree(c->d_mats);
+    (void)hipFree(c->d_nodes);
+    (void)hipFree(c->d_tri_orig);
     c->d_objs = nullptr;
     c->d_tris = nullptr;
     c->d_mats = nullptr;
+    c->d_nodes = nullptr;
+    c->d_tri_orig = nullptr;
 }
 
 }  // namespace
@@ -375,6 +381,8 @@ rt_status rt_commit(rt_ctx* c) {
     RT_HIP(c, up(&c->d_objs, S.objs));
     RT_HIP(c, up(&c->d_tris, S.tris));
     RT_HIP(c, up(&c->d_mats, S.mats));
+    RT_HIP(c, up(&c->d_nodes, S.nodes));
+    RT_HIP(c, up(&c->d_tri_orig, S.tri_orig));
     c->n_objs = (int)S.objs.size();
     c->n_mats = (int)S.mats.size();
     c->committed = true;
@@ -393,6 +401,7 @@ rt_status rt_scene_info(const rt_ctx* c, int32_t out[8]) {
     }
     out[4] = (int32_t)c->scene.tris.size();
     out[5] = (int32_t)c->scene.mats.size();
+    out[6] = (int32_t)c->scene.nodes.size();
     return RT_OK;
 }
 
@@ -433,7 +442,7 @@ rt_status rt_render_device(rt_ctx* c, const rt_render_params* p, float* out, voi
     RT_HIP(c, hipSetDevice(c->device));
     RT_HIP(c, hipMemsetAsync(c->d_counters, 0, rt::kNumCounters * sizeof(unsigned long long), st));
     RT_HIP(c, hipEventRecord(c->ev0, st));
-    rt::KernelScene sc{c->d_objs, c->d_tris, c->d_mats, c->n_objs, c->n_mats};
+    rt::SceneArgs sc{c->d_objs, c->d_tris, c->d_mats, c->d_nodes, c->d_tri_orig, c->n_objs, c->n_mats};
     RT_HIP(c, rt::launch_render(sc, c->scene.camera, L, out, c->d_counters, st));
     RT_HIP(c, hipEventRecord(c->ev1, st));
     c->last = rt_render_stats{};

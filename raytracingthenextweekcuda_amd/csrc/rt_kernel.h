@@ -38,7 +38,7 @@ inline void choose_layout(RenderLaunch& L, int32_t requested) {
 // [3] = BVH node visits, [4] = traversal overflow flag.
 constexpr int kNumCounters = 8;
 
-hipError_t launch_render(const KernelScene& sc, const CamRec& cam, const RenderLaunch& L,
+hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLaunch& L,
                          float* out, unsigned long long* counters, hipStream_t stream);
 
 // Rows of [0, height) owned by (row_block, row_rank, row_world).

@@ -6,17 +6,22 @@
 // (Camera.h:151-168) + cuRAND (main.cu:120-129) with one hand-written kernel.
 //
 // Execution model:
-//  * one lane = one pixel; a 256-thread workgroup covers a 16x16 pixel tile,
-//    each wave64 an 8x8 sub-tile (spatially coherent rays share scene records);
-//  * path regeneration: a lane whose path terminates immediately starts its
-//    next sample, so lanes stay busy until the pixel's last sample instead of
-//    idling for the longest path of every sample; the wave exits when its
-//    ballot of live lanes is empty;
-//  * scene records are read at wave-uniform addresses in the closest-hit scan
-//    (scalar loads, broadcast to 64 lanes); materials per lane;
-//  * stateless Philox RNG (no init kernel, no 48 B/pixel state in HBM);
-//  * per-wave popcount-free counters: lane counts reduced in-wave, one 64-bit
-//    atomic per wave per counter.
+//  * lanes own pixels (or 1/S of a pixel's samples, lanes_per_pixel = S); a
+//    256-thread workgroup covers a 2x2 block of per-wave pixel tiles;
+//  * path regeneration: a lane whose path terminates starts its next sample in
+//    the same loop trip, so lanes stay busy until their last sample;
+//  * the main loop is wave-uniform (exits on an empty __ballot of live lanes),
+//    so the whole wave is available for cooperative work inside a trip;
+//  * small meshes (the reference's brute-force TriangleMesh) are tested with
+//    ballot compaction: the (ray, triangle) pairs of the lanes whose rays hit
+//    the mesh box are packed densely over all 64 lanes, and per-ray results are
+//    merged with a 64-bit LDS atomic-min on (t, triangle index);
+//  * large meshes use the reference's binned-SAH BVH (BVH.cpp) with a per-lane
+//    traversal stack resident in LDS (32 entries x 64 lanes per wave, laid out
+//    so lane i always hits bank i);
+//  * scene records of the closest-hit scan are read at wave-uniform addresses
+//    (scalar loads broadcast to 64 lanes); materials/nodes per lane;
+//  * counter-based RNG (rt_math.h): no init kernel and no RNG state in HBM.
 //
 // Numerics: compiled with -ffp-contract=off and IEEE div/sqrt; every expression
 // keeps the reference's evaluation order (rt_math.h), so the output is
@@ -30,10 +35,8 @@ namespace rt {
 namespace {
 
 constexpr float kInf = __builtin_huge_valf();
-
-#ifndef RT_SCREEN
-#define RT_SCREEN 1  // rcp-screened plane/triangle tests (exact fallback)
-#endif
+constexpr int kWavesPerBlock = 4;
+constexpr int kStackDepth = kBvhStackDepth;
 
 struct Ray {
     v3 o, d;
@@ -62,6 +65,17 @@ __device__ __forceinline__ bool box_hit(const float* f, v3 o, v3 inv) {
         if (t < 0.0f) return false;
     }
     return true;
+}
+
+// Conservative BVH node test (boxes are inflated at build time; NaN slabs from
+// 0 * inf are ignored by fminf/fmaxf, i.e. never cull): entry <= min(exit, tmax).
+__device__ __forceinline__ bool node_hit(const BvhNode& n, v3 o, v3 inv, float tmax) {
+    const float tx0 = (n.lo[0] - o.x) * inv.x, tx1 = (n.hi[0] - o.x) * inv.x;
+    const float ty0 = (n.lo[1] - o.y) * inv.y, ty1 = (n.hi[1] - o.y) * inv.y;
+    const float tz0 = (n.lo[2] - o.z) * inv.z, tz1 = (n.hi[2] - o.z) * inv.z;
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    return tn <= fminf(tf, tmax * 1.00001f + 1e-30f);
 }
 
 // Sphere::hit / MovingSphere::hit root selection (Sphere.cu:3-37, 39-73).
@@ -99,59 +113,153 @@ __device__ __forceinline__ bool plane_in_range(v3 p, const float* f, uint32_t or
     return (p.x > f[0] - f[6]) && (p.x < f[0] + f[6]) && (p.z > f[2] - f[8]) && (p.z < f[2] + f[8]);
 }
 
-// Relative slack that bounds the error of the screening arithmetic: v_rcp_f32
-// is within 1 ulp, each further rounding adds 0.5 ulp, so screened values are
-// within ~4 ulp (4.8e-7 relative) of the exact ones; 1e-5 leaves > 20x room.
-constexpr float kScreen = 1e-5f;
-
-// True only if the exact Plane::hit test is certain to fail.
-__device__ __forceinline__ bool plane_surely_missed(float num, float den, v3 o, v3 d, v3 pos,
-                                                    const float* f, uint32_t orient, float tmax) {
-    const float tq = num * __builtin_amdgcn_rcpf(den);
-    const float mt = fabsf(tq) * kScreen;
-    if (tq + mt < kTMin || tq - mt >= tmax) return true;
-    const v3 pq = add(o, scale(d, tq));
-    // |p - pq| <= |d| |t| 4.8e-7 + rounding of p: covered by slack on |d||tq| and |pq|.
-    auto out = [&](float pa, float da, float lo, float hi) {
-        const float m = (fabsf(da) * fabsf(tq) + fabsf(pa)) * kScreen + 1e-30f;
-        return (pa + m <= lo) || (pa - m >= hi);
-    };
-    if (orient == 0u)
-        return out(pq.x, d.x, f[0] - f[6], f[0] + f[6]) || out(pq.y, d.y, f[1] - f[7], f[1] + f[7]);
-    if (orient == 1u)
-        return out(pq.y, d.y, f[1] - f[7], f[1] + f[7]) || out(pq.z, d.z, f[2] - f[8], f[2] + f[8]);
-    return out(pq.x, d.x, f[0] - f[6], f[0] + f[6]) || out(pq.z, d.z, f[2] - f[8], f[2] + f[8]);
-}
-
-// True only if the exact TriangleMesh::hit acceptance test is certain to fail.
-// NaN/inf screened values compare false and fall through to the exact path.
-__device__ __forceinline__ bool tri_surely_missed(float det, float n_t, float n_b1, float n_b2,
-                                                  float tmax) {
-    if (!(fabsf(det) > 1e-30f)) return false;
-    const float cq = __builtin_amdgcn_rcpf(det);
-    const float tq = cq * n_t, b1 = cq * n_b1, b2 = cq * n_b2;
-    const float mt = fabsf(tq) * kScreen;
-    if (tq + mt < kTMin || tq - mt >= tmax) return true;
-    const float m1 = fabsf(b1) * kScreen, m2 = fabsf(b2) * kScreen;
-    if (b1 + m1 < kFltEpsilon || b2 + m2 < kFltEpsilon) return true;
-    const float r = 1.0f - b1 - b2;
-    return r + (m1 + m2 + 4e-7f) < kFltEpsilon;
+// One triangle of TriangleMesh::hit (TriangleMesh.cu:40-108) without the
+// closestSoFar comparison: returns t if every other acceptance test passes,
+// else +inf. (t < closestSoFar is applied by the caller.)
+__device__ __forceinline__ float tri_t(const TriRec& tr, v3 o, v3 d) {
+    v3 n{tr.nx, tr.ny, tr.nz};
+    if (dot(d, n) > kFltEpsilon) return kInf;  // backface cull
+    v3 e1{tr.e1x, tr.e1y, tr.e1z}, e2{tr.e2x, tr.e2y, tr.e2z};
+    v3 s = sub(o, v3{tr.v0x, tr.v0y, tr.v0z});
+    v3 s1 = cross(d, e2);
+    v3 s2 = cross(s, e1);
+    float coef = 1.0f / dot(s1, e1);
+    float t = coef * dot(s2, e2);
+    float b1 = coef * dot(s1, s);
+    float b2 = coef * dot(s2, d);
+    if (((t >= kFltEpsilon) && (t >= kTMin)) && (b1 >= kFltEpsilon) && (b2 >= kFltEpsilon) &&
+        ((1.0f - b1 - b2) >= kFltEpsilon))
+        return t;
+    return kInf;
 }
 
 struct Hit {
     float t;
-    int32_t obj;   // object table index of the closest hit (-1: none)
-    int32_t tri;   // triangle index for meshes
+    int32_t obj;  // object table index of the closest hit (-1: none)
+    int32_t tri;  // triangle index for meshes
 };
+
+struct WaveLds {
+    unsigned long long key[64];  // per-ray (t bits << 32 | triangle) minima
+    int32_t src[64];             // rank -> lane of the rays wanting a mesh
+};
+
+struct Counters {
+    uint32_t segs, tri_tests, box_tests, node_visits, overflow;
+};
+
+// The lane's rank among the set bits of `mask` below it.
+__device__ __forceinline__ int lane_rank(uint64_t mask) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// Brute-force mesh (TriangleMesh::hit) with ballot compaction. Called by all 64
+// lanes of the wave (uniform control flow); `want` = this lane's ray hit the
+// mesh box. The result equals the reference's sequential scan: the smallest t
+// below the caller's closestSoFar, ties resolved to the lowest triangle index.
+__device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, uint32_t base,
+                                             uint32_t m, bool want, v3 o, v3 d, Hit& h, int32_t obj,
+                                             WaveLds& W, int lane) {
+    const uint64_t mask = __ballot(want);
+    if (mask == 0) return;
+    const int rank = lane_rank(mask);
+    if (want) {
+        W.src[rank] = lane;
+        W.key[rank] = ~0ull;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t total = (uint32_t)__popcll(mask) * m;
+    const float t0 = h.t;
+    for (uint32_t p0 = 0; p0 < total; p0 += 64) {
+        const uint32_t p = p0 + (uint32_t)lane;
+        const bool act = p < total;
+        const uint32_t r = act ? p / m : 0u;
+        const uint32_t k = act ? p - r * m : 0u;
+        const int src = W.src[r];
+        const v3 ro{__shfl(o.x, src, 64), __shfl(o.y, src, 64), __shfl(o.z, src, 64)};
+        const v3 rd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
+        const float rt0 = __shfl(t0, src, 64);
+        if (act) {
+            const float t = tri_t(tris[base + k], ro, rd);
+            if (t < rt0) {
+                const unsigned long long key =
+                    ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)k;
+                atomicMin(&W.key[r], key);
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (want) {
+        const unsigned long long key = W.key[rank];
+        if (key != ~0ull) {
+            h.t = __uint_as_float((uint32_t)(key >> 32));
+            h.obj = obj;
+            h.tri = (int32_t)(base + (uint32_t)(key & 0xFFFFFFFFu));
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// BVH mesh: per-lane traversal of the reference's SAH tree (DFS node order,
+// leaves own contiguous ranges of `tris`, `tri_orig` holds the mesh-local
+// triangle index for the lowest-index tie rule of the sequential scan).
+__device__ __forceinline__ void mesh_bvh(const TriRec* __restrict__ tris,
+                                         const uint32_t* __restrict__ tri_orig,
+                                         const BvhNode* __restrict__ nodes, uint32_t root, bool want,
+                                         v3 o, v3 d, v3 inv, Hit& h, int32_t obj, uint32_t* stack,
+                                         Counters& cnt) {
+    if (!want) return;
+    const float t0 = h.t;
+    float best = t0;
+    uint32_t best_orig = 0xFFFFFFFFu, best_k = 0;
+    stack[0] = root;
+    int sp = 1;
+    while (sp > 0) {
+        const uint32_t ni = stack[(--sp) * 64];
+        const BvhNode nd = nodes[ni];
+        ++cnt.node_visits;
+        if (nd.b & 0x80000000u) {
+            const uint32_t nt = nd.b & 0x7FFFFFFFu;
+            cnt.tri_tests += nt;
+            for (uint32_t k = nd.a; k < nd.a + nt; ++k) {
+                const float t = tri_t(tris[k], o, d);
+                if (t < t0) {
+                    const uint32_t orig = tri_orig[k];
+                    if (t < best || (t == best && orig < best_orig)) {
+                        best = t;
+                        best_orig = orig;
+                        best_k = k;
+                    }
+                }
+            }
+        } else {
+            const bool hl = node_hit(nodes[nd.a], o, inv, best);
+            const bool hr = node_hit(nodes[nd.b], o, inv, best);
+            if (sp + 2 > kStackDepth) {
+                cnt.overflow = 1;
+                break;
+            }
+            if (hr) stack[(sp++) * 64] = nd.b;
+            if (hl) stack[(sp++) * 64] = nd.a;
+        }
+    }
+    if (best_orig != 0xFFFFFFFFu) {
+        h.t = best;
+        h.obj = obj;
+        h.tri = (int32_t)best_k;
+    }
+}
 
 // hit() over the flattened object table (main.cu:43-57): closest so far is
 // passed as tMax to each object, each object's own comparison rule is kept.
-__device__ __forceinline__ Hit closest_hit(const ObjRec* __restrict__ objs, int n_objs,
-                                           const TriRec* __restrict__ tris, const Ray& ray,
-                                           v3 inv, uint32_t& tri_tests, uint32_t& box_tests) {
+// Called with the whole wave active; `live` masks lanes without a path.
+__device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v3 inv, bool live,
+                                           WaveLds& W, uint32_t* stack, int lane, Counters& cnt) {
     Hit h{kInf, -1, -1};
     const v3 o = ray.o, d = ray.d;
-    for (int i = 0; i < n_objs; ++i) {
+    const ObjRec* __restrict__ objs = S.objs;
+    for (int i = 0; i < S.n_objs; ++i) {
         const uint32_t type = objs[i].type;
         const float* f = objs[i].f;
         if (type == kObjPlane) {
@@ -160,18 +268,11 @@ __device__ __forceinline__ Hit closest_hit(const ObjRec* __restrict__ objs, int 
             float den = dot(n, d);
             bool proceed = objs[i].u1 ? (fabsf(den) > kTMin) : (den > kTMin);
             if (proceed) {
-                v3 pos{f[0], f[1], f[2]};
-                float num = dot(sub(pos, o), n);
-                // Screening with v_rcp_f32 (<= 1 ulp): only lanes that are not
-                // clearly rejected evaluate the IEEE division, so every accepted
-                // hit and every close call is decided by the exact arithmetic.
-                if (!RT_SCREEN || !plane_surely_missed(num, den, o, d, pos, f, objs[i].u0, h.t)) {
-                    float t = num / den;
-                    v3 p = add(o, scale(d, t));
-                    if ((t >= kTMin) && (t < h.t) && plane_in_range(p, f, objs[i].u0)) {
-                        h.t = t;
-                        h.obj = i;
-                    }
+                float t = dot(sub(v3{f[0], f[1], f[2]}, o), n) / den;
+                v3 p = add(o, scale(d, t));
+                if ((t >= kTMin) && (t < h.t) && plane_in_range(p, f, objs[i].u0)) {
+                    h.t = t;
+                    h.obj = i;
                 }
             }
         } else if (type == kObjSphere) {
@@ -187,36 +288,18 @@ __device__ __forceinline__ Hit closest_hit(const ObjRec* __restrict__ objs, int 
                 h.obj = i;
             }
         } else {
-            // TriangleMesh::hit (TriangleMesh.cu:34-117): AABB early-out, then
-            // every triangle with the strict t < closestSoFar rule.
-            ++box_tests;
-            if (box_hit(f, o, inv)) {
-                const uint32_t b = objs[i].u0, e = b + objs[i].u1;
-                tri_tests += e - b;
-                for (uint32_t k = b; k < e; ++k) {
-                    const TriRec& tr = tris[k];
-                    v3 n{tr.nx, tr.ny, tr.nz};
-                    if (dot(d, n) > kFltEpsilon) continue;  // backface cull
-                    v3 e1{tr.e1x, tr.e1y, tr.e1z}, e2{tr.e2x, tr.e2y, tr.e2z};
-                    v3 s = sub(o, v3{tr.v0x, tr.v0y, tr.v0z});
-                    v3 s1 = cross(d, e2);
-                    v3 s2 = cross(s, e1);
-                    const float det = dot(s1, e1);
-                    const float n_t = dot(s2, e2), n_b1 = dot(s1, s), n_b2 = dot(s2, d);
-                    if (RT_SCREEN && tri_surely_missed(det, n_t, n_b1, n_b2, h.t)) continue;
-                    float coef = 1.0f / det;
-                    float t = coef * n_t;
-                    float b1 = coef * n_b1;
-                    float b2 = coef * n_b2;
-                    if (((t >= kFltEpsilon) && ((t >= kTMin) && (t < h.t))) &&
-                        (b1 >= kFltEpsilon) && (b2 >= kFltEpsilon) &&
-                        ((1.0f - b1 - b2) >= kFltEpsilon)) {
-                        h.t = t;
-                        h.obj = i;
-                        h.tri = (int32_t)k;
-                    }
-                }
+            // TriangleMesh::hit (TriangleMesh.cu:34-117): the AABB early-out
+            // gates the triangle scan exactly as in the reference.
+            const bool want = live && box_hit(f, o, inv);
+            const uint32_t root = objs[i].u2;
+            if (live) {
+                ++cnt.box_tests;
+                if (want && root == kNoBvh) cnt.tri_tests += objs[i].u1;
             }
+            if (root == kNoBvh)
+                mesh_compact(S.tris, objs[i].u0, objs[i].u1, want, o, d, h, i, W, lane);
+            else
+                mesh_bvh(S.tris, S.tri_orig, S.nodes, root, want, o, d, inv, h, i, stack, cnt);
         }
     }
     return h;
@@ -229,18 +312,35 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 
 }  // namespace
 
-__global__ __launch_bounds__(256) void render_kernel(
+#ifndef RT_WAVES_PER_EU
+#define RT_WAVES_PER_EU 0  // occupancy hint (experiments): min waves per SIMD
+#endif
+#if RT_WAVES_PER_EU > 0
+#define RT_OCC __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
+#else
+#define RT_OCC
+#endif
+
+__global__ __launch_bounds__(256) RT_OCC void render_kernel(
     const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
-    const MatRec* __restrict__ mats, int n_objs, CamRec cam, RenderLaunch L,
+    const MatRec* __restrict__ mats, const BvhNode* __restrict__ nodes,
+    const uint32_t* __restrict__ tri_orig, int n_objs, CamRec cam, RenderLaunch L,
     float* __restrict__ out, unsigned long long* __restrict__ counters) {
+    const SceneArgs S{objs, tris, mats, nodes, tri_orig, n_objs, 0};
+    __shared__ WaveLds lds[kWavesPerBlock];
+    __shared__ uint32_t stacks[kWavesPerBlock][kStackDepth * 64];
+
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    // Lane layout: S = lanes_per_pixel adjacent lanes share one pixel and split
-    // its samples (sub-lane c takes samples c, c+S, c+2S, ...). A wave covers
-    // 64/S pixels as a tw x th tile; a 4-wave workgroup covers 2tw x 2th.
-    const int S = L.lanes_per_pixel;
-    const int c = lane & (S - 1);
-    const int pix = lane / S;
+    WaveLds& W = lds[wave];
+    uint32_t* stack = &stacks[wave][lane];
+
+    // Lane layout: SP = lanes_per_pixel adjacent lanes share one pixel and split
+    // its samples (sub-lane c takes samples c, c+SP, c+2SP, ...). A wave covers
+    // 64/SP pixels as a tw x th tile; a 4-wave workgroup covers 2tw x 2th.
+    const int SP = L.lanes_per_pixel;
+    const int c = lane & (SP - 1);
+    const int pix = lane / SP;
     const int tw = L.tile_w, th = L.tile_h;
     const int px = blockIdx.x * (2 * tw) + (wave & 1) * tw + (pix % tw);
     const int lrow = blockIdx.y * (2 * th) + (wave >> 1) * th + (pix / tw);
@@ -251,18 +351,19 @@ __global__ __launch_bounds__(256) void render_kernel(
     const uint32_t pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
 
     v3 sum{0.0f, 0.0f, 0.0f};
-    uint32_t segs = 0, tri_tests = 0, box_tests = 0;
+    Counters cnt{0, 0, 0, 0, 0};
     int s = c;
     bool alive = valid && s < L.spp;
     bool need_cam = true;
     int depth = 0;
-    Ray ray{};
+    Ray ray{{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 1.0f}, 0.0f};
     v3 thr{1.0f, 1.0f, 1.0f};
-    Rng rng;
+    Rng rng{1u, 0u, 0u, 0u};
     const float fw = (float)(L.width - 1), fh = (float)(L.height - 1);
 
-    while (alive) {
-        if (need_cam) {
+    for (;;) {
+        if (__ballot(alive) == 0) break;  // wave-uniform exit
+        if (alive && need_cam) {
             // renderKernel sample loop body (main.cu:179-185) + getRay (Camera.h:151-168).
             rng.begin(L.seed, pixel, L.sample_offset + (uint32_t)s);
             float rx = rng.next();
@@ -273,8 +374,7 @@ __global__ __launch_bounds__(256) void render_kernel(
             v3 rnd = scale(disk, cam.lens_radius);
             v3 offset = add(scale(cam.right, rnd.x), scale(cam.true_up, rnd.y));
             v3 norig = add(cam.origin, offset);
-            v3 dir = sub(add(add(cam.lower_left, scale(cam.horizontal, dx)),
-                             scale(cam.vertical, dy)),
+            v3 dir = sub(add(add(cam.lower_left, scale(cam.horizontal, dx)), scale(cam.vertical, dy)),
                          norig);
             dir = normalize(dir);
             float tm = random_range(rng, cam.time0, cam.time1);
@@ -284,20 +384,21 @@ __global__ __launch_bounds__(256) void render_kernel(
             need_cam = false;
             if (L.max_depth <= 0) {  // rayColor with BOUNCES = 0 returns black
                 need_cam = true;
-                s += S;
+                s += SP;
                 if (s >= L.spp) alive = false;
-                continue;
             }
         }
+        const bool live = alive && !need_cam;
 
         const v3 inv = rcp(ray.d);
-        Hit h = closest_hit(objs, n_objs, tris, ray, inv, tri_tests, box_tests);
-        ++segs;
+        const Hit h = closest_hit(S, ray, inv, live, W, stack, lane, cnt);
+        if (!live) continue;
+        ++cnt.segs;
 
         bool done;
         v3 contrib;
         if (h.obj >= 0) {
-            const ObjRec& ob = objs[h.obj];
+            const ObjRec& ob = S.objs[h.obj];
             const float* f = ob.f;
             v3 p = add(ray.o, scale(ray.d, h.t));  // ray.at(t)
             v3 outward;
@@ -308,13 +409,13 @@ __global__ __launch_bounds__(256) void render_kernel(
             } else if (ob.type == kObjMovingSphere) {
                 outward = divs(sub(p, moving_center(f, ray.time)), f[8]);
             } else {
-                const TriRec& tr = tris[h.tri];
+                const TriRec& tr = S.tris[h.tri];
                 outward = v3{tr.nx, tr.ny, tr.nz};
             }
             // HitResult::setFaceNormal (HitResult.h:15-18).
             const bool front = dot(ray.d, outward) < kFltEpsilon;
             const v3 n = front ? outward : neg(outward);
-            const MatRec m = mats[ob.material];
+            const MatRec m = S.mats[ob.material];
             v3 att;
             bool scattered;
             v3 nd;
@@ -337,16 +438,15 @@ __global__ __launch_bounds__(256) void render_kernel(
                 att = v3{1.0f, 1.0f, 1.0f};
                 const float ratio = front ? (1.0f / m.p0) : m.p0;
                 v3 ud = normalize(ray.d);
-                float c = fminf(dot(neg(ud), n), 1.0f);
-                float sn = sqrtf(1.0f - c * c);
-                bool cannot = ratio * sn > 1.0f;
+                float cs = fminf(dot(neg(ud), n), 1.0f);
+                float sn = sqrtf(1.0f - cs * cs);
                 bool refl;
-                if (cannot) {
+                if (ratio * sn > 1.0f) {
                     refl = true;
                 } else {
                     float r0 = (1.0f - ratio) / (1.0f + ratio);
                     r0 = r0 * r0;
-                    float R = r0 + (1.0f - r0) * pow5(1.0f - c);
+                    float R = r0 + (1.0f - r0) * pow5(1.0f - cs);
                     refl = R > rng.next();
                 }
                 v3 dir = refl ? reflect(ud, n) : refract(ud, n, ratio);
@@ -379,16 +479,16 @@ __global__ __launch_bounds__(256) void render_kernel(
         if (done) {
             sum = add(sum, contrib);
             need_cam = true;
-            s += S;
+            s += SP;
             if (s >= L.spp) alive = false;
         }
     }
 
-    // Fixed-order combination of the S partial sums: ((p0 + p1) + p2) + ...
-    if (S > 1) {
+    // Fixed-order combination of the SP partial sums: ((p0 + p1) + p2) + ...
+    if (SP > 1) {
         const int base = lane - c;
         v3 acc = sum;
-        for (int j = 1; j < S; ++j) {
+        for (int j = 1; j < SP; ++j) {
             v3 pj{__shfl(sum.x, base + j, 64), __shfl(sum.y, base + j, 64), __shfl(sum.z, base + j, 64)};
             acc = add(acc, pj);
         }
@@ -403,24 +503,28 @@ __global__ __launch_bounds__(256) void render_kernel(
         out[o + 2] = sum.z / fs;
     }
 
-    uint64_t ws = wave_sum_u64(segs);
-    uint64_t wt = wave_sum_u64(tri_tests);
-    uint64_t wb = wave_sum_u64(box_tests);
+    const uint64_t ws = wave_sum_u64(cnt.segs);
+    const uint64_t wt = wave_sum_u64(cnt.tri_tests);
+    const uint64_t wb = wave_sum_u64(cnt.box_tests);
+    const uint64_t wn = wave_sum_u64(cnt.node_visits);
+    const uint64_t wo = wave_sum_u64(cnt.overflow);
     if (lane == 0) {
         atomicAdd(&counters[0], (unsigned long long)ws);
         atomicAdd(&counters[1], (unsigned long long)wt);
         atomicAdd(&counters[2], (unsigned long long)wb);
+        if (wn) atomicAdd(&counters[3], (unsigned long long)wn);
+        if (wo) atomicAdd(&counters[4], (unsigned long long)wo);
     }
 }
 
-hipError_t launch_render(const KernelScene& sc, const CamRec& cam, const RenderLaunch& L,
-                         float* out, unsigned long long* counters, hipStream_t stream) {
-    dim3 block(256);
+hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLaunch& L, float* out,
+                         unsigned long long* counters, hipStream_t stream) {
+    dim3 block(64 * kWavesPerBlock);
     dim3 grid((L.width + 2 * L.tile_w - 1) / (2 * L.tile_w),
               (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-    hipLaunchKernelGGL(render_kernel, grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
-                       sc.n_objs, cam, L, out, counters);
+    hipLaunchKernelGGL(render_kernel, grid, block, 0, stream, sc.objs, sc.tris, sc.mats, sc.nodes,
+                       sc.tri_orig, sc.n_objs, cam, L, out, counters);
     return hipGetLastError();
 }
 

@@ -3,6 +3,8 @@
 // tables of rt_scene.h. Compiled with -ffp-contract=off (see Makefile).
 #include "rt_scene.h"
 
+#include "rt_bvh.h"
+
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
@@ -228,6 +230,9 @@ std::string HostScene::flatten() {
     objs.clear();
     tris.clear();
     mats.clear();
+    nodes.clear();
+    tri_orig.clear();
+    bvh_max_depth = 0;
     for (size_t i = 0; i < materials.size(); ++i) {
         MatRec m = materials[i].rec;
         if (!materials[i].defined) m.type = 0xFFFFFFFFu;  // never referenced by a defined object
@@ -257,6 +262,7 @@ std::string HostScene::flatten() {
             };
             for (const Face& f : faces) {
                 ObjRec r{};
+                r.u2 = kNoBvh;
                 r.type = kObjPlane;
                 r.material = o.material;
                 r.u0 = f.orient;
@@ -271,6 +277,7 @@ std::string HostScene::flatten() {
         ObjRec r{};
         r.type = o.type;
         r.material = o.material;
+        r.u2 = kNoBvh;
         memcpy(r.f, o.f, sizeof(r.f));
         if (o.type == kObjPlane) {
             r.u0 = o.orientation;
@@ -280,6 +287,7 @@ std::string HostScene::flatten() {
             if (nt == 0) continue;  // empty meshes are not created (main.cu:777)
             r.u0 = (uint32_t)tris.size();
             r.u1 = (uint32_t)nt;
+            r.u2 = kNoBvh;
             // computeMeshAABB (main.cu:261-281): per-axis min / max of all vertices.
             v3 lo{o.tri_vertices[0], o.tri_vertices[1], o.tri_vertices[2]}, hi = lo;
             for (size_t k = 0; k < nt * 3; ++k) {
@@ -289,10 +297,50 @@ std::string HostScene::flatten() {
             }
             r.f[0] = lo.x; r.f[1] = lo.y; r.f[2] = lo.z;
             r.f[3] = hi.x; r.f[4] = hi.y; r.f[5] = hi.z;
+            std::vector<int32_t> order(nt);
+            for (size_t t = 0; t < nt; ++t) order[t] = (int32_t)t;
+            if (nt > kBvhMinTris) {
+                // The reference's binned-SAH builder over this mesh's triangles.
+                std::vector<v3> vs(nt * 3);
+                std::vector<uint32_t> ix(nt * 3);
+                for (size_t k = 0; k < nt * 3; ++k) {
+                    vs[k] = v3{o.tri_vertices[3 * k], o.tri_vertices[3 * k + 1], o.tri_vertices[3 * k + 2]};
+                    ix[k] = (uint32_t)k;
+                }
+                CFBvh b;
+                build_cf_bvh(vs, ix, b);
+                if (b.max_depth >= kBvhStackDepth)
+                    return "mesh " + std::to_string(i) + ": BVH depth " + std::to_string(b.max_depth) +
+                           " exceeds the traversal stack (" + std::to_string(kBvhStackDepth) + ")";
+                bvh_max_depth = std::max(bvh_max_depth, b.max_depth);
+                order.assign(b.tri_index.begin(), b.tri_index.end());
+                const uint32_t nb = (uint32_t)nodes.size();
+                r.u2 = nb;
+                for (const CFNode& c : b.nodes) {
+                    BvhNode n;
+                    for (int a = 0; a < 3; ++a) {
+                        // Conservative inflation: node tests may never cull a
+                        // triangle the exact test accepts.
+                        const float m = std::max(fabsf(c.bottom[a]), fabsf(c.top[a]));
+                        const float pad = m * 1e-5f + 1e-30f;
+                        n.lo[a] = c.bottom[a] - pad;
+                        n.hi[a] = c.top[a] + pad;
+                    }
+                    if (c.u0 & 0x80000000u) {
+                        n.a = r.u0 + c.u1;
+                        n.b = c.u0;
+                    } else {
+                        n.a = nb + c.u0;
+                        n.b = nb + c.u1;
+                    }
+                    nodes.push_back(n);
+                }
+            }
             for (size_t t = 0; t < nt; ++t) {
-                const float* p = &o.tri_vertices[9 * t];
+                const float* p = &o.tri_vertices[9 * (size_t)order[t]];
                 tris.push_back(make_triangle(v3{p[0], p[1], p[2]}, v3{p[3], p[4], p[5]},
                                              v3{p[6], p[7], p[8]}));
+                tri_orig.push_back((uint32_t)order[t]);
             }
         }
         objs.push_back(r);

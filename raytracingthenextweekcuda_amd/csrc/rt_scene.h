@@ -28,12 +28,19 @@ struct alignas(16) ObjRec {
     uint32_t material;
     uint32_t u0;  // plane: orientation | mesh: first triangle
     uint32_t u1;  // plane: twoSide     | mesh: triangle count
+    uint32_t u2;  // mesh: BVH root node index, or kNoBvh (brute-force scan)
     // sphere: center xyz, radius
     // moving sphere: center0 xyz, center1 xyz, time0, time1, radius
     // plane: position xyz, normal xyz, extend xyz
-    // mesh: boundsMin xyz, boundsMax xyz
-    float f[12];
+    // mesh: boundsMin xyz, boundsMax xyz (computeMeshAABB, main.cu:261-281)
+    float f[11];
 };
+constexpr uint32_t kNoBvh = 0xFFFFFFFFu;
+// Meshes with more triangles than this are traversed through a BVH.
+constexpr uint32_t kBvhMinTris = 64;
+// Per-lane LDS traversal stack depth; the builder rejects deeper trees, like
+// the reference's BVH_STACK_SIZE check (BVH.cpp:490-496, CUDAPathTracer.h:43).
+constexpr int kBvhStackDepth = 32;
 static_assert(sizeof(ObjRec) == 64, "ObjRec must be 64 B");
 
 // Triangle as prepared by prepareTriangleData (main.cu:334-349): v0, E1, E2.
@@ -46,6 +53,18 @@ struct alignas(16) TriRec {
     float e2x, e2y, e2z, nz;
 };
 static_assert(sizeof(TriRec) == 48, "TriRec must be 48 B");
+
+// BVH node for traversal: the reference's CacheFriendlyBVHNode (BVH.h:46-67)
+// with absolute child / triangle indices and conservatively inflated bounds.
+// Inner: a = left child, b = right child. Leaf: a = first triangle (leaf order),
+// b = 0x80000000 | count.
+struct alignas(16) BvhNode {
+    float lo[3];
+    uint32_t a;
+    float hi[3];
+    uint32_t b;
+};
+static_assert(sizeof(BvhNode) == 32, "BvhNode must be 32 B");
 
 struct alignas(16) MatRec {
     uint32_t type;  // RT_LAMBERTIAN..RT_EMISSION
@@ -61,10 +80,12 @@ struct CamRec {
     float lens_radius, time0, time1;
 };
 
-struct KernelScene {
+struct SceneArgs {
     const ObjRec* objs;
     const TriRec* tris;
     const MatRec* mats;
+    const BvhNode* nodes;
+    const uint32_t* tri_orig;  // mesh-local triangle index of each TriRec
     int32_t n_objs;
     int32_t n_mats;
 };
@@ -98,6 +119,9 @@ struct HostScene {
     std::vector<ObjRec> objs;
     std::vector<TriRec> tris;
     std::vector<MatRec> mats;
+    std::vector<BvhNode> nodes;
+    std::vector<uint32_t> tri_orig;
+    int bvh_max_depth = 0;
 
     // Returns "" on success or an error message.
     std::string flatten();

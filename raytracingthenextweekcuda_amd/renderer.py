@@ -159,6 +159,11 @@ class Renderer:
         self._check(self.L.rt_mesh_obj(self.ctx, index, str(path).encode(), _v(scale), _v(rotate),
                                        _v(offset), _mat_index(material)))
 
+    def mesh_ply(self, index, path, offset=(0, 0, 0), max_coord=1.0, material=3):
+        """PLY mesh with loadObject + processTriangleData semantics (Loader.cpp)."""
+        self._check(self.L.rt_mesh_ply(self.ctx, index, str(path).encode(), _v(offset), max_coord,
+                                       _mat_index(material)))
+
     def mesh_vertices(self, index) -> np.ndarray:
         n = self.L.rt_mesh_triangle_count(self.ctx, index)
         out = np.zeros((n, 9), np.float32)

@@ -75,13 +75,26 @@ def load_yaml_scene(r: Renderer, path: str, width: int, height: int, models_dir:
             r.plane(i, obj["position"], obj["normal"], obj["extend"], r.materials[mid],
                     int(obj["orientation"]), bool(obj["twoSide"]))
         elif ptype == 2:
-            r.mesh_obj(i, os.path.join(models_dir, obj["model"]), obj["scale"], obj["rotate"],
-                       obj["offset"], r.materials[3])
+            model = os.path.join(models_dir, obj["model"])
+            if model.lower().endswith(".ply"):
+                # Build extension: PLY meshes use loadObject/processTriangleData
+                # placement (offset + maxCoord), not the OBJ scale/rotate/offset.
+                r.mesh_ply(i, model, obj.get("offset", (0, 0, 0)), float(obj.get("maxCoord", 1.0)),
+                           r.materials[3])
+            else:
+                r.mesh_obj(i, model, obj["scale"], obj["rotate"], obj["offset"], r.materials[3])
         else:
             raise ValueError(f"unknown primitive type {ptype} in {path}")
     if commit:
         r.commit()
     return camera
+
+
+def bunny_cornell_box(r: Renderer, width: int, height: int, commit: bool = True) -> Camera:
+    """BASELINE config 4: bun_zipper.ply (69,451 triangles) inside the CornellBox1
+    walls (build-defined placement, assets/scenes/bunny_cornellbox.yaml)."""
+    return load_yaml_scene(r, os.path.join(SCENES_DIR, "bunny_cornellbox.yaml"), width, height,
+                           commit=commit)
 
 
 def cornell_box1(r: Renderer, width: int, height: int, commit: bool = True) -> Camera:

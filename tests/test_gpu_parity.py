@@ -175,3 +175,21 @@ def test_auto_lane_layout_fills_small_shards(rtmi):
         rtmi.cornell_box1(r, 64, 64)
         r.render(64, 64, 32, 4, lanes_per_pixel=0)
         assert r.stats()["lanes_per_pixel"] == 16
+
+
+@pytest.mark.parametrize("name,w,h,spp", [("bunny_small_cornellbox.yaml", 48, 48, 4),
+                                          ("bunny_cornellbox.yaml", 20, 20, 1)])
+def test_bvh_mesh_parity(rtmi, name, w, h, spp):
+    """Meshes above 64 triangles are traversed through the reference's SAH BVH;
+    the result must equal the reference's brute-force TriangleMesh scan (the
+    restatement tests every triangle) bit for bit."""
+    depth = 6
+    with rtmi.Renderer(0) as r:
+        rtmi.load_yaml_scene(r, os.path.join(S.SCENES, name), w, h)
+        assert r.object_counts()["bvh_node"] > 0
+        img = r.render(w, h, spp, depth)
+        st = r.stats()
+    assert st["overflow"] == 0 and st["node_visits"] > 0
+    ref, ref_st = _oracle_yaml(name, w, h).render(w, h, spp, depth)
+    _check(img, ref, st, ref_st, name)
+    assert np.array_equal(img, ref)
