@@ -442,7 +442,8 @@ rt_status rt_render_device(rt_ctx* c, const rt_render_params* p, float* out, voi
     RT_HIP(c, hipSetDevice(c->device));
     RT_HIP(c, hipMemsetAsync(c->d_counters, 0, rt::kNumCounters * sizeof(unsigned long long), st));
     RT_HIP(c, hipEventRecord(c->ev0, st));
-    rt::SceneArgs sc{c->d_objs, c->d_tris, c->d_mats, c->d_nodes, c->d_tri_orig, c->n_objs, c->n_mats};
+    rt::SceneArgs sc{c->d_objs,   c->d_tris,  c->d_mats,  c->d_nodes,
+                     c->d_tri_orig, c->n_objs, c->n_mats, !c->scene.nodes.empty()};
     RT_HIP(c, rt::launch_render(sc, c->scene.camera, L, out, c->d_counters, st));
     RT_HIP(c, hipEventRecord(c->ev1, st));
     c->last = rt_render_stats{};

@@ -254,6 +254,7 @@ __device__ __forceinline__ void mesh_bvh(const TriRec* __restrict__ tris,
 // hit() over the flattened object table (main.cu:43-57): closest so far is
 // passed as tMax to each object, each object's own comparison rule is kept.
 // Called with the whole wave active; `live` masks lanes without a path.
+template <bool kBvh>
 __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v3 inv, bool live,
                                            WaveLds& W, uint32_t* stack, int lane, Counters& cnt) {
     Hit h{kInf, -1, -1};
@@ -296,7 +297,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 ++cnt.box_tests;
                 if (want && root == kNoBvh) cnt.tri_tests += objs[i].u1;
             }
-            if (root == kNoBvh)
+            if (!kBvh || root == kNoBvh)
                 mesh_compact(S.tris, objs[i].u0, objs[i].u1, want, o, d, h, i, W, lane);
             else
                 mesh_bvh(S.tris, S.tri_orig, S.nodes, root, want, o, d, inv, h, i, stack, cnt);
@@ -313,7 +314,7 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }  // namespace
 
 #ifndef RT_WAVES_PER_EU
-#define RT_WAVES_PER_EU 0  // occupancy hint (experiments): min waves per SIMD
+#define RT_WAVES_PER_EU 4  // min waves per SIMD (caps VGPRs at 128; measured best)
 #endif
 #if RT_WAVES_PER_EU > 0
 #define RT_OCC __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
@@ -321,19 +322,22 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #define RT_OCC
 #endif
 
+// kBvh: the scene has BVH meshes (needs the 32 KB/block LDS traversal stacks,
+// which would otherwise cap occupancy for scenes that never use them).
+template <bool kBvh>
 __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
     const MatRec* __restrict__ mats, const BvhNode* __restrict__ nodes,
     const uint32_t* __restrict__ tri_orig, int n_objs, CamRec cam, RenderLaunch L,
     float* __restrict__ out, unsigned long long* __restrict__ counters) {
-    const SceneArgs S{objs, tris, mats, nodes, tri_orig, n_objs, 0};
+    const SceneArgs S{objs, tris, mats, nodes, tri_orig, n_objs, 0, kBvh};
     __shared__ WaveLds lds[kWavesPerBlock];
-    __shared__ uint32_t stacks[kWavesPerBlock][kStackDepth * 64];
+    __shared__ uint32_t stacks[kBvh ? kWavesPerBlock : 1][kBvh ? kStackDepth * 64 : 1];
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     WaveLds& W = lds[wave];
-    uint32_t* stack = &stacks[wave][lane];
+    uint32_t* stack = kBvh ? &stacks[wave][lane] : nullptr;
 
     // Lane layout: SP = lanes_per_pixel adjacent lanes share one pixel and split
     // its samples (sub-lane c takes samples c, c+SP, c+2SP, ...). A wave covers
@@ -391,7 +395,7 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
         const bool live = alive && !need_cam;
 
         const v3 inv = rcp(ray.d);
-        const Hit h = closest_hit(S, ray, inv, live, W, stack, lane, cnt);
+        const Hit h = closest_hit<kBvh>(S, ray, inv, live, W, stack, lane, cnt);
         if (!live) continue;
         ++cnt.segs;
 
@@ -523,8 +527,12 @@ hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLau
     dim3 grid((L.width + 2 * L.tile_w - 1) / (2 * L.tile_w),
               (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-    hipLaunchKernelGGL(render_kernel, grid, block, 0, stream, sc.objs, sc.tris, sc.mats, sc.nodes,
-                       sc.tri_orig, sc.n_objs, cam, L, out, counters);
+    if (sc.has_bvh)
+        hipLaunchKernelGGL(render_kernel<true>, grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
+                           sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
+    else
+        hipLaunchKernelGGL(render_kernel<false>, grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
+                           sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
     return hipGetLastError();
 }
 

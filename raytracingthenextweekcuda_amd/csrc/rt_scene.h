@@ -88,6 +88,7 @@ struct SceneArgs {
     const uint32_t* tri_orig;  // mesh-local triangle index of each TriRec
     int32_t n_objs;
     int32_t n_mats;
+    bool has_bvh;  // any mesh carries a BVH (selects the kernel variant)
 };
 
 // ----------------------------------------------------------------------------
