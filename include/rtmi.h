@@ -75,6 +75,7 @@ typedef struct rt_render_stats {
     double kernel_ms;       /* duration of the render kernel (hipEvent) */
     uint32_t overflow;      /* 1 if any lane overflowed the traversal stack */
     uint32_t lanes_per_pixel; /* lane layout used by the last render */
+    uint64_t debug[8];      /* diagnostic section timers (instrumented builds only; 0 otherwise) */
 } rt_render_stats;
 
 /* ---- context (replaces initialize()/cleanup(), main.cu:555-936) ---- */

@@ -468,6 +468,7 @@ rt_status rt_sync_stats(rt_ctx* c, rt_render_stats* out) {
         c->last.node_visits = h[3];
         c->last.overflow = h[4] ? 1u : 0u;
         c->last.kernel_ms = ms;
+        for (int k = 0; k < 8; ++k) c->last.debug[k] = h[8 + k];
         c->stats_pending = false;
     }
     if (out) *out = c->last;

@@ -19,14 +19,15 @@ struct RenderLaunch {
 };
 
 // Lane-layout choice: S = lanes_per_pixel (0 = auto). Auto raises S (power of
-// two, <= spp, <= 16) until the launch has >= 2^19 lanes (8192 waves, 8 per
-// SIMD on 256 CUs x 4 SIMDs) so small shards still fill the chip.
+// two, <= spp, <= 16) until the launch has >= 2^18 lanes (4096 waves: the 4
+// resident waves per SIMD on 256 CUs x 4 SIMDs) so small shards still fill
+// the chip; a 512x512 frame on one GPU keeps S = 1 (measured best).
 inline void choose_layout(RenderLaunch& L, int32_t requested) {
     int32_t s = requested;
     if (s <= 0) {
         s = 1;
         const int64_t px = (int64_t)L.local_rows * L.width;
-        while (s < 16 && 2 * s <= L.spp && px * s < (int64_t(1) << 19)) s *= 2;
+        while (s < 16 && 2 * s <= L.spp && px * s < (int64_t(1) << 18)) s *= 2;
     }
     L.lanes_per_pixel = s;
     const int32_t p = 64 / s;
@@ -36,7 +37,8 @@ inline void choose_layout(RenderLaunch& L, int32_t requested) {
 
 // counters[0] = segments, [1] = triangle tests, [2] = mesh-box tests,
 // [3] = BVH node visits, [4] = traversal overflow flag.
-constexpr int kNumCounters = 8;
+// [8..15] = diagnostic section timers (RT_STAMPS builds only).
+constexpr int kNumCounters = 16;
 
 hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLaunch& L,
                          float* out, unsigned long long* counters, hipStream_t stream);

@@ -87,8 +87,8 @@ __device__ __forceinline__ bool sphere_root(v3 o, v3 d, v3 c, float r, float tmi
     float cc = dot(oc, oc) - r * r;
     float disc = hb * hb - a * cc;
     if (!(disc > kFltEpsilon)) return false;
-    float inva = 1.0f / a;
-    float sq = sqrtf(disc);
+    float inva = fdiv(1.0f, a);
+    float sq = fsqrt(disc);
     float t = (-hb - sq) * inva;
     if (t < tmin || tmax < t) {
         t = (-hb + sq) * inva;
@@ -123,7 +123,7 @@ __device__ __forceinline__ float tri_t(const TriRec& tr, v3 o, v3 d) {
     v3 s = sub(o, v3{tr.v0x, tr.v0y, tr.v0z});
     v3 s1 = cross(d, e2);
     v3 s2 = cross(s, e1);
-    float coef = 1.0f / dot(s1, e1);
+    float coef = fdiv(1.0f, dot(s1, e1));
     float t = coef * dot(s2, e2);
     float b1 = coef * dot(s1, s);
     float b2 = coef * dot(s2, d);
@@ -147,6 +147,23 @@ struct WaveLds {
 struct Counters {
     uint32_t segs, tri_tests, box_tests, node_visits, overflow;
 };
+
+// Diagnostic build only (RT_STAMPS): wave-uniform s_memtime section timers,
+// summed per wave into counters[8..15]. Never enabled in shipped builds.
+#ifdef RT_STAMPS
+__device__ __forceinline__ uint64_t stamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define RT_STAMP(var) const uint64_t var = stamp()
+#define RT_ACC(slot, a, b) (tm[slot] += (b) - (a))
+#else
+#define RT_STAMP(var)
+#define RT_ACC(slot, a, b)
+#endif
 
 // The lane's rank among the set bits of `mask` below it.
 __device__ __forceinline__ int lane_rank(uint64_t mask) {
@@ -254,53 +271,94 @@ __device__ __forceinline__ void mesh_bvh(const TriRec* __restrict__ tris,
 // hit() over the flattened object table (main.cu:43-57): closest so far is
 // passed as tMax to each object, each object's own comparison rule is kept.
 // Called with the whole wave active; `live` masks lanes without a path.
+// One object record as a single wave-uniform 64 B scalar load.
+__device__ __forceinline__ ObjRec load_obj(const ObjRec* __restrict__ objs, int i) {
+    const uint4* q = reinterpret_cast<const uint4*>(objs + i);
+    const uint4 a = q[0], b = q[1], c = q[2], e = q[3];
+    ObjRec r;
+    r.type = a.x;
+    r.material = a.y;
+    r.u0 = a.z;
+    r.u1 = a.w;
+    r.u2 = b.x;
+    r.f[0] = __uint_as_float(b.y);
+    r.f[1] = __uint_as_float(b.z);
+    r.f[2] = __uint_as_float(b.w);
+    r.f[3] = __uint_as_float(c.x);
+    r.f[4] = __uint_as_float(c.y);
+    r.f[5] = __uint_as_float(c.z);
+    r.f[6] = __uint_as_float(c.w);
+    r.f[7] = __uint_as_float(e.x);
+    r.f[8] = __uint_as_float(e.y);
+    r.f[9] = __uint_as_float(e.z);
+    r.f[10] = __uint_as_float(e.w);
+    return r;
+}
+
+// hit() over the flattened object table (main.cu:43-57): closest so far is
+// passed as tMax to each object, each object's own comparison rule is kept.
+// Called with the whole wave active; `live` masks lanes without a path.
+// Records are fetched one object ahead (scalar loads overlap the current
+// object's VALU work); per-object tests are branch-free selects.
 template <bool kBvh>
 __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v3 inv, bool live,
-                                           WaveLds& W, uint32_t* stack, int lane, Counters& cnt) {
+                                           WaveLds& W, uint32_t* stack, int lane, Counters& cnt
+#ifdef RT_STAMPS
+                                           , uint64_t* tm
+#endif
+                                           ) {
     Hit h{kInf, -1, -1};
     const v3 o = ray.o, d = ray.d;
-    const ObjRec* __restrict__ objs = S.objs;
-    for (int i = 0; i < S.n_objs; ++i) {
-        const uint32_t type = objs[i].type;
-        const float* f = objs[i].f;
-        if (type == kObjPlane) {
-            // Plane::hit (Plane.cu:4-52).
-            v3 n{f[3], f[4], f[5]};
-            float den = dot(n, d);
-            bool proceed = objs[i].u1 ? (fabsf(den) > kTMin) : (den > kTMin);
-            if (proceed) {
-                float t = dot(sub(v3{f[0], f[1], f[2]}, o), n) / den;
-                v3 p = add(o, scale(d, t));
-                if ((t >= kTMin) && (t < h.t) && plane_in_range(p, f, objs[i].u0)) {
-                    h.t = t;
-                    h.obj = i;
-                }
-            }
-        } else if (type == kObjSphere) {
-            float t;
-            if (sphere_root(o, d, v3{f[0], f[1], f[2]}, f[3], kTMin, h.t, t)) {
-                h.t = t;
-                h.obj = i;
-            }
-        } else if (type == kObjMovingSphere) {
-            float t;
-            if (sphere_root(o, d, moving_center(f, ray.time), f[8], kTMin, h.t, t)) {
-                h.t = t;
-                h.obj = i;
-            }
+    const int n = S.n_objs;
+    ObjRec cur = load_obj(S.objs, 0);
+    for (int i = 0; i < n; ++i) {
+        const ObjRec ob = cur;
+        if (i + 1 < n) cur = load_obj(S.objs, i + 1);
+        const float* f = ob.f;
+        if (ob.type == kObjPlane) {
+            // Plane::hit (Plane.cu:4-52); t is only used when `proceed` holds.
+            const v3 nrm{f[3], f[4], f[5]};
+            const float den = dot(nrm, d);
+            const bool proceed = ob.u1 ? (fabsf(den) > kTMin) : (den > kTMin);
+            const float t = fdiv(dot(sub(v3{f[0], f[1], f[2]}, o), nrm), den);
+            const v3 p = add(o, scale(d, t));
+            bool in;
+            if (ob.u0 == 0u)
+                in = (p.x > f[0] - f[6]) & (p.x < f[0] + f[6]) & (p.y > f[1] - f[7]) & (p.y < f[1] + f[7]);
+            else if (ob.u0 == 1u)
+                in = (p.y > f[1] - f[7]) & (p.y < f[1] + f[7]) & (p.z > f[2] - f[8]) & (p.z < f[2] + f[8]);
+            else
+                in = (p.x > f[0] - f[6]) & (p.x < f[0] + f[6]) & (p.z > f[2] - f[8]) & (p.z < f[2] + f[8]);
+            const bool acc = proceed & (t >= kTMin) & (t < h.t) & in;
+            h.t = acc ? t : h.t;
+            h.obj = acc ? i : h.obj;
+        } else if (ob.type == kObjSphere) {
+            float t = 0.0f;
+            const bool acc = sphere_root(o, d, v3{f[0], f[1], f[2]}, f[3], kTMin, h.t, t);
+            h.t = acc ? t : h.t;
+            h.obj = acc ? i : h.obj;
+        } else if (ob.type == kObjMovingSphere) {
+            float t = 0.0f;
+            const bool acc = sphere_root(o, d, moving_center(f, ray.time), f[8], kTMin, h.t, t);
+            h.t = acc ? t : h.t;
+            h.obj = acc ? i : h.obj;
         } else {
             // TriangleMesh::hit (TriangleMesh.cu:34-117): the AABB early-out
             // gates the triangle scan exactly as in the reference.
             const bool want = live && box_hit(f, o, inv);
-            const uint32_t root = objs[i].u2;
+            const uint32_t root = ob.u2;
             if (live) {
                 ++cnt.box_tests;
-                if (want && root == kNoBvh) cnt.tri_tests += objs[i].u1;
+                if (want && root == kNoBvh) cnt.tri_tests += ob.u1;
             }
-            if (!kBvh || root == kNoBvh)
-                mesh_compact(S.tris, objs[i].u0, objs[i].u1, want, o, d, h, i, W, lane);
-            else
+            if (!kBvh || root == kNoBvh) {
+                RT_STAMP(t_m0);
+                mesh_compact(S.tris, ob.u0, ob.u1, want, o, d, h, i, W, lane);
+                RT_STAMP(t_m1);
+                RT_ACC(3, t_m0, t_m1);
+            } else {
                 mesh_bvh(S.tris, S.tri_orig, S.nodes, root, want, o, d, inv, h, i, stack, cnt);
+            }
         }
     }
     return h;
@@ -365,15 +423,19 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     Rng rng{1u, 0u, 0u, 0u};
     const float fw = (float)(L.width - 1), fh = (float)(L.height - 1);
 
+#ifdef RT_STAMPS
+    uint64_t tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     for (;;) {
         if (__ballot(alive) == 0) break;  // wave-uniform exit
+        RT_STAMP(t_a);
         if (alive && need_cam) {
             // renderKernel sample loop body (main.cu:179-185) + getRay (Camera.h:151-168).
             rng.begin(L.seed, pixel, L.sample_offset + (uint32_t)s);
             float rx = rng.next();
             float ry = rng.next();
-            float dx = ((float)px + rx) / fw;
-            float dy = ((float)y + ry) / fh;
+            float dx = fdiv((float)px + rx, fw);
+            float dy = fdiv((float)y + ry, fh);
             v3 disk = random_in_unit_disk(rng);
             v3 rnd = scale(disk, cam.lens_radius);
             v3 offset = add(scale(cam.right, rnd.x), scale(cam.true_up, rnd.y));
@@ -393,9 +455,17 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
             }
         }
         const bool live = alive && !need_cam;
+        RT_STAMP(t_b);
+        RT_ACC(0, t_a, t_b);
 
         const v3 inv = rcp(ray.d);
-        const Hit h = closest_hit<kBvh>(S, ray, inv, live, W, stack, lane, cnt);
+        const Hit h = closest_hit<kBvh>(S, ray, inv, live, W, stack, lane, cnt
+#ifdef RT_STAMPS
+                                        , tm
+#endif
+        );
+        RT_STAMP(t_c);
+        RT_ACC(1, t_b, t_c);
         if (!live) continue;
         ++cnt.segs;
 
@@ -486,6 +556,12 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
             s += SP;
             if (s >= L.spp) alive = false;
         }
+#ifdef RT_STAMPS
+        {
+            RT_STAMP(t_d);
+            RT_ACC(2, t_c, t_d);
+        }
+#endif
     }
 
     // Fixed-order combination of the SP partial sums: ((p0 + p1) + p2) + ...
@@ -512,6 +588,10 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     const uint64_t wb = wave_sum_u64(cnt.box_tests);
     const uint64_t wn = wave_sum_u64(cnt.node_visits);
     const uint64_t wo = wave_sum_u64(cnt.overflow);
+#ifdef RT_STAMPS
+    if (lane == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd(&counters[8 + k], (unsigned long long)tm[k]);
+#endif
     if (lane == 0) {
         atomicAdd(&counters[0], (unsigned long long)ws);
         atomicAdd(&counters[1], (unsigned long long)wt);

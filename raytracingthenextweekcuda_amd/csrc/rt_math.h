@@ -23,6 +23,16 @@ namespace rt {
 constexpr float kFltEpsilon = 1.19209290e-07f;  // FLT_EPSILON (HitResult.h:16, TriangleMesh.cu:72)
 constexpr float kTMin = 0.001f;                 // Math::epsilon (Constants.h:23), rayColor tMin (main.cu:69)
 
+// IEEE division / square root. RT_ABL_FASTMATH (timing ablation builds only,
+// never shipped: results differ) swaps in v_rcp_f32 / v_sqrt_f32.
+#if defined(__HIP_DEVICE_COMPILE__) && defined(RT_ABL_FASTMATH)
+RT_HD float fdiv(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+RT_HD float fsqrt(float a) { return __builtin_amdgcn_sqrtf(a); }
+#else
+RT_HD float fdiv(float a, float b) { return a / b; }
+RT_HD float fsqrt(float a) { return sqrtf(a); }
+#endif
+
 struct v3 {
     float x, y, z;
 };
@@ -34,7 +44,7 @@ RT_HD v3 sub(v3 a, v3 b) { return v3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 RT_HD v3 mul(v3 a, v3 b) { return v3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 // v * s and s * v are both evaluated as (v.x*s, v.y*s, v.z*s) (LinearAlgebra.h:35,61-63).
 RT_HD v3 scale(v3 a, float s) { return v3{a.x * s, a.y * s, a.z * s}; }
-RT_HD v3 divs(v3 a, float s) { return v3{a.x / s, a.y / s, a.z / s}; }
+RT_HD v3 divs(v3 a, float s) { return v3{fdiv(a.x, s), fdiv(a.y, s), fdiv(a.z, s)}; }
 RT_HD v3 neg(v3 a) { return v3{-a.x, -a.y, -a.z}; }
 // float + Vector3Df -> (b.x + a, ...) (LinearAlgebra.h:65-67, 39).
 RT_HD v3 adds(v3 a, float s) { return v3{a.x + s, a.y + s, a.z + s}; }
@@ -45,10 +55,10 @@ RT_HD v3 cross(v3 a, v3 b) {
 }
 // normalize(v): norm = sqrtf(x*x+y*y+z*z); (x/norm, y/norm, z/norm) (LinearAlgebra.h:69-72).
 RT_HD v3 normalize(v3 a) {
-    float n = sqrtf(a.x * a.x + a.y * a.y + a.z * a.z);
-    return v3{a.x / n, a.y / n, a.z / n};
+    float n = fsqrt(a.x * a.x + a.y * a.y + a.z * a.z);
+    return v3{fdiv(a.x, n), fdiv(a.y, n), fdiv(a.z, n)};
 }
-RT_HD v3 rcp(v3 a) { return v3{1.0f / a.x, 1.0f / a.y, 1.0f / a.z}; }
+RT_HD v3 rcp(v3 a) { return v3{fdiv(1.0f, a.x), fdiv(1.0f, a.y), fdiv(1.0f, a.z)}; }
 RT_HD float minf_(float a, float b) { return a < b ? a : b; }
 RT_HD float maxf_(float a, float b) { return a > b ? a : b; }
 
@@ -81,7 +91,10 @@ RT_HD u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
 #if defined(__HIPCC__)
 #pragma unroll
 #endif
-    for (int r = 0; r < 10; ++r) {
+#ifndef RT_ABL_PHILOX_ROUNDS
+#define RT_ABL_PHILOX_ROUNDS 10  // ablation builds only
+#endif
+    for (int r = 0; r < RT_ABL_PHILOX_ROUNDS; ++r) {
         uint32_t hi0, lo0, hi1, lo1;
         mulhilo(kPhiloxM0, c.x, hi0, lo0);
         mulhilo(kPhiloxM1, c.z, hi1, lo1);

@@ -216,7 +216,9 @@ class Renderer:
     def stats(self) -> dict:
         s = RenderStats()
         self._check(self.L.rt_sync_stats(self.ctx, C.byref(s)))
-        return {k: getattr(s, k) for k, _ in RenderStats._fields_}
+        d = {k: getattr(s, k) for k, _ in RenderStats._fields_}
+        d["debug"] = list(s.debug)
+        return d
 
 
 def owned_rows(height, block, rank, world) -> int:

@@ -175,6 +175,8 @@ def test_auto_lane_layout_fills_small_shards(rtmi):
         rtmi.cornell_box1(r, 64, 64)
         r.render(64, 64, 32, 4, lanes_per_pixel=0)
         assert r.stats()["lanes_per_pixel"] == 16
+        r.render(512, 512, 2, 1, lanes_per_pixel=0)
+        assert r.stats()["lanes_per_pixel"] == 1
 
 
 @pytest.mark.parametrize("name,w,h,spp", [("bunny_small_cornellbox.yaml", 48, 48, 4),
