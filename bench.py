@@ -99,27 +99,42 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    # RTMI_REHEARSAL=1 (testing only): N ranks share GPU 0 and gather over gloo
+    # through host memory, to exercise the N > 1 code path on a one-GPU box.
+    rehearsal = os.environ.get("RTMI_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import raytracingthenextweekcuda_amd as rtmi
 
     W, H = args.width, args.height
     r = rtmi.Renderer(device=local)
     rtmi.cornell_box1(r, W, H)
+    from raytracingthenextweekcuda_amd.distributed import RowShardedFrame
+
     block = args.row_block
     rows = rtmi.owned_rows(H, block, rank, world)
-    max_rows = max(rtmi.owned_rows(H, block, k, world) for k in range(world))
-    out = torch.zeros((max_rows, W, 3), dtype=torch.float32, device="cuda")
-    gather = [torch.empty_like(out) for _ in range(world)] if (rank == 0 and world > 1) else None
+    frame = RowShardedFrame(W, H, block,
+                            device=torch.device("cpu") if rehearsal else torch.device("cuda", local))
     params = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, world, args.lanes)
     stream = torch.cuda.current_stream()
+    scratch = torch.empty(frame.tile.shape, dtype=torch.float32, device="cuda") if rehearsal else None
+
+    def render_into(tile):
+        if rehearsal:
+            r.render_device(params, scratch.data_ptr(), stream.cuda_stream)
+            tile.copy_(scratch.cpu())
+        else:
+            r.render_device(params, tile.data_ptr(), stream.cuda_stream)
 
     def step():
-        r.render_device(params, out.data_ptr(), stream.cuda_stream)
-        if world > 1:
-            dist.gather(out, gather, dst=0)
+        frame.render(render_into)  # render this rank's row tiles, RCCL gather to rank 0
         return r.stats()  # waits for the kernel's end event, reads counters
 
     for _ in range(args.warmup):
@@ -142,7 +157,7 @@ def main():
 
     # max time over ranks, totals over ranks
     agg = torch.tensor([dt, float(segs), float(tri_tests), float(box_tests), float(np.mean(kern_ms)),
-                        float(rows)], dtype=torch.float64, device="cuda")
+                        float(rows)], dtype=torch.float64, device="cpu" if rehearsal else "cuda")
     if world > 1:
         tmax = agg[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)

@@ -1,0 +1,89 @@
+"""Multi-GPU frame sharding: interleaved pixel-row tiles + one gather.
+
+The reference renders on one GPU (cudaSetDevice(0), main.cu:556). Here one
+process drives one GPU (torch.distributed, backend "nccl" = RCCL over xGMI):
+
+  * rows are dealt round-robin in blocks of `row_block` rows — block k goes to
+    rank k % world — which balances the uneven cost of rows (light, glass);
+  * every rank renders its rows straight into an HBM buffer (rt_render_device);
+  * one gather moves the tiles to rank 0 (no all-reduce: each pixel has exactly
+    one owner, so there is nothing to sum), and rank 0 scatters the tile rows
+    back to frame order.
+
+The RNG stream is keyed by the global pixel index, so the assembled frame is
+bit-identical for any world size (tests/test_gpu_parity.py row-tiling test).
+The collective and assembly logic is device-agnostic and is covered on CPU
+with the gloo backend (tests/test_distributed.py).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+from .renderer import owned_row_ids, owned_rows
+
+
+def tile_rows(height: int, row_block: int, world: int) -> list:
+    """Global row ids owned by each rank, in the order the rank stores them."""
+    return [owned_row_ids(height, row_block, k, world) for k in range(world)]
+
+
+def max_tile_rows(height: int, row_block: int, world: int) -> int:
+    return max(owned_rows(height, row_block, k, world) for k in range(world))
+
+
+class RowShardedFrame:
+    """Per-rank state for rendering frames sharded by row tiles.
+
+    render_into(tile) must write this rank's owned rows (rows x W x 3 float32,
+    increasing global y) into the first rows of `tile`, a (max_rows, W, 3)
+    tensor on this rank's device. gather() returns the full (H, W, 3) frame on
+    rank 0 and None elsewhere.
+    """
+
+    def __init__(self, width: int, height: int, row_block: int, group=None, device=None):
+        import torch
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.torch = torch
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.width, self.height, self.row_block = width, height, row_block
+        self.rows = owned_rows(height, row_block, self.rank, self.world)
+        self.max_rows = max_tile_rows(height, row_block, self.world)
+        self.device = device if device is not None else torch.device("cpu")
+        self.tile = torch.zeros((self.max_rows, width, 3), dtype=torch.float32, device=self.device)
+        self.frame = None
+        self.gather_list = None
+        self.index = None
+        if self.rank == 0:
+            self.frame = torch.zeros((height, width, 3), dtype=torch.float32, device=self.device)
+            if self.world > 1:
+                self.gather_list = [torch.empty_like(self.tile) for _ in range(self.world)]
+                ids = tile_rows(height, row_block, self.world)
+                self.index = [torch.as_tensor(r, dtype=torch.long, device=self.device) for r in ids]
+
+    def gather(self) -> Optional["object"]:
+        """One gather of every rank's tile to rank 0, then de-interleave."""
+        if self.world == 1:
+            self.frame[: self.rows] = self.tile[: self.rows]
+            return self.frame
+        self.dist.gather(self.tile, self.gather_list if self.rank == 0 else None, dst=0,
+                         group=self.group)
+        if self.rank != 0:
+            return None
+        for k, rows in enumerate(self.index):
+            self.frame.index_copy_(0, rows, self.gather_list[k][: rows.numel()])
+        return self.frame
+
+    def render(self, render_into: Callable[["object"], None]):
+        render_into(self.tile)
+        return self.gather()
+
+
+def render_params_for_rank(renderer, width, height, spp, depth, row_block, rank, world, seed=1984,
+                           sample_offset=0, lanes_per_pixel=0):
+    """rt_render_params for this rank's share of the frame."""
+    return renderer.params(width, height, spp, depth, seed, sample_offset, row_block, rank, world,
+                           lanes_per_pixel)
