@@ -1,0 +1,266 @@
+// rtmi.hpp — header-only C++ facade over the C ABI (rtmi.h) that keeps the
+// reference's host-side scene API, so scene code written against
+// RayTracingTheNextWeekCUDA's kernels.h / Camera.h / Canvas.h ports with the
+// same call shapes:
+//
+//   rtmi::Context ctx(0);                                   // initialize()
+//   Material** materials = ctx.materials();                // createObjectPtrArray<Material*>
+//   Hitable** spheres = ctx.objects();
+//   createLambertianMaterial(materials, 0, Vector3Df(1, 0, 0));        // kernels.h:54
+//   createSphere(spheres, 0, {-1, 0, -1}, 0.5f, materials[0]);        // kernels.h:103
+//   Camera camera(eye, center, up, float(w) / h, 60.0f, 0.0f, 2.0f, 0.0f, 1.0f);
+//   ctx.setCamera(camera);
+//   Canvas canvas(w, h);
+//   ctx.pathTracing(canvas, spp, bounces);                  // main.cu:875-898
+//   canvas.writeToPPM("render.ppm");                        // Canvas.h:116-139
+//
+// `materials[i]` is nullptr until slot i is created (the reference's
+// `materials[id] == nullptr` guards, main.cu:714-744). Material* / Hitable*
+// are opaque non-null handles; the device data lives behind the C ABI.
+// Errors throw rtmi::Error (the reference exits the process instead).
+#pragma once
+
+#include <cstdint>
+#include <cstdio>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "rtmi.h"
+
+namespace rtmi {
+
+struct Vector3Df {
+    float x = 0, y = 0, z = 0;
+    Vector3Df() = default;
+    Vector3Df(float x_, float y_, float z_) : x(x_), y(y_), z(z_) {}
+    const float* data() const { return &x; }
+};
+
+struct Error : std::runtime_error {
+    rt_status status;
+    Error(rt_status s, const std::string& m) : std::runtime_error(m), status(s) {}
+};
+
+enum class PlaneOrientation : uint8_t { XY = RT_PLANE_XY, YZ = RT_PLANE_YZ, XZ = RT_PLANE_XZ };
+
+class Context;
+
+// The context that the reference-shaped factories act on: set by
+// Context::materials() / objects() (the tables the factories receive).
+inline Context*& table_owner() {
+    static thread_local Context* owner = nullptr;
+    return owner;
+}
+
+// Opaque device-object handles (stand-ins for the reference's device pointers).
+struct Handle {
+    Context* ctx;
+    int32_t index;
+};
+using Material = Handle;
+using Hitable = Handle;
+
+// Camera (Camera.h:14-34): parameters only; the view basis is derived by the
+// library exactly like Camera::updateViewMatrix.
+struct Camera {
+    Vector3Df eye, center, up;
+    float aspectRatio = 1.0f, fov = 90.0f, aperture = 2.0f, focusDistance = 1.0f;
+    float time0 = 0.0f, time1 = 0.0f;
+    Camera() = default;
+    Camera(const Vector3Df& e, const Vector3Df& c, const Vector3Df& u, float aspect, float fov_ = 90.0f,
+           float aperture_ = 2.0f, float focus = 1.0f, float t0 = 0.0f, float t1 = 0.0f) {
+        initialize(e, c, u, aspect, fov_, aperture_, focus, t0, t1);
+    }
+    void initialize(const Vector3Df& e, const Vector3Df& c, const Vector3Df& u, float aspect,
+                    float fov_ = 90.0f, float aperture_ = 2.0f, float focus = 1.0f, float t0 = 0.0f,
+                    float t1 = 0.0f) {
+        eye = e; center = c; up = u; aspectRatio = aspect; fov = fov_; aperture = aperture_;
+        focusDistance = focus; time0 = t0; time1 = t1;
+    }
+};
+
+// Canvas (Canvas.h): float mean radiance (row 0 = bottom) + gamma'd 8-bit output.
+class Canvas {
+public:
+    Canvas(int32_t w, int32_t h) : width(w), height(h), radiance((size_t)w * h * 3, 0.0f) {}
+    int32_t getWidth() const { return width; }
+    int32_t getHeight() const { return height; }
+    float* data() { return radiance.data(); }
+    const float* data() const { return radiance.data(); }
+    std::vector<uint8_t> pixels() const {
+        std::vector<uint8_t> px(radiance.size());
+        rt_status s = rt_gamma_u8(radiance.data(), (int64_t)radiance.size(), px.data());
+        if (s != RT_OK) throw Error(s, "rt_gamma_u8");
+        return px;
+    }
+    // writeToPPM (Canvas.h:116-139): top row first.
+    void writeToPPM(const std::string& path) const {
+        std::vector<uint8_t> px = pixels();
+        FILE* f = std::fopen(path.c_str(), "wb");
+        if (!f) throw Error(RT_ERR_IO, "cannot write " + path);
+        std::fprintf(f, "P6\n%d %d\n255\n", width, height);
+        for (int32_t y = height - 1; y >= 0; --y) std::fwrite(&px[(size_t)y * width * 3], 1, (size_t)width * 3, f);
+        std::fclose(f);
+    }
+
+private:
+    int32_t width, height;
+    std::vector<float> radiance;
+};
+
+class Context {
+public:
+    explicit Context(int32_t device = 0) {
+        rt_status s = rt_create(device, &ctx_);
+        if (s != RT_OK) throw Error(s, "rt_create failed");
+    }
+    ~Context() {
+        if (table_owner() == this) table_owner() = nullptr;
+        rt_destroy(ctx_);
+    }
+    Context(const Context&) = delete;
+    Context& operator=(const Context&) = delete;
+
+    rt_ctx* raw() const { return ctx_; }
+    void check(rt_status s) const {
+        if (s != RT_OK) throw Error(s, rt_last_error(ctx_));
+    }
+
+    // Pointer tables (createObjectPtrArray<Material*> / <Hitable*>, kernels.h:26-31).
+    Material** materials(int32_t n = 4096) {
+        table_owner() = this;
+        return table(mat_slots_, mat_ptrs_, n, true);
+    }
+    Hitable** objects(int32_t n = 4096) {
+        table_owner() = this;
+        return table(obj_slots_, obj_ptrs_, n, false);
+    }
+
+    void setCamera(const Camera& c) {
+        check(rt_camera(ctx_, c.eye.data(), c.center.data(), c.up.data(), c.aspectRatio, c.fov,
+                        c.aperture, c.focusDistance, c.time0, c.time1));
+    }
+    void commit() { check(rt_commit(ctx_)); }
+
+    // pathTracing (main.cu:875-898): one frame of `spp` samples into the canvas.
+    void pathTracing(Canvas& canvas, int32_t spp, int32_t bounces, uint32_t seed = 1984,
+                     uint32_t sampleOffset = 0) {
+        commit();
+        rt_render_params p{canvas.getWidth(), canvas.getHeight(), spp, bounces, seed, sampleOffset, 1, 0, 1, 0};
+        check(rt_render(ctx_, &p, canvas.data()));
+    }
+
+    // called by the factories below
+    void markMaterial(int32_t i) { slot(mat_slots_, mat_ptrs_, i, true); }
+    void markObject(int32_t i) { slot(obj_slots_, obj_ptrs_, i, false); }
+
+private:
+    Material** table(std::vector<std::unique_ptr<Material>>& slots, std::vector<Material*>& ptrs,
+                     int32_t n, bool) {
+        if ((int32_t)ptrs.size() < n) {
+            ptrs.resize(n, nullptr);
+            slots.resize(n);
+        }
+        return ptrs.data();
+    }
+    void slot(std::vector<std::unique_ptr<Material>>& slots, std::vector<Material*>& ptrs, int32_t i, bool) {
+        // Tables are fixed-size once handed out (growing them would invalidate
+        // the caller's Material** / Hitable**), like createObjectPtrArray(n).
+        if (i < 0 || i >= (int32_t)ptrs.size()) throw Error(RT_ERR_INVALID, "slot index beyond table size");
+        if (!slots[i]) slots[i].reset(new Material{this, i});
+        ptrs[i] = slots[i].get();
+    }
+
+    rt_ctx* ctx_ = nullptr;
+    std::vector<std::unique_ptr<Material>> mat_slots_, obj_slots_;
+    std::vector<Material*> mat_ptrs_, obj_ptrs_;
+};
+
+namespace detail {
+inline int32_t mat_index(Material* m) {
+    if (!m) throw Error(RT_ERR_INVALID, "material is nullptr");
+    return m->index;
+}
+}  // namespace detail
+
+// ---- kernels.h factories (same names and argument order) ----
+// They act on the context whose tables were handed out last (table_owner()).
+
+inline void createLambertianMaterial(Material** materials, int32_t index, Vector3Df albedo, float absorb = 1.0f) {
+    Context& c = *table_owner();
+    c.check(rt_material_lambertian(c.raw(), index, albedo.data(), absorb));
+    c.markMaterial(index);
+    (void)materials;
+}
+inline void createMetalMaterial(Material** materials, int32_t index, Vector3Df albedo, float fuzz = 1.0f) {
+    Context& c = *table_owner();
+    c.check(rt_material_metal(c.raw(), index, albedo.data(), fuzz));
+    c.markMaterial(index);
+    (void)materials;
+}
+inline void createDieletricMaterial(Material** materials, int32_t index, float indexOfRefraction = 1.5f) {
+    Context& c = *table_owner();
+    c.check(rt_material_dielectric(c.raw(), index, indexOfRefraction));
+    c.markMaterial(index);
+    (void)materials;
+}
+inline void createEmissionMaterial(Material** materials, int32_t index, Vector3Df albedo, float intensity = 1.0f) {
+    Context& c = *table_owner();
+    c.check(rt_material_emission(c.raw(), index, albedo.data(), intensity));
+    c.markMaterial(index);
+    (void)materials;
+}
+inline void createSphere(Hitable** spheres, int32_t index, Vector3Df center, float radius, Material* material,
+                         bool bShading = true) {
+    Context& c = *table_owner();
+    c.check(rt_sphere(c.raw(), index, center.data(), radius, detail::mat_index(material), bShading));
+    c.markObject(index);
+    (void)spheres;
+}
+inline void createMovingSphere(Hitable** spheres, int32_t index, Vector3Df center0, Vector3Df center1, float time0,
+                               float time1, float radius, Material* material) {
+    Context& c = *table_owner();
+    c.check(rt_moving_sphere(c.raw(), index, center0.data(), center1.data(), time0, time1, radius,
+                             detail::mat_index(material)));
+    c.markObject(index);
+    (void)spheres;
+}
+inline void createPlane(Hitable** planes, int32_t index, const Vector3Df& position, const Vector3Df& normal,
+                        const Vector3Df& extend, Material* material, PlaneOrientation orientation,
+                        bool bTwoSide = true) {
+    Context& c = *table_owner();
+    c.check(rt_plane(c.raw(), index, position.data(), normal.data(), extend.data(), detail::mat_index(material),
+                     (int32_t)orientation, bTwoSide));
+    c.markObject(index);
+    (void)planes;
+}
+inline void createCube(Hitable** cubes, int32_t index, const Vector3Df& center, const Vector3Df& extend,
+                       Material* material) {
+    Context& c = *table_owner();
+    c.check(rt_cube(c.raw(), index, center.data(), extend.data(), detail::mat_index(material)));
+    c.markObject(index);
+    (void)cubes;
+}
+// createTriangleMeshData + createMesh (main.cu:384-401, kernels.h:126-133) from
+// world-space triangle vertices (loadModel(...).vertices, 3 per triangle).
+inline void createMesh(Hitable** meshes, int32_t index, const std::vector<Vector3Df>& vertices,
+                       Material* material) {
+    Context& c = *table_owner();
+    c.check(rt_mesh(c.raw(), index, vertices.empty() ? nullptr : &vertices[0].x, (int32_t)(vertices.size() / 3),
+                    detail::mat_index(material)));
+    c.markObject(index);
+    (void)meshes;
+}
+// loadModel(file, scale, rotate, offset) + createMesh in one call.
+inline void createMeshFromOBJ(Hitable** meshes, int32_t index, const std::string& path, Vector3Df scale,
+                              Vector3Df rotate, Vector3Df offset, Material* material) {
+    Context& c = *table_owner();
+    c.check(rt_mesh_obj(c.raw(), index, path.c_str(), scale.data(), rotate.data(), offset.data(),
+                        detail::mat_index(material)));
+    c.markObject(index);
+    (void)meshes;
+}
+
+}  // namespace rtmi
