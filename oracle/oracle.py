@@ -237,3 +237,29 @@ def yaml_scene(path: str, models_dir: str, width: int, height: int) -> OracleSce
             else:
                 sc.mesh_obj(i, model, obj["scale"], obj["rotate"], obj["offset"], 3)
     return sc
+
+
+def json_scene(path: str, width: int, height: int) -> OracleScene:
+    """Object-list scenes (assets/scenes/random_spheres.json): one material per
+    object slot, as the reference's SCENE 2 code (main.cu:792-848)."""
+    import json
+
+    with open(path) as fh:
+        d = json.load(fh)
+    sc = OracleScene()
+    c = d["camera"]
+    aspect = float(np.float32(width) / np.float32(height))
+    sc.camera(c["eye"], c["center"], c["up"], aspect, float(c["fov"]), float(c["aperture"]),
+              float(c["focus"]), float(c.get("time0", 0.0)), float(c.get("time1", 0.0)))
+    kinds = {"lambertian": 0, "metal": 1, "dielectric": 2, "emission": 3}
+    for i, o in enumerate(d["objects"]):
+        m = o["material"]
+        k = kinds[m["type"]]
+        param = {0: 1.0, 1: m.get("fuzz", 0.0), 2: m.get("ior", 1.5), 3: m.get("intensity", 1.0)}[k]
+        sc.material(i, k, m.get("albedo", (1, 1, 1)), float(param))
+        if o["kind"] == "sphere":
+            sc.sphere(i, o["center"], float(o["radius"]), i)
+        else:
+            sc.moving_sphere(i, o["center0"], o["center1"], float(o["time0"]), float(o["time1"]),
+                             float(o["radius"]), i)
+    return sc

@@ -11,4 +11,6 @@ from .renderer import (  # noqa: F401
     createEmissionMaterial, createLambertianMaterial, createMesh, createMetalMaterial,
     createMovingSphere, createPlane, createSphere, gamma_u8, owned_row_ids, owned_rows,
 )
-from .scene import bunny_cornell_box, cornell_box1, load_yaml_scene  # noqa: F401
+from .scene import (  # noqa: F401
+    bunny_cornell_box, cornell_box1, load_json_scene, load_yaml_scene, random_spheres,
+)

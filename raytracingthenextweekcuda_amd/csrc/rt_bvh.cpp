@@ -222,20 +222,17 @@ void process_ply_vertices(PlyMesh& m, v3 offset, float max_coord) {
     }
 }
 
-void build_cf_bvh(const std::vector<v3>& vertices, const std::vector<uint32_t>& indices,
-                  CFBvh& out) {
-    // CreateBVH (BVH.cpp:335-392).
-    const size_t nt = indices.size() / 3;
+void build_cf_bvh_boxes(const std::vector<v3>& bottoms, const std::vector<v3>& tops, CFBvh& out) {
+    // CreateBVH (BVH.cpp:335-392) over precomputed primitive boxes.
+    const size_t nt = bottoms.size();
     std::vector<Entry> work;
     work.reserve(nt);
     v3 bottom{FLT_MAX, FLT_MAX, FLT_MAX}, top{-FLT_MAX, -FLT_MAX, -FLT_MAX};
     for (size_t j = 0; j < nt; ++j) {
         Entry b;
         b.tri = (int32_t)j;
-        b.bottom = v3{FLT_MAX, FLT_MAX, FLT_MAX};
-        b.top = v3{-FLT_MAX, -FLT_MAX, -FLT_MAX};
-        for (int k = 0; k < 3; ++k) b.bottom = min3v(b.bottom, vertices[indices[3 * j + k]]);
-        for (int k = 0; k < 3; ++k) b.top = max3v(b.top, vertices[indices[3 * j + k]]);
+        b.bottom = bottoms[j];
+        b.top = tops[j];
         bottom = min3v(bottom, b.bottom);
         top = max3v(top, b.top);
         b.center = scale(add(b.top, b.bottom), 0.5f);
@@ -247,13 +244,27 @@ void build_cf_bvh(const std::vector<v3>& vertices, const std::vector<uint32_t>& 
     B.pool[root].bottom = bottom;
     B.pool[root].top = top;
     // CreateCFBVH (BVH.cpp:467-497).
-    size_t nboxes = B.pool.size();
-    out.nodes.assign(nboxes, CFNode{});
+    out.nodes.assign(B.pool.size(), CFNode{});
     out.tri_index.clear();
     out.tri_index.reserve(nt);
     out.max_depth = 0;
     uint32_t idx = 0;
     B.populate(root, idx, out, 0);
+}
+
+void build_cf_bvh(const std::vector<v3>& vertices, const std::vector<uint32_t>& indices,
+                  CFBvh& out) {
+    // Per-triangle boxes: min3/max3 over the three vertices from FLT_MAX seeds.
+    const size_t nt = indices.size() / 3;
+    std::vector<v3> lo(nt), hi(nt);
+    for (size_t j = 0; j < nt; ++j) {
+        v3 b{FLT_MAX, FLT_MAX, FLT_MAX}, t{-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (int k = 0; k < 3; ++k) b = min3v(b, vertices[indices[3 * j + k]]);
+        for (int k = 0; k < 3; ++k) t = max3v(t, vertices[indices[3 * j + k]]);
+        lo[j] = b;
+        hi[j] = t;
+    }
+    build_cf_bvh_boxes(lo, hi, out);
 }
 
 std::vector<uint8_t> bvh_image(const CFBvh& b) {

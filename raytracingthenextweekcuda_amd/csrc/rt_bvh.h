@@ -50,6 +50,9 @@ struct CFBvh {
 void build_cf_bvh(const std::vector<v3>& vertices, const std::vector<uint32_t>& indices,
                   CFBvh& out);
 
+// Same builder over arbitrary primitive boxes (object-level BVH).
+void build_cf_bvh_boxes(const std::vector<v3>& bottoms, const std::vector<v3>& tops, CFBvh& out);
+
 // The `.bvh` cache image: u32 nodes, u32 indices, nodes, int32 indices.
 std::vector<uint8_t> bvh_image(const CFBvh& b);
 

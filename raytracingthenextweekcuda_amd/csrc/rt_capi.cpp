@@ -383,7 +383,7 @@ rt_status rt_commit(rt_ctx* c) {
     RT_HIP(c, up(&c->d_mats, S.mats));
     RT_HIP(c, up(&c->d_nodes, S.nodes));
     RT_HIP(c, up(&c->d_tri_orig, S.tri_orig));
-    c->n_objs = (int)S.objs.size();
+    c->n_objs = S.n_scan;
     c->n_mats = (int)S.mats.size();
     c->committed = true;
     return RT_OK;
@@ -397,7 +397,7 @@ rt_status rt_scene_info(const rt_ctx* c, int32_t out[8]) {
         if (o.type == rt::kObjPlane) ++out[0];
         else if (o.type == rt::kObjSphere) ++out[1];
         else if (o.type == rt::kObjMovingSphere) ++out[2];
-        else ++out[3];
+        else if (o.type == rt::kObjMesh) ++out[3];
     }
     out[4] = (int32_t)c->scene.tris.size();
     out[5] = (int32_t)c->scene.mats.size();

@@ -133,10 +133,47 @@ __device__ __forceinline__ float tri_t(const TriRec& tr, v3 o, v3 d) {
     return kInf;
 }
 
+// Closest-hit state with the reference's sequential tie rule (hit(),
+// main.cu:43-57, each object called with tMax = closestSoFar): planes and
+// triangles accept t < closestSoFar, spheres t <= closestSoFar (Sphere.cu:25).
+// Among candidates at the minimal t the lowest scan order wins, unless a
+// sphere of higher order is also at that t: then the highest-order such sphere
+// wins. Merging candidates in any order with this rule reproduces the
+// sequential scan, which lets BVHs visit objects out of order.
 struct Hit {
     float t;
-    int32_t obj;  // object table index of the closest hit (-1: none)
-    int32_t tri;  // triangle index for meshes
+    int32_t obj;     // winner so far by lowest order (-1: none)
+    int32_t tri;     // its triangle (meshes)
+    uint32_t mi;     // lowest order at t
+    int32_t ms_obj;  // highest-order sphere at t (-1: none)
+    uint32_t ms;     // its order
+
+    __device__ __forceinline__ void merge(float tc, uint32_t order, bool sphere, int32_t o, int32_t tr) {
+        if (tc < t) {
+            t = tc;
+            mi = order;
+            obj = o;
+            tri = tr;
+            ms_obj = sphere ? o : -1;
+            ms = order;
+        } else if (tc == t) {
+            if (order < mi) {
+                mi = order;
+                obj = o;
+                tri = tr;
+            }
+            if (sphere && (ms_obj < 0 || order > ms)) {
+                ms_obj = o;
+                ms = order;
+            }
+        }
+    }
+    __device__ __forceinline__ void finish() {
+        if (ms_obj >= 0 && ms > mi) {
+            obj = ms_obj;
+            tri = -1;
+        }
+    }
 };
 
 struct WaveLds {
@@ -177,7 +214,7 @@ __device__ __forceinline__ int lane_rank(uint64_t mask) {
 // below the caller's closestSoFar, ties resolved to the lowest triangle index.
 __device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, uint32_t base,
                                              uint32_t m, bool want, v3 o, v3 d, Hit& h, int32_t obj,
-                                             WaveLds& W, int lane) {
+                                             uint32_t order, WaveLds& W, int lane) {
     const uint64_t mask = __ballot(want);
     if (mask == 0) return;
     const int rank = lane_rank(mask);
@@ -199,7 +236,7 @@ __device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, ui
         const float rt0 = __shfl(t0, src, 64);
         if (act) {
             const float t = tri_t(tris[base + k], ro, rd);
-            if (t < rt0) {
+            if (t <= rt0) {
                 const unsigned long long key =
                     ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)k;
                 atomicMin(&W.key[r], key);
@@ -209,11 +246,9 @@ __device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, ui
     __builtin_amdgcn_wave_barrier();
     if (want) {
         const unsigned long long key = W.key[rank];
-        if (key != ~0ull) {
-            h.t = __uint_as_float((uint32_t)(key >> 32));
-            h.obj = obj;
-            h.tri = (int32_t)(base + (uint32_t)(key & 0xFFFFFFFFu));
-        }
+        if (key != ~0ull)
+            h.merge(__uint_as_float((uint32_t)(key >> 32)), order, false, obj,
+                    (int32_t)(base + (uint32_t)(key & 0xFFFFFFFFu)));
     }
     __builtin_amdgcn_wave_barrier();
 }
@@ -224,8 +259,8 @@ __device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, ui
 __device__ __forceinline__ void mesh_bvh(const TriRec* __restrict__ tris,
                                          const uint32_t* __restrict__ tri_orig,
                                          const BvhNode* __restrict__ nodes, uint32_t root, bool want,
-                                         v3 o, v3 d, v3 inv, Hit& h, int32_t obj, uint32_t* stack,
-                                         Counters& cnt) {
+                                         v3 o, v3 d, v3 inv, Hit& h, int32_t obj, uint32_t order,
+                                         uint32_t* stack, Counters& cnt) {
     if (!want) return;
     const float t0 = h.t;
     float best = t0;
@@ -241,7 +276,7 @@ __device__ __forceinline__ void mesh_bvh(const TriRec* __restrict__ tris,
             cnt.tri_tests += nt;
             for (uint32_t k = nd.a; k < nd.a + nt; ++k) {
                 const float t = tri_t(tris[k], o, d);
-                if (t < t0) {
+                if (t <= t0) {
                     const uint32_t orig = tri_orig[k];
                     if (t < best || (t == best && orig < best_orig)) {
                         best = t;
@@ -261,17 +296,11 @@ __device__ __forceinline__ void mesh_bvh(const TriRec* __restrict__ tris,
             if (hl) stack[(sp++) * 64] = nd.a;
         }
     }
-    if (best_orig != 0xFFFFFFFFu) {
-        h.t = best;
-        h.obj = obj;
-        h.tri = (int32_t)best_k;
-    }
+    if (best_orig != 0xFFFFFFFFu) h.merge(best, order, false, obj, (int32_t)best_k);
 }
 
-// hit() over the flattened object table (main.cu:43-57): closest so far is
-// passed as tMax to each object, each object's own comparison rule is kept.
-// Called with the whole wave active; `live` masks lanes without a path.
-// One object record as a single wave-uniform 64 B scalar load.
+// One object record (64 B) as a single wave-uniform scalar load; the same
+// helper serves per-lane loads of sphere-group members.
 __device__ __forceinline__ ObjRec load_obj(const ObjRec* __restrict__ objs, int i) {
     const uint4* q = reinterpret_cast<const uint4*>(objs + i);
     const uint4 a = q[0], b = q[1], c = q[2], e = q[3];
@@ -281,25 +310,69 @@ __device__ __forceinline__ ObjRec load_obj(const ObjRec* __restrict__ objs, int 
     r.u0 = a.z;
     r.u1 = a.w;
     r.u2 = b.x;
-    r.f[0] = __uint_as_float(b.y);
-    r.f[1] = __uint_as_float(b.z);
-    r.f[2] = __uint_as_float(b.w);
-    r.f[3] = __uint_as_float(c.x);
-    r.f[4] = __uint_as_float(c.y);
-    r.f[5] = __uint_as_float(c.z);
-    r.f[6] = __uint_as_float(c.w);
-    r.f[7] = __uint_as_float(e.x);
-    r.f[8] = __uint_as_float(e.y);
-    r.f[9] = __uint_as_float(e.z);
-    r.f[10] = __uint_as_float(e.w);
+    r.order = b.y;
+    r.f[0] = __uint_as_float(b.z);
+    r.f[1] = __uint_as_float(b.w);
+    r.f[2] = __uint_as_float(c.x);
+    r.f[3] = __uint_as_float(c.y);
+    r.f[4] = __uint_as_float(c.z);
+    r.f[5] = __uint_as_float(c.w);
+    r.f[6] = __uint_as_float(e.x);
+    r.f[7] = __uint_as_float(e.y);
+    r.f[8] = __uint_as_float(e.z);
+    r.f[9] = __uint_as_float(e.w);
     return r;
 }
 
-// hit() over the flattened object table (main.cu:43-57): closest so far is
-// passed as tMax to each object, each object's own comparison rule is kept.
-// Called with the whole wave active; `live` masks lanes without a path.
-// Records are fetched one object ahead (scalar loads overlap the current
-// object's VALU work); per-object tests are branch-free selects.
+// Candidate root of a (moving) sphere independent of closestSoFar: the near
+// root if >= tMin, else the far root (Sphere.cu:20-31 with tMax = +inf; the
+// sequential tMax test is applied by Hit::merge). NaN = no candidate.
+__device__ __forceinline__ float sphere_candidate(const ObjRec& ob, v3 o, v3 d, float time) {
+    const float* f = ob.f;
+    const bool moving = ob.type == kObjMovingSphere;
+    const v3 c = moving ? moving_center(f, time) : v3{f[0], f[1], f[2]};
+    const float r = moving ? f[8] : f[3];
+    float t = 0.0f;
+    return sphere_root(o, d, c, r, kTMin, kInf, t) ? t : __builtin_nanf("");
+}
+
+// Sphere group: per-lane traversal of the object BVH over the scene's spheres
+// (members are ObjRecs stored after the scan list, in leaf order).
+__device__ __forceinline__ void sphere_group(const ObjRec* __restrict__ objs,
+                                             const BvhNode* __restrict__ nodes, uint32_t root,
+                                             bool live, const Ray& ray, v3 inv, Hit& h,
+                                             uint32_t* stack, Counters& cnt) {
+    if (!live) return;
+    const v3 o = ray.o, d = ray.d;
+    stack[0] = root;
+    int sp = 1;
+    while (sp > 0) {
+        const uint32_t ni = stack[(--sp) * 64];
+        const BvhNode nd = nodes[ni];
+        ++cnt.node_visits;
+        if (nd.b & 0x80000000u) {
+            const uint32_t n = nd.b & 0x7FFFFFFFu;
+            for (uint32_t k = nd.a; k < nd.a + n; ++k) {
+                const ObjRec ob = load_obj(objs, (int)k);
+                h.merge(sphere_candidate(ob, o, d, ray.time), ob.order, true, (int32_t)k, -1);
+            }
+        } else {
+            const bool hl = node_hit(nodes[nd.a], o, inv, h.t);
+            const bool hr = node_hit(nodes[nd.b], o, inv, h.t);
+            if (sp + 2 > kStackDepth) {
+                cnt.overflow = 1;
+                break;
+            }
+            if (hr) stack[(sp++) * 64] = nd.b;
+            if (hl) stack[(sp++) * 64] = nd.a;
+        }
+    }
+}
+
+// hit() over the flattened object table (main.cu:43-57). Called with the whole
+// wave active; `live` masks lanes without a path. Records are fetched one
+// object ahead (scalar loads overlap the current object's VALU work), and the
+// per-object tests are branch-free candidates merged with Hit's tie rule.
 template <bool kBvh>
 __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v3 inv, bool live,
                                            WaveLds& W, uint32_t* stack, int lane, Counters& cnt
@@ -307,7 +380,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                                            , uint64_t* tm
 #endif
                                            ) {
-    Hit h{kInf, -1, -1};
+    Hit h{kInf, -1, -1, 0xFFFFFFFFu, -1, 0u};
     const v3 o = ray.o, d = ray.d;
     const int n = S.n_objs;
     ObjRec cur = load_obj(S.objs, 0);
@@ -329,20 +402,11 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 in = (p.y > f[1] - f[7]) & (p.y < f[1] + f[7]) & (p.z > f[2] - f[8]) & (p.z < f[2] + f[8]);
             else
                 in = (p.x > f[0] - f[6]) & (p.x < f[0] + f[6]) & (p.z > f[2] - f[8]) & (p.z < f[2] + f[8]);
-            const bool acc = proceed & (t >= kTMin) & (t < h.t) & in;
-            h.t = acc ? t : h.t;
-            h.obj = acc ? i : h.obj;
-        } else if (ob.type == kObjSphere) {
-            float t = 0.0f;
-            const bool acc = sphere_root(o, d, v3{f[0], f[1], f[2]}, f[3], kTMin, h.t, t);
-            h.t = acc ? t : h.t;
-            h.obj = acc ? i : h.obj;
-        } else if (ob.type == kObjMovingSphere) {
-            float t = 0.0f;
-            const bool acc = sphere_root(o, d, moving_center(f, ray.time), f[8], kTMin, h.t, t);
-            h.t = acc ? t : h.t;
-            h.obj = acc ? i : h.obj;
-        } else {
+            const bool ok = proceed & (t >= kTMin) & in;
+            h.merge(ok ? t : __builtin_nanf(""), ob.order, false, i, -1);
+        } else if (ob.type == kObjSphere || ob.type == kObjMovingSphere) {
+            h.merge(sphere_candidate(ob, o, d, ray.time), ob.order, true, i, -1);
+        } else if (ob.type == kObjMesh) {
             // TriangleMesh::hit (TriangleMesh.cu:34-117): the AABB early-out
             // gates the triangle scan exactly as in the reference.
             const bool want = live && box_hit(f, o, inv);
@@ -353,14 +417,17 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             }
             if (!kBvh || root == kNoBvh) {
                 RT_STAMP(t_m0);
-                mesh_compact(S.tris, ob.u0, ob.u1, want, o, d, h, i, W, lane);
+                mesh_compact(S.tris, ob.u0, ob.u1, want, o, d, h, i, ob.order, W, lane);
                 RT_STAMP(t_m1);
                 RT_ACC(3, t_m0, t_m1);
             } else {
-                mesh_bvh(S.tris, S.tri_orig, S.nodes, root, want, o, d, inv, h, i, stack, cnt);
+                mesh_bvh(S.tris, S.tri_orig, S.nodes, root, want, o, d, inv, h, i, ob.order, stack, cnt);
             }
+        } else if (kBvh) {  // kObjSphereGroup
+            sphere_group(S.objs, S.nodes, ob.u2, live, ray, inv, h, stack, cnt);
         }
     }
+    h.finish();
     return h;
 }
 

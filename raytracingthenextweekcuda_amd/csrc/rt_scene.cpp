@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <fstream>
 #include <sstream>
@@ -228,6 +229,7 @@ std::string load_obj_transformed(const std::string& path, v3 scl, v3 rot, v3 off
 
 std::string HostScene::flatten() {
     objs.clear();
+    n_scan = 0;
     tris.clear();
     mats.clear();
     nodes.clear();
@@ -345,6 +347,83 @@ std::string HostScene::flatten() {
         }
         objs.push_back(r);
     }
+    for (size_t k = 0; k < objs.size(); ++k) objs[k].order = (uint32_t)k;  // sequential scan position
+    n_scan = (int)objs.size();
+    return group_spheres();
+}
+
+// Moves the (moving) spheres of a large scene behind one kObjSphereGroup record
+// with the reference's binned-SAH builder over their boxes. The kernel merges
+// hits with the sequential scan's tie rule (ObjRec::order), so the result is
+// the same as scanning them in slot order.
+std::string HostScene::group_spheres() {
+    std::vector<ObjRec> scan, members;
+    for (const ObjRec& r : objs) {
+        if (r.type == kObjSphere || r.type == kObjMovingSphere) members.push_back(r);
+        else scan.push_back(r);
+    }
+    if (members.size() < kSphereBvhMin) return "";
+    const float t0 = has_camera ? camera.time0 : 0.0f, t1 = has_camera ? camera.time1 : 0.0f;
+    std::vector<v3> lo(members.size()), hi(members.size());
+    for (size_t k = 0; k < members.size(); ++k) {
+        const float* f = members[k].f;
+        v3 a, b;
+        float r;
+        if (members[k].type == kObjSphere) {
+            a = b = v3{f[0], f[1], f[2]};
+            r = fabsf(f[3]);
+        } else {
+            // The centre is affine in the ray time, and ray times lie in the
+            // camera's shutter interval: its endpoints bound the motion.
+            auto centre = [&](float t) {
+                const float w = (t - f[6]) / (f[7] - f[6]);
+                return v3{f[0] + w * (f[3] - f[0]), f[1] + w * (f[4] - f[1]), f[2] + w * (f[5] - f[2])};
+            };
+            a = centre(t0);
+            b = centre(t1);
+            r = fabsf(f[8]);
+        }
+        v3 l{std::min(a.x, b.x) - r, std::min(a.y, b.y) - r, std::min(a.z, b.z) - r};
+        v3 h{std::max(a.x, b.x) + r, std::max(a.y, b.y) + r, std::max(a.z, b.z) + r};
+        if (!(std::isfinite(l.x) && std::isfinite(l.y) && std::isfinite(l.z) && std::isfinite(h.x) &&
+              std::isfinite(h.y) && std::isfinite(h.z)))
+            return "sphere with non-finite bounds (degenerate moving-sphere time range?)";
+        lo[k] = l;
+        hi[k] = h;
+    }
+    CFBvh b;
+    build_cf_bvh_boxes(lo, hi, b);
+    if (b.max_depth >= kBvhStackDepth)
+        return "sphere BVH depth " + std::to_string(b.max_depth) + " exceeds the traversal stack";
+    bvh_max_depth = std::max(bvh_max_depth, b.max_depth);
+    ObjRec g{};
+    g.type = kObjSphereGroup;
+    g.order = 0xFFFFFFFFu;
+    g.u0 = (uint32_t)(scan.size() + 1);  // members follow the scan list
+    g.u1 = (uint32_t)members.size();
+    g.u2 = (uint32_t)nodes.size();
+    const uint32_t nb = (uint32_t)nodes.size();
+    for (const CFNode& c : b.nodes) {
+        BvhNode n;
+        for (int a = 0; a < 3; ++a) {
+            const float m = std::max(fabsf(c.bottom[a]), fabsf(c.top[a]));
+            const float pad = m * 1e-5f + 1e-30f;
+            n.lo[a] = c.bottom[a] - pad;
+            n.hi[a] = c.top[a] + pad;
+        }
+        if (c.u0 & 0x80000000u) {
+            n.a = g.u0 + c.u1;
+            n.b = c.u0;
+        } else {
+            n.a = nb + c.u0;
+            n.b = nb + c.u1;
+        }
+        nodes.push_back(n);
+    }
+    scan.push_back(g);
+    n_scan = (int)scan.size();
+    for (int32_t k : b.tri_index) scan.push_back(members[(size_t)k]);
+    objs.swap(scan);
     return "";
 }
 

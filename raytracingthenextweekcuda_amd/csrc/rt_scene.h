@@ -18,7 +18,13 @@
 
 namespace rt {
 
-enum ObjType : uint32_t { kObjSphere = 0, kObjMovingSphere = 1, kObjPlane = 2, kObjMesh = 3 };
+enum ObjType : uint32_t {
+    kObjSphere = 0,
+    kObjMovingSphere = 1,
+    kObjPlane = 2,
+    kObjMesh = 3,
+    kObjSphereGroup = 4  // BVH over (moving) spheres: u0 = first member, u1 = count, u2 = root
+};
 
 // One hitable (Sphere.h, Plane.h, TriangleMesh.h). Cube is flattened into its
 // six planes at build time: Cube::hit (Cube.cu:10-23) is a closest scan over its
@@ -28,16 +34,19 @@ struct alignas(16) ObjRec {
     uint32_t material;
     uint32_t u0;  // plane: orientation | mesh: first triangle
     uint32_t u1;  // plane: twoSide     | mesh: triangle count
-    uint32_t u2;  // mesh: BVH root node index, or kNoBvh (brute-force scan)
+    uint32_t u2;     // mesh / sphere group: BVH root node index, or kNoBvh (brute-force scan)
+    uint32_t order;  // position in the reference's sequential hit() scan (tie rule)
     // sphere: center xyz, radius
     // moving sphere: center0 xyz, center1 xyz, time0, time1, radius
     // plane: position xyz, normal xyz, extend xyz
     // mesh: boundsMin xyz, boundsMax xyz (computeMeshAABB, main.cu:261-281)
-    float f[11];
+    float f[10];
 };
 constexpr uint32_t kNoBvh = 0xFFFFFFFFu;
 // Meshes with more triangles than this are traversed through a BVH.
 constexpr uint32_t kBvhMinTris = 64;
+// Scenes with at least this many (moving) spheres get an object-level BVH.
+constexpr uint32_t kSphereBvhMin = 16;
 // Per-lane LDS traversal stack depth; the builder rejects deeper trees, like
 // the reference's BVH_STACK_SIZE check (BVH.cpp:490-496, CUDAPathTracer.h:43).
 constexpr int kBvhStackDepth = 32;
@@ -86,7 +95,7 @@ struct SceneArgs {
     const MatRec* mats;
     const BvhNode* nodes;
     const uint32_t* tri_orig;  // mesh-local triangle index of each TriRec
-    int32_t n_objs;
+    int32_t n_objs;            // records scanned by hit(); sphere-group members follow them
     int32_t n_mats;
     bool has_bvh;  // any mesh carries a BVH (selects the kernel variant)
 };
@@ -117,7 +126,8 @@ struct HostScene {
     CamRec camera{};
 
     // Flattened tables (valid after flatten()).
-    std::vector<ObjRec> objs;
+    std::vector<ObjRec> objs;  // scan list, then sphere-group members
+    int n_scan = 0;
     std::vector<TriRec> tris;
     std::vector<MatRec> mats;
     std::vector<BvhNode> nodes;
@@ -126,6 +136,7 @@ struct HostScene {
 
     // Returns "" on success or an error message.
     std::string flatten();
+    std::string group_spheres();
 };
 
 // Camera::initialize + updateViewMatrix (Camera.h:19-34, 86-103) on the host.

@@ -97,6 +97,52 @@ def bunny_cornell_box(r: Renderer, width: int, height: int, commit: bool = True)
                            commit=commit)
 
 
+def _material(r: Renderer, index: int, m: dict):
+    kind = m["type"]
+    if kind == "lambertian":
+        r.lambertian(index, m["albedo"])
+    elif kind == "metal":
+        r.metal(index, m["albedo"], float(m["fuzz"]))
+    elif kind == "dielectric":
+        r.dielectric(index, float(m["ior"]))
+    elif kind == "emission":
+        r.emission(index, m["albedo"], float(m["intensity"]))
+    else:
+        raise ValueError(f"unknown material {kind}")
+
+
+def load_json_scene(r: Renderer, path: str, width: int, height: int, commit: bool = True) -> Camera:
+    """Object-list scenes (one material per object slot, as in the reference's
+    SCENE 0/2 code, main.cu:592-622 / 792-848)."""
+    import json
+
+    with open(path) as fh:
+        d = json.load(fh)
+    c = d["camera"]
+    aspect = np.float32(width) / np.float32(height)
+    camera = Camera(c["eye"], c["center"], c["up"], float(aspect), float(c["fov"]), float(c["aperture"]),
+                    float(c["focus"]), float(c.get("time0", 0.0)), float(c.get("time1", 0.0)))
+    r.set_camera(camera)
+    for i, o in enumerate(d["objects"]):
+        _material(r, i, o["material"])
+        if o["kind"] == "sphere":
+            r.sphere(i, o["center"], float(o["radius"]), i)
+        elif o["kind"] == "moving_sphere":
+            r.moving_sphere(i, o["center0"], o["center1"], float(o["time0"]), float(o["time1"]),
+                            float(o["radius"]), i)
+        else:
+            raise ValueError(f"unknown object kind {o['kind']}")
+    if commit:
+        r.commit()
+    return camera
+
+
+def random_spheres(r: Renderer, width: int, height: int, commit: bool = True) -> Camera:
+    """BASELINE config 3: the RTNW final scene (488 spheres, 388 moving),
+    assets/scenes/random_spheres.json (tools/gen_random_spheres.py)."""
+    return load_json_scene(r, os.path.join(SCENES_DIR, "random_spheres.json"), width, height, commit)
+
+
 def cornell_box1(r: Renderer, width: int, height: int, commit: bool = True) -> Camera:
     """BASELINE configs 1-2: resources/scenes/cornellbox1.yaml."""
     return load_yaml_scene(r, os.path.join(SCENES_DIR, "cornellbox1.yaml"), width, height, commit=commit)

@@ -108,3 +108,30 @@ def mixed_scene():
             ("sphere", 7, (0.0, 0.1, -0.5), 0.1, 1),
         ],
     }
+
+
+def duplicate_spheres_scene(n_extra=20):
+    """Exact ties: identical spheres in several slots (the reference's inclusive
+    sphere test makes the LAST one win) next to a plane, plus enough spheres to
+    put them behind the object BVH. Materials differ per slot so a wrong tie
+    rule changes the image."""
+    objs = [
+        ("plane", 0, (0.0, -0.5, 0.0), (0.0, 1.0, 0.0), (5.0, 5.0, 5.0), 0, 2, True),
+        ("sphere", 1, (0.0, 0.0, -1.0), 0.5, 1),
+        ("sphere", 2, (0.0, 0.0, -1.0), 0.5, 2),
+        ("moving_sphere", 3, (0.6, 0.0, -1.2), (0.6, 0.0, -1.2), 0.0, 1.0, 0.3, 3),
+        ("sphere", 4, (0.6, 0.0, -1.2), 0.3, 4),
+        ("sphere", 5, (0.0, 0.0, -1.0), 0.5, 3),
+    ]
+    rng = np.random.RandomState(5)
+    for k in range(n_extra):
+        c = (float(rng.uniform(-3, 3)), float(rng.uniform(-0.4, 0.6)), float(rng.uniform(-6, -2)))
+        objs.append(("sphere", 6 + k, c, 0.1 + 0.1 * (k % 3), k % 5))
+    return {
+        "camera": ((0.0, 0.3, 1.0), (0.0, 0.0, -1.0), (0.0, 1.0, 0.0), 1.0, 50.0, 0.0, 2.0, 0.0, 1.0),
+        "materials": [
+            ("lambertian", 0, (0.5, 0.5, 0.5)), ("lambertian", 1, (0.9, 0.1, 0.1)),
+            ("metal", 2, (0.8, 0.8, 0.8), 0.1), ("dielectric", 3, 1.5), ("lambertian", 4, (0.1, 0.1, 0.9)),
+        ],
+        "objects": objs,
+    }

@@ -195,3 +195,36 @@ def test_bvh_mesh_parity(rtmi, name, w, h, spp):
     ref, ref_st = _oracle_yaml(name, w, h).render(w, h, spp, depth)
     _check(img, ref, st, ref_st, name)
     assert np.array_equal(img, ref)
+
+
+def test_random_spheres_parity(rtmi):
+    """BASELINE config 3 scene (488 spheres behind the object BVH, defocus
+    blur, motion blur) against the restatement's sequential scan."""
+    from oracle import oracle as orc
+
+    w, h, spp, depth = 96, 54, 4, 10
+    with rtmi.Renderer(0) as r:
+        rtmi.random_spheres(r, w, h)
+        assert r.object_counts()["bvh_node"] > 0
+        img = r.render(w, h, spp, depth)
+        st = r.stats()
+    assert st["overflow"] == 0 and st["node_visits"] > 0
+    ref, ref_st = orc.json_scene(os.path.join(S.SCENES, "random_spheres.json"), w, h).render(w, h, spp, depth)
+    _check(img, ref, st, ref_st, "random_spheres")
+    assert np.array_equal(img, ref)
+
+
+@pytest.mark.parametrize("n_extra", [0, 20])
+def test_exact_ties_follow_sequential_rule(rtmi, n_extra):
+    """Coincident spheres (ties in t): with and without the object BVH the
+    winner is the reference's (last sphere wins under the inclusive test)."""
+    spec = S.duplicate_spheres_scene(n_extra)
+    w, h, spp, depth = 48, 48, 2, 6
+    with rtmi.Renderer(0) as r:
+        S.build_product(r, spec)
+        assert (r.object_counts()["bvh_node"] > 0) == (n_extra >= 16)
+        img = r.render(w, h, spp, depth)
+        st = r.stats()
+    ref, ref_st = S.build_oracle(spec).render(w, h, spp, depth)
+    _check(img, ref, st, ref_st, f"ties{n_extra}")
+    assert np.array_equal(img, ref)
