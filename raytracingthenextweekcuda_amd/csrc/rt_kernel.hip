@@ -115,10 +115,11 @@ __device__ __forceinline__ bool plane_in_range(v3 p, const float* f, uint32_t or
 
 // One triangle of TriangleMesh::hit (TriangleMesh.cu:40-108) without the
 // closestSoFar comparison: returns t if every other acceptance test passes,
-// else +inf. (t < closestSoFar is applied by the caller.)
+// else NaN (compares false with anything). The caller applies closestSoFar.
 __device__ __forceinline__ float tri_t(const TriRec& tr, v3 o, v3 d) {
+    const float kNo = __builtin_nanf("");
     v3 n{tr.nx, tr.ny, tr.nz};
-    if (dot(d, n) > kFltEpsilon) return kInf;  // backface cull
+    if (dot(d, n) > kFltEpsilon) return kNo;  // backface cull
     v3 e1{tr.e1x, tr.e1y, tr.e1z}, e2{tr.e2x, tr.e2y, tr.e2z};
     v3 s = sub(o, v3{tr.v0x, tr.v0y, tr.v0z});
     v3 s1 = cross(d, e2);
@@ -130,7 +131,7 @@ __device__ __forceinline__ float tri_t(const TriRec& tr, v3 o, v3 d) {
     if (((t >= kFltEpsilon) && (t >= kTMin)) && (b1 >= kFltEpsilon) && (b2 >= kFltEpsilon) &&
         ((1.0f - b1 - b2) >= kFltEpsilon))
         return t;
-    return kInf;
+    return kNo;
 }
 
 // Closest-hit state with the reference's sequential tie rule (hit(),
