@@ -29,20 +29,37 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 BYTES = {"plane": 40, "sphere": 20, "moving_sphere": 36, "box": 24, "tri": 36, "node": 32, "pixel": 12}
 
 
+# BASELINE.json configs: scene loader, default W, H, spp, depth.
+SCENES = {
+    "cornellbox1": ("cornell_box1", 512, 512, 128, 8, "CornellBox1 (6 planes + 2 cube_small.obj meshes, 24 triangles)"),
+    "spheres": ("random_spheres", 1280, 720, 256, 10, "RTNW final scene (488 spheres, 388 moving; object BVH)"),
+    "bunny": ("bunny_cornell_box", 1024, 1024, 512, 8, "bun_zipper.ply (69,451 triangles, SAH BVH) in CornellBox1 walls"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--width", type=int, default=512)
-    ap.add_argument("--height", type=int, default=512)
-    ap.add_argument("--spp", type=int, default=128)
-    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--scene", default="cornellbox1", choices=sorted(SCENES),
+                    help="BASELINE config: cornellbox1 (2), spheres (3), bunny (4); the metric line is config 2")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--lanes", type=int, default=0, help="lanes per pixel (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-spp", type=int, default=32)
-    return ap.parse_args()
+    ap.add_argument("--cpu-spp", type=int, default=None)
+    a = ap.parse_args()
+    _, w, h, spp, depth, _ = SCENES[a.scene]
+    a.width = a.width or w
+    a.height = a.height or h
+    a.spp = a.spp or spp
+    a.depth = a.depth or depth
+    a.cpu_spp = a.cpu_spp or max(1, a.spp // 4 if a.scene == "cornellbox1" else a.spp // 64)
+    return a
 
 
 def object_bytes_per_segment(r) -> int:
@@ -59,8 +76,13 @@ def cpu_baseline(args, threads: int):
     bounded sample of the same workload: full frame at --cpu-spp spp."""
     from oracle import oracle as orc
 
-    sc = orc.yaml_scene(os.path.join(REPO, "assets", "scenes", "cornellbox1.yaml"),
-                        os.path.join(REPO, "assets", "models"), args.width, args.height)
+    scenes = os.path.join(REPO, "assets", "scenes")
+    if args.scene == "spheres":
+        sc = orc.json_scene(os.path.join(scenes, "random_spheres.json"), args.width, args.height)
+    else:
+        name = "cornellbox1.yaml" if args.scene == "cornellbox1" else "bunny_cornellbox.yaml"
+        sc = orc.yaml_scene(os.path.join(scenes, name), os.path.join(REPO, "assets", "models"),
+                            args.width, args.height)
     sc.render(64, 64, 1, args.depth, threads=threads)  # warm-up
     t0 = time.perf_counter()
     _, st = sc.render(args.width, args.height, args.cpu_spp, args.depth, threads=threads)
@@ -70,7 +92,7 @@ def cpu_baseline(args, threads: int):
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"CornellBox1 {args.width}x{args.height} spp={args.cpu_spp} depth={args.depth} "
+        "sample": (f"{args.scene} {args.width}x{args.height} spp={args.cpu_spp} depth={args.depth} "
                    f"(spp/{args.spp // max(args.cpu_spp, 1)} of the GPU frame), {dt:.2f} s wall, "
                    f"{st['segments']} segments; ms/frame scaled to spp={args.spp}: "
                    f"{dt * 1e3 * args.spp / args.cpu_spp:.0f}"),
@@ -115,7 +137,7 @@ def main():
 
     W, H = args.width, args.height
     r = rtmi.Renderer(device=local)
-    rtmi.cornell_box1(r, W, H)
+    getattr(rtmi, SCENES[args.scene][0])(r, W, H)
     from raytracingthenextweekcuda_amd.distributed import RowShardedFrame
 
     block = args.row_block
@@ -143,13 +165,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    kern_ms, segs, tri_tests, box_tests = [], 0, 0, 0
+    kern_ms, segs, tri_tests, box_tests, nodes = [], 0, 0, 0, 0
     for _ in range(args.steps):
         st = step()
         kern_ms.append(st["kernel_ms"])
         segs += st["segments"]
         tri_tests += st["tri_tests"]
         box_tests += st["box_tests"]
+        nodes += st["node_visits"]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -157,7 +180,7 @@ def main():
 
     # max time over ranks, totals over ranks
     agg = torch.tensor([dt, float(segs), float(tri_tests), float(box_tests), float(np.mean(kern_ms)),
-                        float(rows)], dtype=torch.float64, device="cpu" if rehearsal else "cuda")
+                        float(rows), float(nodes)], dtype=torch.float64, device="cpu" if rehearsal else "cuda")
     if world > 1:
         tmax = agg[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -165,7 +188,7 @@ def main():
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dt = float(tmax.item())
         segs, tri_tests, box_tests = (float(x) for x in tot[:3].tolist())
-        kmean_sum, rows_tot = float(tot[3].item()), float(tot[4].item())
+        kmean_sum, rows_tot, nodes = float(tot[3].item()), float(tot[4].item()), float(tot[5].item())
         kmean = kmean_sum / world
     else:
         kmean, rows_tot = float(np.mean(kern_ms)), float(rows)
@@ -178,9 +201,10 @@ def main():
         # (rank 0's launch stands for the per-GPU launch).
         seg_launch = segs / K / world
         alg_bytes = (seg_launch * object_bytes_per_segment(r) + tri_tests / K / world * BYTES["tri"]
-                     + box_tests / K / world * BYTES["box"] + rows_tot / world * W * BYTES["pixel"])
+                     + box_tests / K / world * BYTES["box"] + nodes / K / world * BYTES["node"]
+                     + rows_tot / world * W * BYTES["pixel"])
         achieved = alg_bytes / (kmean * 1e-3) / 1e9
-        workload = f"cornellbox1_{W}x{H}_spp{args.spp}_d{args.depth}_n{world}"
+        workload = f"{args.scene}_{W}x{H}_spp{args.spp}_d{args.depth}_n{world}"
         traffic = load_pmc_traffic(workload)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -202,7 +226,7 @@ def main():
                     "Philox RNG seed 1984)",
             "config": {
                 "workload": workload,
-                "scene": "CornellBox1 (6 planes + 2 cube_small.obj meshes, 24 triangles)",
+                "scene": SCENES[args.scene][5],
                 "width": W, "height": H, "spp": args.spp, "depth": args.depth,
                 "row_block": block, "lanes_per_pixel": int(st["lanes_per_pixel"]), "parallelism": f"row-tiles x{world} + RCCL gather" if world > 1 else "single GPU",
                 "segments_per_frame": int(segs / K),
