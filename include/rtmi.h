@@ -75,6 +75,8 @@ typedef struct rt_render_stats {
     double kernel_ms;       /* duration of the render kernel (hipEvent) */
     uint32_t overflow;      /* 1 if any lane overflowed the traversal stack */
     uint32_t lanes_per_pixel; /* lane layout used by the last render */
+    uint64_t group_sphere_tests;        /* spheres tested in object-BVH leaves */
+    uint64_t group_moving_sphere_tests; /* moving spheres tested in object-BVH leaves */
     uint64_t debug[8];      /* diagnostic section timers (instrumented builds only; 0 otherwise) */
 } rt_render_stats;
 
@@ -144,7 +146,8 @@ rt_status rt_camera(rt_ctx* ctx, const float eye[3], const float center[3], cons
 rt_status rt_commit(rt_ctx* ctx);
 /* Committed scene census: out[0] planes (cube faces included), [1] spheres,
  * [2] moving spheres, [3] meshes, [4] triangles, [5] material slots,
- * [6] BVH nodes, [7] reserved. */
+ * [6] BVH nodes, [7] spheres placed behind the object BVH (the counts
+ * [1]/[2] include them). */
 rt_status rt_scene_info(const rt_ctx* ctx, int32_t out[8]);
 
 /* ---- render (renderKernel, main.cu:160-206, launched by pathTracing 875-898) ----

@@ -53,6 +53,7 @@ class RenderStats(C.Structure):
         ("segments", C.c_uint64), ("samples", C.c_uint64), ("node_visits", C.c_uint64),
         ("tri_tests", C.c_uint64), ("box_tests", C.c_uint64), ("kernel_ms", C.c_double),
         ("overflow", C.c_uint32), ("lanes_per_pixel", C.c_uint32),
+        ("group_sphere_tests", C.c_uint64), ("group_moving_sphere_tests", C.c_uint64),
         ("debug", C.c_uint64 * 8),
     ]
 

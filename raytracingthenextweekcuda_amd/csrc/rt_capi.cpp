@@ -402,6 +402,7 @@ rt_status rt_scene_info(const rt_ctx* c, int32_t out[8]) {
     out[4] = (int32_t)c->scene.tris.size();
     out[5] = (int32_t)c->scene.mats.size();
     out[6] = (int32_t)c->scene.nodes.size();
+    out[7] = (int32_t)(c->scene.objs.size() - (size_t)c->scene.n_scan);
     return RT_OK;
 }
 
@@ -467,6 +468,8 @@ rt_status rt_sync_stats(rt_ctx* c, rt_render_stats* out) {
         c->last.box_tests = h[2];
         c->last.node_visits = h[3];
         c->last.overflow = h[4] ? 1u : 0u;
+        c->last.group_sphere_tests = h[5];
+        c->last.group_moving_sphere_tests = h[6];
         c->last.kernel_ms = ms;
         for (int k = 0; k < 8; ++k) c->last.debug[k] = h[8 + k];
         c->stats_pending = false;

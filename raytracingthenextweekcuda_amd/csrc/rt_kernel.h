@@ -36,7 +36,8 @@ inline void choose_layout(RenderLaunch& L, int32_t requested) {
 }
 
 // counters[0] = segments, [1] = triangle tests, [2] = mesh-box tests,
-// [3] = BVH node visits, [4] = traversal overflow flag.
+// [3] = BVH node visits, [4] = traversal overflow flag, [5] / [6] = spheres /
+// moving spheres tested in object-BVH leaves.
 // [8..15] = diagnostic section timers (RT_STAMPS builds only).
 constexpr int kNumCounters = 16;
 

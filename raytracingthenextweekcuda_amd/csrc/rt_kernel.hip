@@ -183,7 +183,7 @@ struct WaveLds {
 };
 
 struct Counters {
-    uint32_t segs, tri_tests, box_tests, node_visits, overflow;
+    uint32_t segs, tri_tests, box_tests, node_visits, overflow, grp_spheres, grp_moving;
 };
 
 // Diagnostic build only (RT_STAMPS): wave-uniform s_memtime section timers,
@@ -355,6 +355,8 @@ __device__ __forceinline__ void sphere_group(const ObjRec* __restrict__ objs,
             const uint32_t n = nd.b & 0x7FFFFFFFu;
             for (uint32_t k = nd.a; k < nd.a + n; ++k) {
                 const ObjRec ob = load_obj(objs, (int)k);
+                if (ob.type == kObjMovingSphere) ++cnt.grp_moving;
+                else ++cnt.grp_spheres;
                 h.merge(sphere_candidate(ob, o, d, ray.time), ob.order, true, (int32_t)k, -1);
             }
         } else {
@@ -481,7 +483,7 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     const uint32_t pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
 
     v3 sum{0.0f, 0.0f, 0.0f};
-    Counters cnt{0, 0, 0, 0, 0};
+    Counters cnt{0, 0, 0, 0, 0, 0, 0};
     int s = c;
     bool alive = valid && s < L.spp;
     bool need_cam = true;
@@ -656,6 +658,8 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     const uint64_t wb = wave_sum_u64(cnt.box_tests);
     const uint64_t wn = wave_sum_u64(cnt.node_visits);
     const uint64_t wo = wave_sum_u64(cnt.overflow);
+    const uint64_t wgs = wave_sum_u64(cnt.grp_spheres);
+    const uint64_t wgm = wave_sum_u64(cnt.grp_moving);
 #ifdef RT_STAMPS
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(&counters[8 + k], (unsigned long long)tm[k]);
@@ -666,6 +670,8 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
         atomicAdd(&counters[2], (unsigned long long)wb);
         if (wn) atomicAdd(&counters[3], (unsigned long long)wn);
         if (wo) atomicAdd(&counters[4], (unsigned long long)wo);
+        if (wgs) atomicAdd(&counters[5], (unsigned long long)wgs);
+        if (wgm) atomicAdd(&counters[6], (unsigned long long)wgm);
     }
 }
 

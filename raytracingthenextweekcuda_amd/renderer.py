@@ -185,7 +185,8 @@ class Renderer:
         """Census of the committed device tables (rt_scene_info)."""
         out = (C.c_int32 * 8)()
         self._check(self.L.rt_scene_info(self.ctx, out))
-        keys = ["plane", "sphere", "moving_sphere", "mesh", "triangle", "material", "bvh_node"]
+        keys = ["plane", "sphere", "moving_sphere", "mesh", "triangle", "material", "bvh_node",
+                "grouped_spheres"]
         return {k: int(out[i]) for i, k in enumerate(keys)}
 
     # ---- render ----
