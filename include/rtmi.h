@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define RTMI_ABI_VERSION 1
+#define RTMI_ABI_VERSION 2
 
 typedef int32_t rt_status;
 enum {
@@ -40,6 +40,11 @@ enum {
 enum { RT_LAMBERTIAN = 0, RT_METAL = 1, RT_DIELECTRIC = 2, RT_EMISSION = 3 };
 /* Plane orientation (Plane.h:5-9 PlaneOrientation). */
 enum { RT_PLANE_XY = 0, RT_PLANE_YZ = 1, RT_PLANE_XZ = 2 };
+/* Integrator run by renderKernel: rayColor (main.cu:60-113, the Hitable scene)
+ * or pathTrace (CUDAPathTracer.cu:358-622, the committed call at main.cu:187). */
+enum { RT_INTEGRATOR_RAYCOLOR = 0, RT_INTEGRATOR_PATHTRACE = 1 };
+/* pathTrace surface kinds (CUDAPathTracer.h ReflectionType). */
+enum { RT_PT_DIFFUSE = 0, RT_PT_METAL = 1, RT_PT_SPECULAR = 2, RT_PT_REFRACTION = 3, RT_PT_COAT = 4 };
 
 typedef struct rt_ctx rt_ctx;
 
@@ -64,6 +69,8 @@ typedef struct rt_render_params {
                                power of two <= 64. Partial sums are combined in a
                                fixed order, so results are deterministic for a
                                given value; 1 = the reference's sequential sum. */
+    int32_t integrator;     /* RT_INTEGRATOR_RAYCOLOR (0) or RT_INTEGRATOR_PATHTRACE (1).
+                               pathTrace bounces max_depth times (reference: 5). */
 } rt_render_params;
 
 typedef struct rt_render_stats {
@@ -135,6 +142,22 @@ rt_status rt_mesh_ply(rt_ctx* ctx, int32_t index, const char* path, const float 
  * `capacity` bytes to `out` (may be NULL) and the full size to *size. */
 rt_status rt_ply_bvh_image(const char* path, const float offset[3], float max_coord,
                            uint8_t* out, int64_t capacity, int64_t* size);
+
+/* ---- pathTrace scene (prepareCUDAscene, main.cu:404-553) ----
+ * loadObject (Loader.cpp:207-319): appends a PLY mesh whose triangles carry
+ * `reflection_type` (RT_PT_*); indices are offset by the vertices already
+ * loaded. */
+rt_status rt_load_object(rt_ctx* ctx, const char* path, int32_t reflection_type);
+/* processTriangleData(offset) (Loader.cpp:98-205, max |coord| = max_coord,
+ * reference 1.0) + UpdateBoundingVolumeHierarchy (BVH.cpp:500-554) + the
+ * device upload of prepareCUDAscene. The six built-in spheres
+ * (CUDAPathTracer.cu:94-121) need no call. out_info (may be NULL):
+ * [0] triangles, [1] BVH nodes, [2] triangle-list entries, [3] tree depth. */
+rt_status rt_process_triangle_data(rt_ctx* ctx, const float offset[3], float max_coord,
+                                   int32_t out_info[4]);
+/* The `.bvh` cache image UpdateBoundingVolumeHierarchy writes for the processed
+ * pathTrace scene (BVH.cpp:537-540; same layout as rt_ply_bvh_image). */
+rt_status rt_pathtrace_bvh_image(const rt_ctx* ctx, uint8_t* out, int64_t capacity, int64_t* size);
 
 /* ---- camera (Camera.h:19-34 initialize, 86-103 updateViewMatrix) ---- */
 rt_status rt_camera(rt_ctx* ctx, const float eye[3], const float center[3], const float up[3],

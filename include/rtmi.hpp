@@ -144,11 +144,29 @@ public:
     }
     void commit() { check(rt_commit(ctx_)); }
 
-    // pathTracing (main.cu:875-898): one frame of `spp` samples into the canvas.
+    // pathTracing (main.cu:875-898): one frame of `spp` samples into the canvas,
+    // with rayColor over the create* scene.
     void pathTracing(Canvas& canvas, int32_t spp, int32_t bounces, uint32_t seed = 1984,
                      uint32_t sampleOffset = 0) {
         commit();
-        rt_render_params p{canvas.getWidth(), canvas.getHeight(), spp, bounces, seed, sampleOffset, 1, 0, 1, 0};
+        rt_render_params p{canvas.getWidth(), canvas.getHeight(), spp, bounces, seed, sampleOffset,
+                           1, 0, 1, 0, RT_INTEGRATOR_RAYCOLOR};
+        check(rt_render(ctx_, &p, canvas.data()));
+    }
+
+    // prepareCUDAscene (main.cu:404-553): loadObject(...) per PLY, then
+    // processTriangleData(offset) builds the BVH and uploads it.
+    void loadObject(const std::string& file, int32_t reflectionType) {
+        check(rt_load_object(ctx_, file.c_str(), reflectionType));
+    }
+    void processTriangleData(Vector3Df offset, float maxCoord = 1.0f) {
+        check(rt_process_triangle_data(ctx_, offset.data(), maxCoord, nullptr));
+    }
+    // renderKernel's committed pathTrace call (main.cu:187; 5 bounces there).
+    void pathTraceFrame(Canvas& canvas, int32_t spp, int32_t bounces = 5, uint32_t seed = 1984,
+                        uint32_t sampleOffset = 0) {
+        rt_render_params p{canvas.getWidth(), canvas.getHeight(), spp, bounces, seed, sampleOffset,
+                           1, 0, 1, 0, RT_INTEGRATOR_PATHTRACE};
         check(rt_render(ctx_, &p, canvas.data()));
     }
 

@@ -58,6 +58,20 @@ def lib():
         L.orc_philox.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.orc_uniforms.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, fp]
         L.orc_trace.argtypes = [vp, fp, fp, C.c_float, fp, fp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.orc_pt_new.restype = vp
+        L.orc_pt_free.argtypes = [vp]
+        L.orc_pt_load_object.argtypes = [vp, C.c_char_p, C.c_int]
+        L.orc_pt_process.argtypes = [vp, fp, C.c_float]
+        L.orc_pt_set_bvh.argtypes = [vp, C.POINTER(C.c_uint8), C.c_int64]
+        L.orc_pt_render.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_uint32,
+                                    C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, fp,
+                                    C.POINTER(C.c_uint64)]
+        L.orc_pt_sinf.argtypes = [C.c_float]
+        L.orc_pt_sinf.restype = C.c_float
+        L.orc_pt_cosf.argtypes = [C.c_float]
+        L.orc_pt_cosf.restype = C.c_float
+        L.orc_pt_powf.argtypes = [C.c_float, C.c_float]
+        L.orc_pt_powf.restype = C.c_float
         L.orc_gamma_u8.argtypes = [fp, C.c_int64, C.POINTER(C.c_uint8)]
         _lib = L
     return _lib
@@ -168,6 +182,50 @@ class OracleScene:
         if rc != 0:
             raise RuntimeError(f"orc_render failed with {rc}")
         return out, {"segments": int(stats[0]), "tri_tests": int(stats[1])}
+
+
+REFLECTION_TYPES = {"DIFFUSE": 0, "METAL": 1, "SPECULAR": 2, "REFRACTION": 3, "COAT": 4}
+
+
+class OraclePathTrace:
+    """pathTrace scene of the CPU restatement (prepareCUDAscene, main.cu:404-553):
+    PLY meshes via load_object, processTriangleData via process, and the BVH
+    from a `.bvh` cache image (the reference's own files in the tests). The
+    camera comes from an OracleScene (its `camera`)."""
+
+    def __init__(self):
+        self.L = lib()
+        self.h = self.L.orc_pt_new()
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.orc_pt_free(self.h)
+            self.h = None
+
+    def load_object(self, path, reflection_type="COAT"):
+        t = REFLECTION_TYPES[reflection_type] if isinstance(reflection_type, str) else int(reflection_type)
+        assert self.L.orc_pt_load_object(self.h, str(path).encode(), t) == 0, path
+
+    def process(self, offset=(0.0, 0.0, 0.0), max_coord=1.0):
+        assert self.L.orc_pt_process(self.h, f3(offset), max_coord) == 0
+
+    def set_bvh(self, image: bytes):
+        buf = (C.c_uint8 * len(image)).from_buffer_copy(image)
+        rc = self.L.orc_pt_set_bvh(self.h, buf, len(image))
+        if rc:
+            raise ValueError(f"bad .bvh image ({rc})")
+
+    def render(self, cam: OracleScene, width, height, spp, bounces=5, seed=1984, sample_offset=0,
+               row_block=1, row_rank=0, row_world=1, threads=0, lanes_per_pixel=1):
+        rows = owned_rows(height, row_block, row_rank, row_world)
+        out = np.zeros((rows, width, 3), np.float32)
+        stats = (C.c_uint64 * 3)()
+        rc = self.L.orc_pt_render(self.h, cam.h, width, height, spp, bounces, seed, sample_offset,
+                                  row_block, row_rank, row_world, lanes_per_pixel, threads,
+                                  out.ctypes.data_as(C.POINTER(C.c_float)), stats)
+        if rc != 0:
+            raise RuntimeError(f"orc_pt_render failed with {rc}")
+        return out, {"segments": int(stats[0]), "tri_tests": int(stats[1]), "overflow": int(stats[2])}
 
 
 def owned_rows(height, block, rank, world):

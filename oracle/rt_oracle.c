@@ -732,12 +732,10 @@ int orc_load_obj(const char* path, const float scale[3], const float rotate[3], 
 
 void orc_free(void* p) { free(p); }
 
-/* loadObject (ASCII PLY, Loader.cpp:207-319) + the vertex transform of
- * processTriangleData (Loader.cpp:98-144): centre the triangles' bounds, scale
- * to max |coord| = max_coord (MaxCoordAfterRescale, :58), add offset.
- * Returns triangle count or -1; *out (malloc'ed) holds 9 floats per triangle
- * in (idx1, idx2, idx3) vertex order. */
-int orc_load_ply(const char* path, const float offset[3], float max_coord, float** out) {
+/* loadObject's ASCII PLY reader (Loader.cpp:207-319) as a triangle soup of raw
+ * vertices, 9 floats per triangle in (idx1, idx2, idx3) order. Returns the
+ * triangle count or -1. */
+static int ply_read_soup(const char* path, float** out) {
     FILE* f = fopen(path, "rb");
     if (!f) return -1;
     char line[1024];
@@ -781,9 +779,22 @@ int orc_load_ply(const char* path, const float offset[3], float max_coord, float
     }
     fclose(f);
     if (!inside) { free(v); free(ix); return -1; }
+    float* t = (float*)malloc((size_t)(ct ? ct : 1) * 9 * sizeof(float));
+    for (unsigned i = 0; i < 3 * ct; ++i) {
+        t[3 * i] = v[3 * ix[i]]; t[3 * i + 1] = v[3 * ix[i] + 1]; t[3 * i + 2] = v[3 * ix[i] + 2];
+    }
+    free(v); free(ix);
+    *out = t;
+    return (int)ct;
+}
+
+/* processTriangleData (Loader.cpp:98-144) on a soup: centre the triangles'
+ * bounds, scale to max |coord| = max_coord (MaxCoordAfterRescale, :58), add
+ * offset. */
+static void soup_transform(float* t, unsigned ct, const float offset[3], float max_coord) {
     V3 mn = v3(FLT_MAX_, FLT_MAX_, FLT_MAX_), mx = v3(-FLT_MAX_, -FLT_MAX_, -FLT_MAX_);
     for (unsigned i = 0; i < 3 * ct; ++i) {
-        V3 q = v3(v[3 * ix[i]], v[3 * ix[i] + 1], v[3 * ix[i] + 2]);
+        V3 q = v3(t[3 * i], t[3 * i + 1], t[3 * i + 2]);
         mn = v3(mn.x < q.x ? mn.x : q.x, mn.y < q.y ? mn.y : q.y, mn.z < q.z ? mn.z : q.z);
         mx = v3(mx.x > q.x ? mx.x : q.x, mx.y > q.y ? mx.y : q.y, mx.z > q.z ? mx.z : q.z);
     }
@@ -794,18 +805,20 @@ int orc_load_ply(const char* path, const float offset[3], float max_coord, float
     for (int k = 0; k < 6; ++k) maxi = (maxi < cand[k]) ? cand[k] : maxi;
     float sc = max_coord / maxi;
     V3 off = v3(offset[0], offset[1], offset[2]);
-    for (unsigned i = 0; i < cv; ++i) {
-        V3 q = v3(v[3 * i], v[3 * i + 1], v[3 * i + 2]);
-        q = vadd(vmul(vsub(q, c), sc), off);
-        v[3 * i] = q.x; v[3 * i + 1] = q.y; v[3 * i + 2] = q.z;
-    }
-    float* t = (float*)malloc((size_t)(ct ? ct : 1) * 9 * sizeof(float));
     for (unsigned i = 0; i < 3 * ct; ++i) {
-        t[3 * i] = v[3 * ix[i]]; t[3 * i + 1] = v[3 * ix[i] + 1]; t[3 * i + 2] = v[3 * ix[i] + 2];
+        V3 q = v3(t[3 * i], t[3 * i + 1], t[3 * i + 2]);
+        q = vadd(vmul(vsub(q, c), sc), off);
+        t[3 * i] = q.x; t[3 * i + 1] = q.y; t[3 * i + 2] = q.z;
     }
-    free(v); free(ix);
-    *out = t;
-    return (int)ct;
+}
+
+/* loadObject + processTriangleData's vertex transform. Returns the triangle
+ * count or -1; *out (malloc'ed) holds 9 floats per triangle. */
+int orc_load_ply(const char* path, const float offset[3], float max_coord, float** out) {
+    int ct = ply_read_soup(path, out);
+    if (ct < 0) return -1;
+    soup_transform(*out, (unsigned)ct, offset, max_coord);
+    return ct;
 }
 
 int orc_mesh_obj(Scene* s, int idx, const char* path, const float scale[3], const float rotate[3],
@@ -937,4 +950,456 @@ void orc_gamma_u8(const float* rgb, int64_t n, uint8_t* out) {
         float v = fmaxf(0.0f, fminf(sqrtf(rgb[i]), 0.999f));
         out[i] = (uint8_t)(uint32_t)(255.99f * v);
     }
+}
+
+/* =========================================================================
+ * pathTrace integrator (CUDAPathTracer.cu:358-622, called by renderKernel at
+ * main.cu:187) over the PLY triangles of prepareCUDAscene (main.cu:404-553)
+ * and the six built-in spheres (CUDAPathTracer.cu:94-121).
+ *
+ * The BVH is NOT rebuilt here: the oracle traverses a `.bvh` cache image
+ * (BVH.cpp:537-540 layout) handed to it — in the tests, the reference's own
+ * resources/models/<model>/<model>.ply.bvh files — exactly as BVH_IntersectTriangles
+ * does: full DFS, right child pushed before left, strict `<` on distance².
+ *
+ * Deviations: sinf/cosf/powf are the explicit double-precision
+ * algorithms below (the reference's CUDA libdevice results are not available
+ * here); a ray that hits nothing returns black (the reference reads
+ * uninitialised state there, scene_t == 1e20 slips past its `> 1e20` check).
+ * ========================================================================= */
+typedef struct {
+    float n[3], d, e1[3], d1, e2[3], d2, e3[3], d3;
+    int material;
+} PtTri;
+
+typedef struct {
+    float lo[3], hi[3];
+    uint32_t u0, u1;
+} PtNode;
+
+typedef struct {
+    float* raw;        /* loaded soup, 9 floats per triangle, untransformed */
+    int* raw_mat;      /* ReflectionType per triangle */
+    int n_raw;
+    PtTri* tris;
+    int n_tris;
+    PtNode* nodes;
+    int n_nodes;
+    int32_t* list;
+    int n_list;
+} PtScene;
+
+enum { PT_DIFFUSE = 0, PT_METAL = 1, PT_SPECULAR = 2, PT_REFRACTION = 3, PT_COAT = 4 };
+
+typedef struct { float rad; V3 pos, emi, col; int type; } PtSphere;
+static const PtSphere pt_spheres[6] = {
+    {1.6f, {0.0f, 2.8f, 0.0f}, {6.0f, 4.0f, 2.0f}, {0.0f, 0.0f, 0.0f}, PT_DIFFUSE},
+    {10000.0f, {50.0f, 40.8f, -1060.0f}, {0.51f, 0.51f, 0.51f}, {0.175f, 0.175f, 0.25f}, PT_DIFFUSE},
+    {100000.0f, {0.0f, -100001.1f, 0.0f}, {0.0f, 0.0f, 0.0f}, {0.5f, 0.0f, 0.0f}, PT_COAT},
+    {100000.0f, {0.0f, -100001.2f, 0.0f}, {0.0f, 0.0f, 0.0f}, {0.3f, 0.3f, 0.3f}, PT_DIFFUSE},
+    {110000.0f, {50.0f, -110048.5f, 0.0f}, {3.6f, 2.0f, 0.2f}, {0.0f, 0.0f, 0.0f}, PT_DIFFUSE},
+    {1.1f, {1.6f, 0.0f, 1.0f}, {0.0f, 0.0f, 0.0f}, {0.9f, 0.9f, 0.9f}, PT_SPECULAR},
+};
+
+/* sin/cos: Cody-Waite reduction by pi/2, Taylor to degree 17 / 16 (double). */
+static void pt_sincos(double x, double* s, double* c) {
+    const double two_over_pi = 0.63661977236758134308;
+    const double pio2_hi = 1.57079632673412561417;
+    const double pio2_lo = 6.07710050650619224932e-11;
+    const double k = floor(x * two_over_pi + 0.5);
+    const double r = (x - k * pio2_hi) - k * pio2_lo;
+    const double r2 = r * r;
+    double ps = 1.0 / 355687428096000.0;
+    ps = ps * r2 - 1.0 / 1307674368000.0;
+    ps = ps * r2 + 1.0 / 6227020800.0;
+    ps = ps * r2 - 1.0 / 39916800.0;
+    ps = ps * r2 + 1.0 / 362880.0;
+    ps = ps * r2 - 1.0 / 5040.0;
+    ps = ps * r2 + 1.0 / 120.0;
+    ps = ps * r2 - 1.0 / 6.0;
+    const double sn = r + (r * r2) * ps;
+    double pc = 1.0 / 20922789888000.0;
+    pc = pc * r2 - 1.0 / 87178291200.0;
+    pc = pc * r2 + 1.0 / 479001600.0;
+    pc = pc * r2 - 1.0 / 3628800.0;
+    pc = pc * r2 + 1.0 / 40320.0;
+    pc = pc * r2 - 1.0 / 720.0;
+    pc = pc * r2 + 1.0 / 24.0;
+    pc = pc * r2 - 0.5;
+    const double cs = 1.0 + r2 * pc;
+    const long q = ((long)k) & 3;
+    *s = q == 0 ? sn : q == 1 ? cs : q == 2 ? -sn : -cs;
+    *c = q == 0 ? cs : q == 1 ? -sn : q == 2 ? -cs : sn;
+}
+static float pt_sinf(float x) { double s, c; pt_sincos((double)x, &s, &c); return (float)s; }
+static float pt_cosf(float x) { double s, c; pt_sincos((double)x, &s, &c); return (float)c; }
+
+/* x^y, x >= 0: exp(y ln x), atanh series for ln, Taylor exp (double). */
+static float pt_powf(float xf, float yf) {
+    if (!(xf > 0.0f)) return xf == 0.0f ? (yf > 0.0f ? 0.0f : 1.0f) : NAN;
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    int e;
+    double m = frexp((double)xf, &e);
+    if (m < 0.70710678118654752440) { m = m * 2.0; e = e - 1; }
+    const double t = (m - 1.0) / (m + 1.0), t2 = t * t;
+    double p = 1.0 / 23.0;
+    p = p * t2 + 1.0 / 21.0;
+    p = p * t2 + 1.0 / 19.0;
+    p = p * t2 + 1.0 / 17.0;
+    p = p * t2 + 1.0 / 15.0;
+    p = p * t2 + 1.0 / 13.0;
+    p = p * t2 + 1.0 / 11.0;
+    p = p * t2 + 1.0 / 9.0;
+    p = p * t2 + 1.0 / 7.0;
+    p = p * t2 + 1.0 / 5.0;
+    p = p * t2 + 1.0 / 3.0;
+    p = p * t2 + 1.0;
+    const double ln_m = 2.0 * t * p;
+    const double de = (double)e;
+    const double lnx = (de * ln2_hi + ln_m) + de * ln2_lo;
+    const double z = (double)yf * lnx;
+    const double n = floor(z * 1.44269504088896338700 + 0.5);
+    const double r = (z - n * ln2_hi) - n * ln2_lo;
+    double q = 1.0 / 6227020800.0;
+    q = q * r + 1.0 / 479001600.0;
+    q = q * r + 1.0 / 39916800.0;
+    q = q * r + 1.0 / 3628800.0;
+    q = q * r + 1.0 / 362880.0;
+    q = q * r + 1.0 / 40320.0;
+    q = q * r + 1.0 / 5040.0;
+    q = q * r + 1.0 / 720.0;
+    q = q * r + 1.0 / 120.0;
+    q = q * r + 1.0 / 24.0;
+    q = q * r + 1.0 / 6.0;
+    q = q * r + 0.5;
+    q = q * r + 1.0;
+    q = q * r + 1.0;
+    return (float)ldexp(q, (int)n);
+}
+float orc_pt_sinf(float x) { return pt_sinf(x); }
+float orc_pt_cosf(float x) { return pt_cosf(x); }
+float orc_pt_powf(float x, float y) { return pt_powf(x, y); }
+
+PtScene* orc_pt_new(void) { return (PtScene*)calloc(1, sizeof(PtScene)); }
+
+void orc_pt_free(PtScene* p) {
+    if (!p) return;
+    free(p->raw); free(p->raw_mat); free(p->tris); free(p->nodes); free(p->list);
+    free(p);
+}
+
+/* loadObject(file, reflectionType, meshIndex) (Loader.cpp:207-319): append. */
+int orc_pt_load_object(PtScene* p, const char* path, int reflection_type) {
+    float* soup = NULL;
+    int ct = ply_read_soup(path, &soup);
+    if (ct < 0) return 1;
+    p->raw = (float*)realloc(p->raw, (size_t)(p->n_raw + ct + 1) * 9 * sizeof(float));
+    p->raw_mat = (int*)realloc(p->raw_mat, (size_t)(p->n_raw + ct + 1) * sizeof(int));
+    memcpy(p->raw + (size_t)p->n_raw * 9, soup, (size_t)ct * 9 * sizeof(float));
+    for (int i = 0; i < ct; ++i) p->raw_mat[p->n_raw + i] = reflection_type;
+    p->n_raw += ct;
+    free(soup);
+    return 0;
+}
+
+/* processTriangleData (Loader.cpp:98-205): transform, then the Kuchkuda
+ * precompute (:166-202) per triangle. */
+int orc_pt_process(PtScene* p, const float offset[3], float max_coord) {
+    free(p->tris);
+    p->tris = (PtTri*)calloc((size_t)(p->n_raw ? p->n_raw : 1), sizeof(PtTri));
+    p->n_tris = p->n_raw;
+    float* t = (float*)malloc((size_t)(p->n_raw ? p->n_raw : 1) * 9 * sizeof(float));
+    memcpy(t, p->raw, (size_t)p->n_raw * 9 * sizeof(float));
+    soup_transform(t, (unsigned)p->n_raw, offset, max_coord);
+    for (int i = 0; i < p->n_raw; ++i) {
+        V3 a = v3(t[9 * i], t[9 * i + 1], t[9 * i + 2]);
+        V3 b = v3(t[9 * i + 3], t[9 * i + 4], t[9 * i + 5]);
+        V3 c = v3(t[9 * i + 6], t[9 * i + 7], t[9 * i + 8]);
+        V3 vc1 = vsub(b, a), vc2 = vsub(c, b), vc3 = vsub(a, c);
+        V3 n = vcross(vc1, vc2);
+        V3 alt1 = vcross(vc2, vc3);
+        if (vlen(alt1) > vlen(n)) n = alt1;
+        V3 alt2 = vcross(vc3, vc1);
+        if (vlen(alt2) > vlen(n)) n = alt2;
+        n = vnorm(n);
+        V3 e1 = vnorm(vcross(n, vc1)), e2 = vnorm(vcross(n, vc2)), e3 = vnorm(vcross(n, vc3));
+        PtTri* q = &p->tris[i];
+        q->n[0] = n.x; q->n[1] = n.y; q->n[2] = n.z; q->d = vdot(n, a);
+        q->e1[0] = e1.x; q->e1[1] = e1.y; q->e1[2] = e1.z; q->d1 = vdot(e1, a);
+        q->e2[0] = e2.x; q->e2[1] = e2.y; q->e2[2] = e2.z; q->d2 = vdot(e2, b);
+        q->e3[0] = e3.x; q->e3[1] = e3.y; q->e3[2] = e3.z; q->d3 = vdot(e3, c);
+        q->material = p->raw_mat[i];
+    }
+    free(t);
+    return 0;
+}
+
+/* The `.bvh` cache image (BVH.cpp:537-540): u32 nodes, u32 indices, 32 B
+ * CacheFriendlyBVHNode[] (bottom, top, u0, u1), int32 indices. Returns 0 on a
+ * well-formed image whose indices are all < the processed triangle count. */
+int orc_pt_set_bvh(PtScene* p, const uint8_t* img, int64_t size) {
+    uint32_t nn, ni;
+    if (size < 8) return 1;
+    memcpy(&nn, img, 4);
+    memcpy(&ni, img + 4, 4);
+    if ((int64_t)8 + (int64_t)nn * 32 + (int64_t)ni * 4 != size) return 1;
+    free(p->nodes); free(p->list);
+    p->nodes = (PtNode*)malloc((size_t)(nn ? nn : 1) * sizeof(PtNode));
+    p->list = (int32_t*)malloc((size_t)(ni ? ni : 1) * sizeof(int32_t));
+    memcpy(p->nodes, img + 8, (size_t)nn * 32);
+    memcpy(p->list, img + 8 + (size_t)nn * 32, (size_t)ni * 4);
+    p->n_nodes = (int)nn;
+    p->n_list = (int)ni;
+    for (uint32_t i = 0; i < ni; ++i)
+        if (p->list[i] < 0 || p->list[i] >= p->n_tris) return 2;
+    return 0;
+}
+
+/* Sphere::intersect (CUDAPathTracer.cu:66-79) */
+static float pt_sphere_hit(const PtSphere* sp, V3 o, V3 d) {
+    V3 op = vsub(sp->pos, o);
+    float t, eps = 0.01f;
+    float b = vdot(op, d);
+    float disc = b * b - vdot(op, op) + sp->rad * sp->rad;
+    if (disc < 0) return 0;
+    disc = sqrtf(disc);
+    return (t = b - disc) > eps ? t : ((t = b + disc) > eps ? t : 0);
+}
+
+/* RayIntersectsBox (CUDAPathTracer.cu:124-181) */
+static int pt_box(const PtNode* nd, V3 o, V3 d) {
+    float tnear = -FLT_MAX_, tfar = FLT_MAX_;
+    const float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+    for (int c = 0; c < 3; ++c) {
+        float lo = nd->lo[c], hi = nd->hi[c];
+        if (dd[c] == 0.f) {
+            if (oo[c] < lo) return 0;
+            if (oo[c] > hi) return 0;
+        } else {
+            float t1 = (lo - oo[c]) / dd[c];
+            float t2 = (hi - oo[c]) / dd[c];
+            if (t1 > t2) { float tmp = t1; t1 = t2; t2 = tmp; }
+            if (t1 > tnear) tnear = t1;
+            if (t2 < tfar) tfar = t2;
+            if (tnear > tfar) return 0;
+            if (tfar < 0.f) return 0;
+        }
+    }
+    return 1;
+}
+
+/* BVH_IntersectTriangles (CUDAPathTracer.cu:192-352). Returns -1 on stack
+ * overflow (the reference returns early), else the number of triangles tested. */
+static int pt_intersect(const PtScene* p, V3 o, V3 d, unsigned avoid_self, int* best_idx, V3* best_hit,
+                        float* hitdist, int* mat, int* overflow) {
+    int stack[32];
+    int sp = 0, tested = 0;
+    float best = FLT_MAX_;
+    *best_idx = -1;
+    if (p->n_nodes == 0) return 0;
+    stack[sp++] = 0;
+    while (sp) {
+        const PtNode* nd = &p->nodes[stack[--sp]];
+        if (!(nd->u0 & 0x80000000u)) {
+            if (pt_box(nd, o, d)) {
+                if (sp + 2 > 32) { *overflow = 1; return tested; }
+                stack[sp++] = (int)nd->u1;
+                stack[sp++] = (int)nd->u0;
+            }
+        } else {
+            uint32_t cnt = nd->u0 & 0x7fffffffu;
+            for (uint32_t i = nd->u1; i < nd->u1 + cnt; ++i) {
+                int idx = p->list[i];
+                if (avoid_self == (unsigned)idx) continue;
+                const PtTri* t = &p->tris[idx];
+                ++tested;
+                V3 n = v3(t->n[0], t->n[1], t->n[2]);
+                float k = vdot(n, d);
+                if (k == 0.0f) continue;
+                float s = (t->d - vdot(n, o)) / k;
+                if (s <= 0.0f) continue;
+                if (s <= 1e-3f) continue;
+                V3 hit = vadd(vmul(d, s), o);
+                if (vdot(v3(t->e1[0], t->e1[1], t->e1[2]), hit) - t->d1 < 0.0f) continue;
+                if (vdot(v3(t->e2[0], t->e2[1], t->e2[2]), hit) - t->d2 < 0.0f) continue;
+                if (vdot(v3(t->e3[0], t->e3[1], t->e3[2]), hit) - t->d3 < 0.0f) continue;
+                float hz = (o.x - hit.x) * (o.x - hit.x) + (o.y - hit.y) * (o.y - hit.y) +
+                           (o.z - hit.z) * (o.z - hit.z);
+                if (hz < best) {
+                    best = hz;
+                    *hitdist = sqrtf(best);
+                    *best_idx = idx;
+                    *best_hit = hit;
+                    *mat = t->material;
+                }
+            }
+        }
+    }
+    return tested;
+}
+
+/* orthonormal frame around w and a lobe direction (CUDAPathTracer.cu:462-469, 491-496) */
+static V3 pt_lobe(V3 w, float phi, float a, float b) {
+    V3 u = vnorm(vcross(((double)fabsf(w.x) > .1) ? v3(0, 1, 0) : v3(1, 0, 0), w));
+    V3 v = vcross(w, u);
+    return vnorm(vadd(vadd(vmul(vmul(u, pt_cosf(phi)), a), vmul(vmul(v, pt_sinf(phi)), a)), vmul(w, b)));
+}
+
+#define PT_TWO_PI (2.0f * 3.1415926535897932384626422832795028841971f)
+
+/* pathTrace (CUDAPathTracer.cu:358-622) */
+static V3 pt_path(const PtScene* p, V3 o, V3 d, int bounces, RandState* rs, uint64_t* segs,
+                  uint64_t* tests, int* overflow) {
+    V3 mask = v3(1.0f, 1.0f, 1.0f), accu = v3(0.0f, 0.0f, 0.0f);
+    int avoid = -1;
+    for (int bounce = 0; bounce < bounces; ++bounce) {
+        int best_idx = -1, mat = 0, sphere_id = -1, geom = -1;
+        V3 best_hit = v3(0, 0, 0);
+        float hitdistance = 1e20f, scene_t = 1e20f;
+        ++*segs;
+        int tt = pt_intersect(p, o, d, (unsigned)avoid, &best_idx, &best_hit, &hitdistance, &mat, overflow);
+        *tests += (uint64_t)tt;
+        for (int i = 6; i--;) {
+            float dist = pt_sphere_hit(&pt_spheres[i], o, d);
+            if (dist != 0.0f && dist < scene_t) { scene_t = dist; sphere_id = i; geom = 1; }
+        }
+        avoid = best_idx;
+        if (hitdistance < scene_t && hitdistance > 0.002f) { scene_t = hitdistance; geom = 2; }
+        if (scene_t > 1e20f || geom < 0) return v3(0.0f, 0.0f, 0.0f);
+
+        V3 hitp, normal, oriented, f;
+        int rtype;
+        if (geom == 1) {
+            const PtSphere* sp = &pt_spheres[sphere_id];
+            hitp = vadd(o, vmul(d, scene_t));
+            normal = vnorm(v3(hitp.x - sp->pos.x, hitp.y - sp->pos.y, hitp.z - sp->pos.z));
+            oriented = vdot(normal, d) < 0 ? normal : vmul(normal, -1.0f);
+            f = sp->col;
+            rtype = sp->type;
+            accu = vadd(accu, vmulv(mask, sp->emi));
+        } else {
+            const PtTri* t = &p->tris[best_idx];
+            hitp = best_hit;
+            normal = vnorm(v3(t->n[0], t->n[1], t->n[2]));
+            oriented = vdot(normal, d) < 0 ? normal : vmul(normal, -1.0f);
+            f = v3(0.9f, 0.3f, 0.0f);
+            rtype = mat;
+            accu = vadd(accu, vmulv(mask, v3(0.0f, 0.0f, 0.0f)));
+        }
+        V3 next = d, point = hitp;
+        V3 mirror = vsub(d, vmul(vmul(normal, 2.0f), vdot(normal, d)));
+        if (rtype == PT_DIFFUSE) {
+            float phi = PT_TWO_PI * curand_uniform_(rs);
+            float r2 = curand_uniform_(rs);
+            V3 w = vnorm(oriented);
+            next = pt_lobe(w, phi, sqrtf(r2), sqrtf(1 - r2));
+            point = vadd(hitp, vmul(w, 0.01f));
+            mask = vmulv(mask, f);
+        } else if (rtype == PT_METAL) {
+            float phi = PT_TWO_PI * curand_uniform_(rs);
+            float r2 = curand_uniform_(rs);
+            float cos_t = pt_powf(1 - r2, 1.0f / (20.0f + 1));
+            float sin_t = sqrtf(1 - cos_t * cos_t);
+            V3 w = vnorm(mirror);
+            next = pt_lobe(w, phi, sin_t, cos_t);
+            point = vadd(hitp, vmul(w, 0.01f));
+            mask = vmulv(mask, f);
+        } else if (rtype == PT_SPECULAR) {
+            next = mirror;
+            point = vadd(hitp, vmul(oriented, 0.01f));
+            mask = vmulv(mask, f);
+        } else if (rtype == PT_COAT) {
+            if (curand_uniform_(rs) < 0.05f) {
+                mask = vmulv(mask, v3(1, 1, 1));
+                next = mirror;
+                point = vadd(hitp, vmul(oriented, 0.01f));
+            } else {
+                float r1 = PT_TWO_PI * curand_uniform_(rs);
+                float r2 = curand_uniform_(rs);
+                next = pt_lobe(vnorm(oriented), r1, sqrtf(r2), sqrtf(1 - r2));
+                point = vadd(hitp, vmul(oriented, 0.01f));
+                mask = vmulv(mask, f);
+            }
+        } else if (rtype == PT_REFRACTION) {
+            int into = vdot(normal, oriented) > 0;
+            float nc = 1.0f, nt = 1.5f;
+            float nnt = into ? nc / nt : nt / nc;
+            float ddn = vdot(d, oriented);
+            float cos2t = 1.0f - nnt * nnt * (1.f - ddn * ddn);
+            if (cos2t < 0.0f) {
+                next = mirror;
+                point = vadd(hitp, vmul(oriented, 0.01f));
+            } else {
+                V3 tdir = vmul(d, nnt);
+                tdir = vsub(tdir, vmul(normal, (float)(into ? 1 : -1) * (ddn * nnt + sqrtf(cos2t))));
+                tdir = vnorm(tdir);
+                float R0 = (nt - nc) * (nt - nc) / (nt + nc) * (nt + nc);
+                float c = 1.0f - (into ? -ddn : vdot(tdir, normal));
+                float Re = R0 + (1.0f - R0) * c * c * c * c * c;
+                float Tr = 1 - Re;
+                float P = 0.25f + 0.5f * Re;
+                float RP = Re / P;
+                float TP = Tr / (1.0f - P);
+                if (curand_uniform_(rs) < 0.25f) {
+                    mask = vmul(mask, RP);
+                    next = mirror;
+                    point = vadd(hitp, vmul(oriented, 0.01f));
+                } else {
+                    mask = vmul(mask, TP);
+                    next = tdir;
+                    point = vadd(hitp, vmul(oriented, 0.001f));
+                }
+            }
+        }
+        o = point;
+        d = next;
+    }
+    return accu;
+}
+
+/* renderKernel (main.cu:160-206) with the committed pathTrace call (:187),
+ * rows/lanes/summation order as orc_render. stats: [0] segments,
+ * [1] triangles tested, [2] overflow flag. */
+int orc_pt_render(const PtScene* p, const Scene* cam, int width, int height, int spp, int bounces,
+                  uint32_t seed, uint32_t sample_offset, int row_block, int row_rank, int row_world,
+                  int lanes_per_pixel, int threads, float* out, uint64_t* stats) {
+    const int S = lanes_per_pixel;
+    if (!cam->has_camera || width < 2 || height < 2 || spp < 1 || bounces < 1 || row_block < 1 ||
+        row_world < 1 || row_rank < 0 || row_rank >= row_world || S < 1 || S > 64 || (S & (S - 1)))
+        return 1;
+    if (p->n_tris > 0 && p->n_nodes == 0) return 2;
+    int local_rows = owned_rows(height, row_block, row_rank, row_world);
+    uint64_t segs = 0, tests = 0;
+    int overflow = 0;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : segs, tests) reduction(| : overflow)
+#endif
+    for (int lr = 0; lr < local_rows; ++lr) {
+        int lb = lr / row_block;
+        int y = (lb * row_world + row_rank) * row_block + (lr - lb * row_block);
+        for (int x = 0; x < width; ++x) {
+            uint32_t pixel = (uint32_t)y * (uint32_t)width + (uint32_t)x;
+            V3 color = v3(0.0f, 0.0f, 0.0f);
+            for (int c = 0; c < S; ++c) {
+                V3 part = v3(0.0f, 0.0f, 0.0f);
+                for (int i = c; i < spp; i += S) {
+                    RandState rs;
+                    rand_init(&rs, seed, pixel, sample_offset + (uint32_t)i);
+                    float rx = curand_uniform_(&rs);
+                    float ry = curand_uniform_(&rs);
+                    float dx = ((float)x + rx) / (float)(width - 1);
+                    float dy = ((float)y + ry) / (float)(height - 1);
+                    Ray ray = camera_get_ray(cam, dx, dy, &rs);
+                    part = vadd(part, pt_path(p, ray.origin, ray.direction, bounces, &rs, &segs, &tests, &overflow));
+                }
+                color = c == 0 ? part : vadd(color, part);
+            }
+            V3 m = vdiv(color, (float)spp);
+            float* o = out + ((size_t)lr * width + x) * 3;
+            o[0] = m.x; o[1] = m.y; o[2] = m.z;
+        }
+    }
+    if (stats) { stats[0] = segs; stats[1] = tests; stats[2] = (uint64_t)overflow; }
+    return 0;
 }

@@ -23,12 +23,15 @@ STATUS_NAMES = {
 }
 
 # Every symbol include/rtmi.h declares (checked by tests/test_abi.py).
+ABI_VERSION = 2  # include/rtmi.h RTMI_ABI_VERSION
+
 EXPORTS = [
     "rt_abi_version", "rt_create", "rt_destroy", "rt_last_error", "rt_clear_scene",
     "rt_material_lambertian", "rt_material_metal", "rt_material_dielectric",
     "rt_material_emission", "rt_material_defined", "rt_sphere", "rt_moving_sphere", "rt_plane",
     "rt_cube", "rt_mesh", "rt_mesh_obj", "rt_mesh_triangle_count", "rt_mesh_vertices",
-    "rt_mesh_ply", "rt_ply_bvh_image",
+    "rt_mesh_ply", "rt_ply_bvh_image", "rt_load_object", "rt_process_triangle_data",
+    "rt_pathtrace_bvh_image",
     "rt_camera", "rt_commit", "rt_scene_info", "rt_render", "rt_render_device", "rt_sync_stats", "rt_gamma_u8",
 ]
 
@@ -44,7 +47,7 @@ class RenderParams(C.Structure):
         ("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32),
         ("max_depth", C.c_int32), ("seed", C.c_uint32), ("sample_offset", C.c_uint32),
         ("row_block", C.c_int32), ("row_rank", C.c_int32), ("row_world", C.c_int32),
-        ("lanes_per_pixel", C.c_int32),
+        ("lanes_per_pixel", C.c_int32), ("integrator", C.c_int32),
     ]
 
 
@@ -107,6 +110,9 @@ def lib():
     L.rt_mesh_ply.argtypes = [vp, i32, C.c_char_p, fp, C.c_float, i32]
     L.rt_ply_bvh_image.argtypes = [C.c_char_p, fp, C.c_float, C.POINTER(C.c_uint8), C.c_int64,
                                    C.POINTER(C.c_int64)]
+    L.rt_load_object.argtypes = [vp, C.c_char_p, i32]
+    L.rt_process_triangle_data.argtypes = [vp, fp, C.c_float, C.POINTER(C.c_int32)]
+    L.rt_pathtrace_bvh_image.argtypes = [vp, C.POINTER(C.c_uint8), C.c_int64, C.POINTER(C.c_int64)]
     L.rt_camera.argtypes = [vp, fp, fp, fp] + [C.c_float] * 6
     L.rt_commit.argtypes = [vp]
     L.rt_scene_info.argtypes = [vp, C.POINTER(C.c_int32)]

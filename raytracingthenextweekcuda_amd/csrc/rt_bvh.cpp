@@ -267,6 +267,51 @@ void build_cf_bvh(const std::vector<v3>& vertices, const std::vector<uint32_t>& 
     build_cf_bvh_boxes(lo, hi, out);
 }
 
+namespace {
+inline float vlen(v3 a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }
+// Vector3Df::normalize (LinearAlgebra.h:30): in place, x /= norm ...
+inline v3 vnormalize(v3 a) {
+    const float n = sqrtf(a.x * a.x + a.y * a.y + a.z * a.z);
+    return v3{a.x / n, a.y / n, a.z / n};
+}
+}  // namespace
+
+void kuchkuda_triangles(const PlyMesh& m, const std::vector<uint32_t>& materials,
+                        std::vector<KTri>& out) {
+    const size_t nt = m.indices.size() / 3;
+    out.resize(nt);
+    for (size_t i = 0; i < nt; ++i) {
+        const v3 a = m.vertices[m.indices[3 * i]], b = m.vertices[m.indices[3 * i + 1]],
+                 c = m.vertices[m.indices[3 * i + 2]];
+        const v3 vc1 = sub(b, a), vc2 = sub(c, b), vc3 = sub(a, c);
+        v3 n = cross(vc1, vc2);
+        const v3 alt1 = cross(vc2, vc3);
+        if (vlen(alt1) > vlen(n)) n = alt1;
+        const v3 alt2 = cross(vc3, vc1);
+        if (vlen(alt2) > vlen(n)) n = alt2;
+        n = vnormalize(n);
+        const v3 e1 = vnormalize(cross(n, vc1)), e2 = vnormalize(cross(n, vc2)),
+                 e3 = vnormalize(cross(n, vc3));
+        KTri& t = out[i];
+        t.n[0] = n.x; t.n[1] = n.y; t.n[2] = n.z; t.d = dot(n, a);
+        t.e1[0] = e1.x; t.e1[1] = e1.y; t.e1[2] = e1.z; t.d1 = dot(e1, a);
+        t.e2[0] = e2.x; t.e2[1] = e2.y; t.e2[2] = e2.z; t.d2 = dot(e2, b);
+        t.e3[0] = e3.x; t.e3[1] = e3.y; t.e3[2] = e3.z; t.d3 = dot(e3, c);
+        t.material = (float)materials[i];
+        t.pad[0] = t.pad[1] = t.pad[2] = 0.0f;
+    }
+}
+
+std::string append_ply(const std::string& path, PlyMesh& accum) {
+    PlyMesh m;
+    std::string e = load_ply(path, m);
+    if (!e.empty()) return e;
+    const uint32_t base = (uint32_t)accum.vertices.size();
+    accum.vertices.insert(accum.vertices.end(), m.vertices.begin(), m.vertices.end());
+    for (uint32_t i : m.indices) accum.indices.push_back(i + base);
+    return "";
+}
+
 std::vector<uint8_t> bvh_image(const CFBvh& b) {
     const uint32_t nn = (uint32_t)b.nodes.size(), ni = (uint32_t)b.tri_index.size();
     std::vector<uint8_t> img(8 + (size_t)nn * sizeof(CFNode) + (size_t)ni * 4);

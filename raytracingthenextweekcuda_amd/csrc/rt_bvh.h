@@ -53,6 +53,27 @@ void build_cf_bvh(const std::vector<v3>& vertices, const std::vector<uint32_t>& 
 // Same builder over arbitrary primitive boxes (object-level BVH).
 void build_cf_bvh_boxes(const std::vector<v3>& bottoms, const std::vector<v3>& tops, CFBvh& out);
 
+// Kuchkuda triangle record of the pathTrace integrator, as uploaded by
+// prepareCUDAscene (main.cu:457-494) minus the unused centre: plane normal + d,
+// three edge planes + d1..d3 (processTriangleData, Loader.cpp:166-202) and the
+// triangle's ReflectionType.
+struct alignas(16) KTri {
+    float n[3], d;
+    float e1[3], d1;
+    float e2[3], d2;
+    float e3[3], d3;
+    float material, pad[3];
+};
+static_assert(sizeof(KTri) == 80, "KTri must be 80 B");
+
+// processTriangleData's Kuchkuda precompute over (already transformed) vertices.
+void kuchkuda_triangles(const PlyMesh& m, const std::vector<uint32_t>& materials,
+                        std::vector<KTri>& out);
+
+// loadObject appending to an existing mesh (Loader.cpp:228, 282-284: indices
+// are offset by the vertices already loaded).
+std::string append_ply(const std::string& path, PlyMesh& accum);
+
 // The `.bvh` cache image: u32 nodes, u32 indices, nodes, int32 indices.
 std::vector<uint8_t> bvh_image(const CFBvh& b);
 

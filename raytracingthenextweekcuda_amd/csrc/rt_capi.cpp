@@ -38,6 +38,16 @@ struct rt_ctx {
     bool have_events = false;
     rt_render_stats last{};
     bool stats_pending = false;
+
+    // pathTrace scene (prepareCUDAscene): raw loaded PLY data + device tables
+    rt::PlyMesh pt_raw;
+    std::vector<uint32_t> pt_materials;  // ReflectionType per triangle
+    bool pt_ready = false;
+    int pt_tris = 0;
+    rt::CFBvh pt_bvh;  // host copy (the `.bvh` cache image source)
+    rt::KTri* d_pt_tris = nullptr;
+    rt::CFNode* d_pt_nodes = nullptr;
+    int32_t* d_pt_list = nullptr;
 };
 
 namespace {
@@ -87,6 +97,19 @@ void free_device(rt_ctx* c) {
     c->d_tri_orig = nullptr;
 }
 
+void free_pathtrace(rt_ctx* c) {
+    if (c->device >= 0) {
+        (void)hipFree(c->d_pt_tris);
+        (void)hipFree(c->d_pt_nodes);
+        (void)hipFree(c->d_pt_list);
+    }
+    c->d_pt_tris = nullptr;
+    c->d_pt_nodes = nullptr;
+    c->d_pt_list = nullptr;
+    c->pt_ready = false;
+    c->pt_tris = 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -127,6 +150,7 @@ void rt_destroy(rt_ctx* c) {
     if (c->device >= 0) {
         (void)hipSetDevice(c->device);
         free_device(c);
+        free_pathtrace(c);
         (void)hipFree(c->d_counters);
         (void)hipFree(c->d_out);
         if (c->have_events) {
@@ -143,6 +167,10 @@ rt_status rt_clear_scene(rt_ctx* c) {
     if (!c) return RT_ERR_INVALID;
     c->scene = rt::HostScene();
     c->committed = false;
+    if (c->device >= 0) (void)hipSetDevice(c->device);
+    free_pathtrace(c);
+    c->pt_raw = rt::PlyMesh();
+    c->pt_materials.clear();
     return RT_OK;
 }
 
@@ -345,6 +373,65 @@ rt_status rt_mesh_vertices(const rt_ctx* c, int32_t index, float* out, int32_t m
     return RT_OK;
 }
 
+// ---- pathTrace scene (main.cu:404-553) ----
+rt_status rt_load_object(rt_ctx* c, const char* path, int32_t reflection_type) {
+    if (!c) return RT_ERR_INVALID;
+    if (!path || reflection_type < RT_PT_DIFFUSE || reflection_type > RT_PT_COAT)
+        return fail(c, RT_ERR_INVALID, "load_object: bad arguments");
+    std::string e = rt::append_ply(path, c->pt_raw);
+    if (!e.empty()) return fail(c, RT_ERR_IO, e);
+    c->pt_materials.resize(c->pt_raw.indices.size() / 3, (uint32_t)reflection_type);
+    c->pt_ready = false;
+    return RT_OK;
+}
+
+rt_status rt_process_triangle_data(rt_ctx* c, const float offset[3], float max_coord,
+                                   int32_t out_info[4]) {
+    if (!c) return RT_ERR_INVALID;
+    if (!finite3(offset) || !isfinite(max_coord) || max_coord <= 0.0f)
+        return fail(c, RT_ERR_INVALID, "process_triangle_data: bad arguments");
+    if (c->device >= 0) RT_HIP(c, hipSetDevice(c->device));
+    free_pathtrace(c);
+    rt::PlyMesh m = c->pt_raw;
+    std::vector<rt::KTri> kt;
+    rt::CFBvh b;
+    if (!m.indices.empty()) {
+        rt::process_ply_vertices(m, rt::v3{offset[0], offset[1], offset[2]}, max_coord);
+        rt::kuchkuda_triangles(m, c->pt_materials, kt);
+        rt::build_cf_bvh(m.vertices, m.indices, b);
+    }
+    if (out_info) {
+        out_info[0] = (int32_t)kt.size();
+        out_info[1] = (int32_t)b.nodes.size();
+        out_info[2] = (int32_t)b.tri_index.size();
+        out_info[3] = b.max_depth;
+    }
+    if (c->device >= 0) {
+        auto up = [&](auto** dst, const auto& vec) -> hipError_t {
+            size_t bytes = vec.size() * sizeof(vec[0]);
+            hipError_t err = hipMalloc((void**)dst, bytes ? bytes : 64);
+            if (err != hipSuccess || !bytes) return err;
+            return hipMemcpy(*dst, vec.data(), bytes, hipMemcpyHostToDevice);
+        };
+        RT_HIP(c, up(&c->d_pt_tris, kt));
+        RT_HIP(c, up(&c->d_pt_nodes, b.nodes));
+        RT_HIP(c, up(&c->d_pt_list, b.tri_index));
+    }
+    c->pt_tris = (int)kt.size();
+    c->pt_bvh = std::move(b);
+    c->pt_ready = true;
+    return RT_OK;
+}
+
+rt_status rt_pathtrace_bvh_image(const rt_ctx* c, uint8_t* out, int64_t capacity, int64_t* size) {
+    if (!c || !size) return RT_ERR_INVALID;
+    if (!c->pt_ready) return RT_ERR_STATE;
+    std::vector<uint8_t> img = rt::bvh_image(c->pt_bvh);
+    *size = (int64_t)img.size();
+    if (out && capacity > 0) memcpy(out, img.data(), (size_t)std::min<int64_t>(capacity, *size));
+    return RT_OK;
+}
+
 rt_status rt_camera(rt_ctx* c, const float eye[3], const float center[3], const float up[3],
                     float aspect, float fov, float aperture, float focus, float t0, float t1) {
     if (!c) return RT_ERR_INVALID;
@@ -409,7 +496,14 @@ rt_status rt_scene_info(const rt_ctx* c, int32_t out[8]) {
 static rt_status validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& L) {
     if (!p) return fail(c, RT_ERR_INVALID, "null params");
     if (c->device < 0) return fail(c, RT_ERR_NODEV, "context has no device");
-    if (!c->committed) return fail(c, RT_ERR_STATE, "scene not committed (call rt_commit)");
+    if (p->integrator != RT_INTEGRATOR_RAYCOLOR && p->integrator != RT_INTEGRATOR_PATHTRACE)
+        return fail(c, RT_ERR_INVALID, "unknown integrator");
+    if (p->integrator == RT_INTEGRATOR_RAYCOLOR && !c->committed)
+        return fail(c, RT_ERR_STATE, "scene not committed (call rt_commit)");
+    if (p->integrator == RT_INTEGRATOR_PATHTRACE && !c->pt_ready)
+        return fail(c, RT_ERR_STATE, "pathTrace scene not processed (call rt_process_triangle_data)");
+    if (p->integrator == RT_INTEGRATOR_PATHTRACE && p->max_depth < 1)
+        return fail(c, RT_ERR_INVALID, "pathTrace needs max_depth >= 1");
     if (!c->scene.has_camera) return fail(c, RT_ERR_STATE, "camera not set");
     if (p->width < 2 || p->height < 2) return fail(c, RT_ERR_INVALID, "width/height must be >= 2");
     if ((int64_t)p->width * p->height > (int64_t)1 << 31) return fail(c, RT_ERR_INVALID, "frame too large");
@@ -430,6 +524,7 @@ static rt_status validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch
     if (s < 0 || s > 64 || (s & (s - 1)) != 0)
         return fail(c, RT_ERR_INVALID, "lanes_per_pixel must be 0 (auto) or a power of two <= 64");
     rt::choose_layout(L, s);
+    L.pt_has_mesh = c->pt_tris > 0 ? 1 : 0;
     return RT_OK;
 }
 
@@ -443,9 +538,14 @@ rt_status rt_render_device(rt_ctx* c, const rt_render_params* p, float* out, voi
     RT_HIP(c, hipSetDevice(c->device));
     RT_HIP(c, hipMemsetAsync(c->d_counters, 0, rt::kNumCounters * sizeof(unsigned long long), st));
     RT_HIP(c, hipEventRecord(c->ev0, st));
-    rt::SceneArgs sc{c->d_objs,   c->d_tris,  c->d_mats,  c->d_nodes,
-                     c->d_tri_orig, c->n_objs, c->n_mats, !c->scene.nodes.empty()};
-    RT_HIP(c, rt::launch_render(sc, c->scene.camera, L, out, c->d_counters, st));
+    if (p->integrator == RT_INTEGRATOR_PATHTRACE) {
+        rt::PtSceneArgs pt{c->d_pt_tris, c->d_pt_nodes, c->d_pt_list};
+        RT_HIP(c, rt::launch_pathtrace(pt, c->scene.camera, L, out, c->d_counters, st));
+    } else {
+        rt::SceneArgs sc{c->d_objs,   c->d_tris,  c->d_mats,  c->d_nodes,
+                         c->d_tri_orig, c->n_objs, c->n_mats, !c->scene.nodes.empty()};
+        RT_HIP(c, rt::launch_render(sc, c->scene.camera, L, out, c->d_counters, st));
+    }
     RT_HIP(c, hipEventRecord(c->ev1, st));
     c->last = rt_render_stats{};
     c->last.samples = (uint64_t)L.local_rows * (uint64_t)L.width * (uint64_t)L.spp;

@@ -16,6 +16,7 @@ struct RenderLaunch {
     int32_t local_rows;  // rows owned by this shard (output has local_rows * width pixels)
     int32_t lanes_per_pixel;  // S: power of two in [1, 64]
     int32_t tile_w, tile_h;   // per-wave pixel tile, tile_w * tile_h = 64 / S
+    int32_t pt_has_mesh;      // pathTrace: a triangle BVH is present
 };
 
 // Lane-layout choice: S = lanes_per_pixel (0 = auto). Auto raises S (power of
@@ -40,6 +41,18 @@ inline void choose_layout(RenderLaunch& L, int32_t requested) {
 // moving spheres tested in object-BVH leaves.
 // [8..15] = diagnostic section timers (RT_STAMPS builds only).
 constexpr int kNumCounters = 16;
+
+struct KTri;
+struct CFNode;
+// Device tables of the pathTrace integrator (prepareCUDAscene, main.cu:404-553).
+struct PtSceneArgs {
+    const KTri* ktris;
+    const CFNode* nodes;      // the reference's CacheFriendlyBVHNode array, exact bounds
+    const int32_t* tri_list;  // leaf triangle lists in DFS order
+};
+
+hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec& cam, const RenderLaunch& L,
+                            float* out, unsigned long long* counters, hipStream_t stream);
 
 hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLaunch& L,
                          float* out, unsigned long long* counters, hipStream_t stream);

@@ -28,6 +28,7 @@
 // bit-identical to the CPU restatement in oracle/.
 #include <hip/hip_runtime.h>
 
+#include "rt_bvh.h"
 #include "rt_kernel.h"
 
 namespace rt {
@@ -434,6 +435,25 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
     return h;
 }
 
+// renderKernel sample loop body (main.cu:179-185) + Camera::getRay
+// (Camera.h:151-168): starts sample s's stream and returns its camera ray.
+__device__ __forceinline__ Ray camera_sample(const CamRec& cam, const RenderLaunch& L, Rng& rng,
+                                             uint32_t pixel, int px, int y, int s, float fw, float fh) {
+    rng.begin(L.seed, pixel, L.sample_offset + (uint32_t)s);
+    const float rx = rng.next();
+    const float ry = rng.next();
+    const float dx = fdiv((float)px + rx, fw);
+    const float dy = fdiv((float)y + ry, fh);
+    const v3 disk = random_in_unit_disk(rng);
+    const v3 rnd = scale(disk, cam.lens_radius);
+    const v3 offset = add(scale(cam.right, rnd.x), scale(cam.true_up, rnd.y));
+    const v3 norig = add(cam.origin, offset);
+    v3 dir = sub(add(add(cam.lower_left, scale(cam.horizontal, dx)), scale(cam.vertical, dy)), norig);
+    dir = normalize(dir);
+    const float tm = random_range(rng, cam.time0, cam.time1);
+    return Ray{add(cam.origin, offset), dir, tm};
+}
+
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     return v;
@@ -500,21 +520,7 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
         if (__ballot(alive) == 0) break;  // wave-uniform exit
         RT_STAMP(t_a);
         if (alive && need_cam) {
-            // renderKernel sample loop body (main.cu:179-185) + getRay (Camera.h:151-168).
-            rng.begin(L.seed, pixel, L.sample_offset + (uint32_t)s);
-            float rx = rng.next();
-            float ry = rng.next();
-            float dx = fdiv((float)px + rx, fw);
-            float dy = fdiv((float)y + ry, fh);
-            v3 disk = random_in_unit_disk(rng);
-            v3 rnd = scale(disk, cam.lens_radius);
-            v3 offset = add(scale(cam.right, rnd.x), scale(cam.true_up, rnd.y));
-            v3 norig = add(cam.origin, offset);
-            v3 dir = sub(add(add(cam.lower_left, scale(cam.horizontal, dx)), scale(cam.vertical, dy)),
-                         norig);
-            dir = normalize(dir);
-            float tm = random_range(rng, cam.time0, cam.time1);
-            ray = Ray{add(cam.origin, offset), dir, tm};
+            ray = camera_sample(cam, L, rng, pixel, px, y, s, fw, fh);
             thr = v3{1.0f, 1.0f, 1.0f};
             depth = 0;
             need_cam = false;
@@ -673,6 +679,355 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
         if (wgs) atomicAdd(&counters[5], (unsigned long long)wgs);
         if (wgm) atomicAdd(&counters[6], (unsigned long long)wgm);
     }
+}
+
+// ===========================================================================
+// pathTrace integrator (CUDAPathTracer.cu:358-622, wired by main.cu:187): the
+// smallpt-style material model over the Kuchkuda-triangle BVH of the loaded
+// PLY meshes plus the six built-in spheres (CUDAPathTracer.cu:94-121).
+// ===========================================================================
+namespace {
+
+enum : uint32_t { kDiffuse = 0, kMetalPhong = 1, kSpecular = 2, kRefraction = 3, kCoat = 4 };
+// `2 * M_PI` with CUDAPathTracer.cu:38's float M_PI: an exact float product.
+constexpr float kPtTwoPi = 2.0f * 3.14159265358979323846f;
+
+struct PtSphere {
+    float rad;
+    float pos[3], emi[3], col[3];
+    uint32_t type;
+};
+// CUDAPathTracer.cu:94-121 (double literals rounded to float as in the reference).
+__constant__ PtSphere kPtSpheres[6] = {
+    {1.6f, {0.0f, 2.8f, 0.0f}, {6.0f, 4.0f, 2.0f}, {0.0f, 0.0f, 0.0f}, kDiffuse},
+    {10000.0f, {50.0f, 40.8f, -1060.0f}, {0.51f, 0.51f, 0.51f}, {0.175f, 0.175f, 0.25f}, kDiffuse},
+    {100000.0f, {0.0f, -100001.1f, 0.0f}, {0.0f, 0.0f, 0.0f}, {0.5f, 0.0f, 0.0f}, kCoat},
+    {100000.0f, {0.0f, -100001.2f, 0.0f}, {0.0f, 0.0f, 0.0f}, {0.3f, 0.3f, 0.3f}, kDiffuse},
+    {110000.0f, {50.0f, -110048.5f, 0.0f}, {3.6f, 2.0f, 0.2f}, {0.0f, 0.0f, 0.0f}, kDiffuse},
+    {1.1f, {1.6f, 0.0f, 1.0f}, {0.0f, 0.0f, 0.0f}, {0.9f, 0.9f, 0.9f}, kSpecular},
+};
+
+// Sphere::intersect (CUDAPathTracer.cu:66-79): distance, 0 if no hit.
+__device__ __forceinline__ float pt_sphere_hit(int i, v3 o, v3 d) {
+    const PtSphere& sp = kPtSpheres[i];
+    const v3 op = sub(v3{sp.pos[0], sp.pos[1], sp.pos[2]}, o);
+    const float b = dot(op, d);
+    float disc = b * b - dot(op, op) + sp.rad * sp.rad;
+    if (disc < 0.0f) return 0.0f;
+    disc = fsqrt(disc);
+    float t;
+    return (t = b - disc) > 0.01f ? t : ((t = b + disc) > 0.01f ? t : 0.0f);
+}
+
+// RayIntersectsBox (CUDAPathTracer.cu:124-181), exact; also returns Tnear.
+__device__ __forceinline__ bool pt_box(const CFNode& n, v3 o, v3 d, float& tnear) {
+    float tn = -3.40282347e+38f, tf = 3.40282347e+38f;
+    const float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float lo = n.bottom[c], hi = n.top[c];
+        if (dd[c] == 0.0f) {
+            if (oo[c] < lo) return false;
+            if (oo[c] > hi) return false;
+        } else {
+            float t1 = fdiv(lo - oo[c], dd[c]);
+            float t2 = fdiv(hi - oo[c], dd[c]);
+            if (t1 > t2) {
+                const float tmp = t1;
+                t1 = t2;
+                t2 = tmp;
+            }
+            if (t1 > tn) tn = t1;
+            if (t2 < tf) tf = t2;
+            if (tn > tf) return false;
+            if (tf < 0.0f) return false;
+        }
+    }
+    tnear = tn;
+    return true;
+}
+
+}  // namespace
+
+template <bool kDummy>
+__global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
+    const KTri* __restrict__ ktris, const CFNode* __restrict__ nodes,
+    const int32_t* __restrict__ tri_list, CamRec cam, RenderLaunch L, float* __restrict__ out,
+    unsigned long long* __restrict__ counters) {
+    __shared__ uint32_t stacks[kWavesPerBlock][kStackDepth * 64];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    uint32_t* stack = &stacks[wave][lane];
+
+    const int SP = L.lanes_per_pixel;
+    const int c = lane & (SP - 1);
+    const int pix = lane / SP;
+    const int tw = L.tile_w, th = L.tile_h;
+    const int px = blockIdx.x * (2 * tw) + (wave & 1) * tw + (pix % tw);
+    const int lrow = blockIdx.y * (2 * th) + (wave >> 1) * th + (pix / tw);
+    const int lb = lrow / L.row_block;
+    const int y = (lb * L.row_world + L.row_rank) * L.row_block + (lrow - lb * L.row_block);
+    const bool valid = (px < L.width) && (lrow < L.local_rows) && (y < L.height);
+    const uint32_t pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
+
+    v3 sum{0.0f, 0.0f, 0.0f};
+    Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    int s = c;
+    bool alive = valid && s < L.spp;
+    bool need_cam = true;
+    int bounce = 0;
+    int avoid = -1;
+    v3 o{0.0f, 0.0f, 0.0f}, d{0.0f, 0.0f, 1.0f};
+    v3 mask{1.0f, 1.0f, 1.0f}, accu{0.0f, 0.0f, 0.0f};
+    Rng rng{1u, 0u, 0u, 0u};
+    const float fw = (float)(L.width - 1), fh = (float)(L.height - 1);
+    const bool has_mesh = L.pt_has_mesh != 0;
+
+    for (;;) {
+        if (__ballot(alive) == 0) break;
+        if (alive && need_cam) {
+            const Ray r = camera_sample(cam, L, rng, pixel, px, y, s, fw, fh);
+            o = r.o;
+            d = r.d;
+            mask = v3{1.0f, 1.0f, 1.0f};
+            accu = v3{0.0f, 0.0f, 0.0f};
+            avoid = -1;  // renderKernel passes avoidSelf = -1 (main.cu:187)
+            bounce = 0;
+            need_cam = false;
+        }
+        if (!alive) continue;
+        ++cnt.segs;
+
+        // BVH_IntersectTriangles (CUDAPathTracer.cu:192-352). Candidates merge on
+        // (distance^2, position in the DFS triangle list): the reference's
+        // first-in-DFS-order tie rule, so subtrees can be pruned once their
+        // entry distance exceeds the best hit without changing the result.
+        float best = 3.40282347e+38f;
+        int best_i = -1, best_idx = -1;
+        v3 best_hit{0.0f, 0.0f, 0.0f};
+        uint32_t best_mat = kDiffuse;
+        if (has_mesh) {
+            const float dd = dot(d, d);
+            stack[0] = 0u;
+            int sp = 1;
+            while (sp > 0) {
+                const uint32_t ni = stack[(--sp) * 64];
+                const CFNode nd = nodes[ni];
+                ++cnt.node_visits;
+                if (!(nd.u0 & 0x80000000u)) {
+                    float tn;
+                    if (pt_box(nd, o, d, tn)) {
+                        if (tn > 0.0f && (tn * tn) * dd > best * 1.0001f) continue;  // cannot win
+                        if (sp + 2 > kStackDepth) {
+                            cnt.overflow = 1;
+                            break;
+                        }
+                        stack[(sp++) * 64] = nd.u1;  // right
+                        stack[(sp++) * 64] = nd.u0;  // left (popped first)
+                    }
+                } else {
+                    const uint32_t n = nd.u0 & 0x7FFFFFFFu;
+                    cnt.tri_tests += n;
+                    for (uint32_t i = nd.u1; i < nd.u1 + n; ++i) {
+                        const int idx = tri_list[i];
+                        if (avoid == idx) continue;
+                        const KTri T = ktris[idx];
+                        const v3 nn{T.n[0], T.n[1], T.n[2]};
+                        const float k = dot(nn, d);
+                        if (k == 0.0f) continue;
+                        const float sd = fdiv(T.d - dot(nn, o), k);
+                        if (sd <= 0.0f) continue;
+                        if (sd <= 1e-3f) continue;  // NUDGE_FACTOR
+                        const v3 hit = add(scale(d, sd), o);
+                        if (dot(v3{T.e1[0], T.e1[1], T.e1[2]}, hit) - T.d1 < 0.0f) continue;
+                        if (dot(v3{T.e2[0], T.e2[1], T.e2[2]}, hit) - T.d2 < 0.0f) continue;
+                        if (dot(v3{T.e3[0], T.e3[1], T.e3[2]}, hit) - T.d3 < 0.0f) continue;
+                        const v3 df = sub(o, hit);
+                        const float hz = df.x * df.x + df.y * df.y + df.z * df.z;  // distancesq
+                        if (hz < best || (hz == best && (int)i < best_i)) {
+                            best = hz;
+                            best_i = (int)i;
+                            best_idx = idx;
+                            best_hit = hit;
+                            best_mat = (uint32_t)T.material;
+                        }
+                    }
+                }
+            }
+        }
+        const float hitdistance = best_idx >= 0 ? fsqrt(best) : 1e20f;
+
+        // the six spheres, scanned i = 5 .. 0 (CUDAPathTracer.cu:400-404)
+        float scene_t = 1e20f;
+        int sphere_id = -1, geom = -1;
+        for (int i = 5; i >= 0; --i) {
+            const float dist = pt_sphere_hit(i, o, d);
+            if (dist != 0.0f && dist < scene_t) {
+                scene_t = dist;
+                sphere_id = i;
+                geom = 1;
+            }
+        }
+        avoid = best_idx;  // avoidSelf = pBestTriIdx (CUDAPathTracer.cu:408)
+        if (hitdistance < scene_t && hitdistance > 0.002f) {
+            scene_t = hitdistance;
+            geom = 2;
+        }
+
+        bool done = false;
+        v3 contrib{0.0f, 0.0f, 0.0f};
+        if (geom < 0 || scene_t > 1e20f) {
+            done = true;  // escaped: black (CUDAPathTracer.cu:417)
+        } else {
+            v3 hitp, normal, oriented, f;
+            uint32_t rt;
+            if (geom == 1) {
+                const PtSphere& sp = kPtSpheres[sphere_id];
+                hitp = add(o, scale(d, scene_t));
+                normal = normalize(sub(hitp, v3{sp.pos[0], sp.pos[1], sp.pos[2]}));
+                oriented = dot(normal, d) < 0.0f ? normal : scale(normal, -1.0f);
+                f = v3{sp.col[0], sp.col[1], sp.col[2]};
+                rt = sp.type;
+                accu = add(accu, mul(mask, v3{sp.emi[0], sp.emi[1], sp.emi[2]}));
+            } else {
+                const KTri& T = ktris[best_idx];
+                hitp = best_hit;
+                normal = normalize(v3{T.n[0], T.n[1], T.n[2]});
+                oriented = dot(normal, d) < 0.0f ? normal : scale(normal, -1.0f);
+                f = v3{0.9f, 0.3f, 0.0f};  // hard-coded triangle colour (CUDAPathTracer.cu:444)
+                rt = best_mat;
+                accu = add(accu, mul(mask, v3{0.0f, 0.0f, 0.0f}));
+            }
+            v3 next = d, point = hitp;
+            auto hemisphere = [&](v3 w, float phi, float r2) {
+                // orthonormal frame + cosine-weighted direction (CUDAPathTracer.cu:462-469)
+                const v3 a = ((double)fabsf(w.x) > 0.1) ? v3{0.0f, 1.0f, 0.0f} : v3{1.0f, 0.0f, 0.0f};
+                const v3 uu = normalize(cross(a, w));
+                const v3 vv = cross(w, uu);
+                const float r2s = fsqrt(r2);
+                const v3 dir = add(add(scale(scale(uu, pt_cosf(phi)), r2s), scale(scale(vv, pt_sinf(phi)), r2s)),
+                                   scale(w, fsqrt(1.0f - r2)));
+                return normalize(dir);
+            };
+            const v3 mirror = sub(d, scale(scale(normal, 2.0f), dot(normal, d)));
+            if (rt == kDiffuse) {
+                const float phi = kPtTwoPi * rng.next();
+                const float r2 = rng.next();
+                const v3 w = normalize(oriented);
+                next = hemisphere(w, phi, r2);
+                point = add(hitp, scale(w, 0.01f));
+                mask = mul(mask, f);
+            } else if (rt == kMetalPhong) {
+                const float phi = kPtTwoPi * rng.next();
+                const float r2 = rng.next();
+                const float cos_t = pt_powf(1.0f - r2, 1.0f / (20.0f + 1.0f));
+                const float sin_t = fsqrt(1.0f - cos_t * cos_t);
+                const v3 w = normalize(mirror);
+                const v3 a = ((double)fabsf(w.x) > 0.1) ? v3{0.0f, 1.0f, 0.0f} : v3{1.0f, 0.0f, 0.0f};
+                const v3 uu = normalize(cross(a, w));
+                const v3 vv = cross(w, uu);
+                next = normalize(add(add(scale(scale(uu, pt_cosf(phi)), sin_t), scale(scale(vv, pt_sinf(phi)), sin_t)),
+                                     scale(w, cos_t)));
+                point = add(hitp, scale(w, 0.01f));
+                mask = mul(mask, f);
+            } else if (rt == kSpecular) {
+                next = mirror;
+                point = add(hitp, scale(oriented, 0.01f));
+                mask = mul(mask, f);
+            } else if (rt == kCoat) {
+                if (rng.next() < 0.05f) {
+                    mask = mul(mask, v3{1.0f, 1.0f, 1.0f});
+                    next = mirror;
+                    point = add(hitp, scale(oriented, 0.01f));
+                } else {
+                    const float r1 = kPtTwoPi * rng.next();
+                    const float r2 = rng.next();
+                    next = hemisphere(normalize(oriented), r1, r2);
+                    point = add(hitp, scale(oriented, 0.01f));
+                    mask = mul(mask, f);
+                }
+            } else {  // kRefraction (CUDAPathTracer.cu:566-614)
+                const bool into = dot(normal, oriented) > 0.0f;
+                const float nc = 1.0f, nt = 1.5f;
+                const float nnt = into ? nc / nt : nt / nc;
+                const float ddn = dot(d, oriented);
+                const float cos2t = 1.0f - nnt * nnt * (1.0f - ddn * ddn);
+                if (cos2t < 0.0f) {
+                    next = mirror;
+                    point = add(hitp, scale(oriented, 0.01f));
+                } else {
+                    v3 tdir = scale(d, nnt);
+                    tdir = sub(tdir, scale(normal, (float)(into ? 1 : -1) * (ddn * nnt + fsqrt(cos2t))));
+                    tdir = normalize(tdir);
+                    const float R0 = (nt - nc) * (nt - nc) / (nt + nc) * (nt + nc);  // sic
+                    const float cc = 1.0f - (into ? -ddn : dot(tdir, normal));
+                    const float Re = R0 + (1.0f - R0) * cc * cc * cc * cc * cc;
+                    const float Tr = 1.0f - Re;
+                    const float P = 0.25f + 0.5f * Re;
+                    const float RP = fdiv(Re, P), TP = fdiv(Tr, 1.0f - P);
+                    if (rng.next() < 0.25f) {
+                        mask = scale(mask, RP);
+                        next = mirror;
+                        point = add(hitp, scale(oriented, 0.01f));
+                    } else {
+                        mask = scale(mask, TP);
+                        next = tdir;
+                        point = add(hitp, scale(oriented, 0.001f));
+                    }
+                }
+            }
+            o = point;
+            d = next;
+            if (++bounce == L.max_depth) {  // 5 in the reference (CUDAPathTracer.cu:366)
+                done = true;
+                contrib = accu;
+            }
+        }
+        if (done) {
+            sum = add(sum, contrib);
+            need_cam = true;
+            s += SP;
+            if (s >= L.spp) alive = false;
+        }
+    }
+
+    if (SP > 1) {
+        const int base = lane - c;
+        v3 acc = sum;
+        for (int j = 1; j < SP; ++j) {
+            v3 pj{__shfl(sum.x, base + j, 64), __shfl(sum.y, base + j, 64), __shfl(sum.z, base + j, 64)};
+            acc = add(acc, pj);
+        }
+        sum = acc;
+    }
+    if (valid && c == 0) {
+        const float fs = (float)L.spp;
+        const size_t oi = ((size_t)lrow * (size_t)L.width + (size_t)px) * 3;
+        out[oi + 0] = sum.x / fs;
+        out[oi + 1] = sum.y / fs;
+        out[oi + 2] = sum.z / fs;
+    }
+    const uint64_t ws = wave_sum_u64(cnt.segs);
+    const uint64_t wt = wave_sum_u64(cnt.tri_tests);
+    const uint64_t wn = wave_sum_u64(cnt.node_visits);
+    const uint64_t wo = wave_sum_u64(cnt.overflow);
+    if (lane == 0) {
+        atomicAdd(&counters[0], (unsigned long long)ws);
+        atomicAdd(&counters[1], (unsigned long long)wt);
+        if (wn) atomicAdd(&counters[3], (unsigned long long)wn);
+        if (wo) atomicAdd(&counters[4], (unsigned long long)wo);
+    }
+}
+
+hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec& cam, const RenderLaunch& L,
+                            float* out, unsigned long long* counters, hipStream_t stream) {
+    dim3 block(64 * kWavesPerBlock);
+    dim3 grid((L.width + 2 * L.tile_w - 1) / (2 * L.tile_w),
+              (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
+    if (grid.x == 0 || grid.y == 0) return hipSuccess;
+    hipLaunchKernelGGL(pathtrace_kernel<true>, grid, block, 0, stream, sc.ktris, sc.nodes,
+                       sc.tri_list, cam, L, out, counters);
+    return hipGetLastError();
 }
 
 hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLaunch& L, float* out,

@@ -15,7 +15,7 @@
 #define RT_HD __host__ __device__ __forceinline__
 #else
 #include <math.h>
-#define RT_HD static inline
+#define RT_HD inline
 #endif
 
 namespace rt {
@@ -184,6 +184,110 @@ RT_HD v3 refract(v3 uv, v3 n, float eta) {
 RT_HD float pow5(float x) {
     float x2 = x * x;
     return (x2 * x2) * x;
+}
+
+// ---------------------------------------------------------------------------
+// Transcendentals of the pathTrace integrator: cosf/sinf/powf at
+// CUDAPathTracer.cu:468,486,496,553 (the reference built them with
+// --use_fast_math, i.e. __cosf/__sinf/__powf, which are not reproducible).
+// Here they are evaluated in IEEE double with fixed polynomial kernels and
+// exact frexp/ldexp, so host and device produce the same bits; results are
+// within ~1 ulp of the correctly rounded float functions.
+// ---------------------------------------------------------------------------
+#if defined(__HIPCC__)
+#define RT_HD_NOINLINE __host__ __device__
+#else
+#define RT_HD_NOINLINE static
+#endif
+
+// sin / cos of x (|x| up to ~1e6): Cody-Waite reduction by pi/2, Taylor
+// polynomials to degree 17 / 16 on [-pi/4, pi/4].
+RT_HD void sincos_d(double x, double* s, double* c) {
+    const double two_over_pi = 0.63661977236758134308;
+    const double pio2_hi = 1.57079632673412561417;      // first 33 bits of pi/2
+    const double pio2_lo = 6.07710050650619224932e-11;  // pi/2 - pio2_hi
+    const double k = floor(x * two_over_pi + 0.5);
+    const double r = (x - k * pio2_hi) - k * pio2_lo;
+    const double r2 = r * r;
+    double ps = 1.0 / 355687428096000.0;                 // 1/17!
+    ps = ps * r2 - 1.0 / 1307674368000.0;                // 1/15!
+    ps = ps * r2 + 1.0 / 6227020800.0;
+    ps = ps * r2 - 1.0 / 39916800.0;
+    ps = ps * r2 + 1.0 / 362880.0;
+    ps = ps * r2 - 1.0 / 5040.0;
+    ps = ps * r2 + 1.0 / 120.0;
+    ps = ps * r2 - 1.0 / 6.0;
+    const double sn = r + (r * r2) * ps;
+    double pc = 1.0 / 20922789888000.0;                  // 1/16!
+    pc = pc * r2 - 1.0 / 87178291200.0;
+    pc = pc * r2 + 1.0 / 479001600.0;
+    pc = pc * r2 - 1.0 / 3628800.0;
+    pc = pc * r2 + 1.0 / 40320.0;
+    pc = pc * r2 - 1.0 / 720.0;
+    pc = pc * r2 + 1.0 / 24.0;
+    pc = pc * r2 - 0.5;
+    const double cs = 1.0 + r2 * pc;
+    const long q = ((long)k) & 3;
+    *s = q == 0 ? sn : q == 1 ? cs : q == 2 ? -sn : -cs;
+    *c = q == 0 ? cs : q == 1 ? -sn : q == 2 ? -cs : sn;
+}
+
+RT_HD float pt_sinf(float x) {
+    double s, c;
+    sincos_d((double)x, &s, &c);
+    return (float)s;
+}
+RT_HD float pt_cosf(float x) {
+    double s, c;
+    sincos_d((double)x, &s, &c);
+    return (float)c;
+}
+
+// x^y for x >= 0 (powf at CUDAPathTracer.cu:486): exp(y * ln x) with an atanh
+// series for ln on [sqrt(1/2), sqrt(2)) and a Taylor exp after reduction by ln 2.
+RT_HD float pt_powf(float xf, float yf) {
+    if (!(xf > 0.0f)) return xf == 0.0f ? (yf > 0.0f ? 0.0f : 1.0f) : __builtin_nanf("");
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    int e;
+    double m = frexp((double)xf, &e);  // exact: m in [0.5, 1)
+    if (m < 0.70710678118654752440) {
+        m = m * 2.0;
+        e = e - 1;
+    }
+    const double t = (m - 1.0) / (m + 1.0), t2 = t * t;
+    double p = 1.0 / 23.0;
+    p = p * t2 + 1.0 / 21.0;
+    p = p * t2 + 1.0 / 19.0;
+    p = p * t2 + 1.0 / 17.0;
+    p = p * t2 + 1.0 / 15.0;
+    p = p * t2 + 1.0 / 13.0;
+    p = p * t2 + 1.0 / 11.0;
+    p = p * t2 + 1.0 / 9.0;
+    p = p * t2 + 1.0 / 7.0;
+    p = p * t2 + 1.0 / 5.0;
+    p = p * t2 + 1.0 / 3.0;
+    p = p * t2 + 1.0;
+    const double ln_m = 2.0 * t * p;
+    const double de = (double)e;
+    const double lnx = (de * ln2_hi + ln_m) + de * ln2_lo;
+    const double z = (double)yf * lnx;
+    const double n = floor(z * 1.44269504088896338700 + 0.5);
+    const double r = (z - n * ln2_hi) - n * ln2_lo;
+    double q = 1.0 / 6227020800.0;  // 1/13!
+    q = q * r + 1.0 / 479001600.0;
+    q = q * r + 1.0 / 39916800.0;
+    q = q * r + 1.0 / 3628800.0;
+    q = q * r + 1.0 / 362880.0;
+    q = q * r + 1.0 / 40320.0;
+    q = q * r + 1.0 / 5040.0;
+    q = q * r + 1.0 / 720.0;
+    q = q * r + 1.0 / 120.0;
+    q = q * r + 1.0 / 24.0;
+    q = q * r + 1.0 / 6.0;
+    q = q * r + 0.5;
+    q = q * r + 1.0;
+    q = q * r + 1.0;
+    return (float)ldexp(q, (int)n);
 }
 
 }  // namespace rt

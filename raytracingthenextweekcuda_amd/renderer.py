@@ -164,6 +164,25 @@ class Renderer:
         self._check(self.L.rt_mesh_ply(self.ctx, index, str(path).encode(), _v(offset), max_coord,
                                        _mat_index(material)))
 
+    # ---- pathTrace scene (prepareCUDAscene, main.cu:404-553) ----
+    def load_object(self, path, reflection_type="COAT"):
+        """loadObject(file, ReflectionType, meshIndex) (Loader.cpp:207-319): append a PLY mesh."""
+        self._check(self.L.rt_load_object(self.ctx, str(path).encode(), _reflection_type(reflection_type)))
+
+    def process_triangle_data(self, offset=(0.0, 0.0, 0.0), max_coord=1.0) -> dict:
+        """processTriangleData (Loader.cpp:98-205) + BVH build + upload. Returns the census."""
+        out = (C.c_int32 * 4)()
+        self._check(self.L.rt_process_triangle_data(self.ctx, _v(offset), max_coord, out))
+        return {"triangles": out[0], "bvh_nodes": out[1], "tri_list": out[2], "depth": out[3]}
+
+    def pathtrace_bvh_image(self) -> bytes:
+        """The `.bvh` cache image of the processed pathTrace scene (BVH.cpp:537-540)."""
+        size = C.c_int64()
+        self._check(self.L.rt_pathtrace_bvh_image(self.ctx, None, 0, C.byref(size)))
+        buf = (C.c_uint8 * size.value)()
+        self._check(self.L.rt_pathtrace_bvh_image(self.ctx, buf, size.value, C.byref(size)))
+        return bytes(buf)
+
     def mesh_vertices(self, index) -> np.ndarray:
         n = self.L.rt_mesh_triangle_count(self.ctx, index)
         out = np.zeros((n, 9), np.float32)
@@ -192,17 +211,19 @@ class Renderer:
     # ---- render ----
     @staticmethod
     def params(width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,
-               row_rank=0, row_world=1, lanes_per_pixel=1) -> RenderParams:
+               row_rank=0, row_world=1, lanes_per_pixel=1, integrator="rayColor") -> RenderParams:
         return RenderParams(width, height, spp, max_depth, seed, sample_offset, row_block,
-                            row_rank, row_world, lanes_per_pixel)
+                            row_rank, row_world, lanes_per_pixel, _integrator(integrator))
 
     def render(self, width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,
-               row_rank=0, row_world=1, lanes_per_pixel=1) -> np.ndarray:
+               row_rank=0, row_world=1, lanes_per_pixel=1, integrator="rayColor") -> np.ndarray:
         """Mean radiance of the owned rows, shape (rows, width, 3), y = 0 bottom.
         lanes_per_pixel=1 keeps the reference's sequential per-pixel sample sum;
-        0 lets the library pick a lane layout that fills the GPU."""
+        0 lets the library pick a lane layout that fills the GPU. integrator
+        "pathTrace" runs CUDAPathTracer.cu's integrator over the
+        load_object/process_triangle_data scene (max_depth = its 5 bounces)."""
         p = self.params(width, height, spp, max_depth, seed, sample_offset, row_block, row_rank,
-                        row_world, lanes_per_pixel)
+                        row_world, lanes_per_pixel, integrator)
         rows = owned_rows(height, row_block, row_rank, row_world)
         out = np.zeros((rows, width, 3), np.float32)
         self._check(self.L.rt_render(self.ctx, C.byref(p), out.ctypes.data_as(C.POINTER(C.c_float))))
@@ -220,6 +241,22 @@ class Renderer:
         d = {k: getattr(s, k) for k, _ in RenderStats._fields_}
         d["debug"] = list(s.debug)
         return d
+
+
+REFLECTION_TYPES = {"DIFFUSE": 0, "METAL": 1, "SPECULAR": 2, "REFRACTION": 3, "COAT": 4}
+INTEGRATORS = {"rayColor": 0, "pathTrace": 1}
+
+
+def _reflection_type(t) -> int:
+    if isinstance(t, str):
+        return REFLECTION_TYPES[t.upper()]
+    return int(t)
+
+
+def _integrator(i) -> int:
+    if isinstance(i, str):
+        return INTEGRATORS[i]
+    return int(i)
 
 
 def owned_rows(height, block, rank, world) -> int:

@@ -135,3 +135,44 @@ def duplicate_spheres_scene(n_extra=20):
         ],
         "objects": objs,
     }
+
+
+# ---- pathTrace integrator scenes (prepareCUDAscene, main.cu:404-553) ----
+# Each names the PLY files (with their ReflectionType), the processTriangleData
+# offset and the reference's own `.bvh` cache file for that combination.
+PT_CAMERA = ((0.0, 0.5, 3.0), (0.1, 0.0, -1.0), (0.0, 1.0, 0.0), 1.0, 45.0, 0.0, 4.0, 0.0, 1.0)
+PT_SCENES = {
+    # the committed configuration (main.cu:430-432)
+    "materialball": ([("materialball/materialball.ply", "COAT")], (0.1, 0.0, -1.0), "materialball.ply.bvh"),
+    # the commented three-suzanne configuration (main.cu:418-428); its cache is
+    # the reference's suzanne/suzanne2.ply.bvh
+    "suzanne": ([("suzanne/suzanne0.ply", "COAT"), ("suzanne/suzanne1.ply", "REFRACTION"),
+                 ("suzanne/suzanne2.ply", "METAL")], (0.0, 0.0, 0.0), "suzanne012.ply.bvh"),
+    "bunny": ([("bunny/bunny.ply", "DIFFUSE")], (0.0, 0.0, 0.0), "bunny.ply.bvh"),
+}
+
+
+def build_pathtrace_product(r, name, camera=PT_CAMERA):
+    import raytracingthenextweekcuda_amd as rtmi
+
+    plys, offset, _ = PT_SCENES[name]
+    r.set_camera(rtmi.Camera(*camera))
+    for path, kind in plys:
+        r.load_object(os.path.join(MODELS, path), kind)
+    return r.process_triangle_data(offset)
+
+
+def build_pathtrace_oracle(name, camera=PT_CAMERA):
+    """(OraclePathTrace, camera OracleScene), the BVH from the reference's cache file."""
+    from oracle import oracle as orc
+
+    plys, offset, bvh = PT_SCENES[name]
+    pt = orc.OraclePathTrace()
+    for path, kind in plys:
+        pt.load_object(os.path.join(MODELS, path), kind)
+    pt.process(offset)
+    with open(os.path.join(GOLDEN, "bvh", bvh), "rb") as fh:
+        pt.set_bvh(fh.read())
+    cam = orc.OracleScene()
+    cam.camera(*camera)
+    return pt, cam

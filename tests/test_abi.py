@@ -25,7 +25,8 @@ def test_library_exports_every_declared_symbol():
     L = _lib.lib()
     for name in declared_symbols():
         assert hasattr(L, name), name
-    assert L.rt_abi_version() == 1
+    assert L.rt_abi_version() == _lib.ABI_VERSION
+    assert f"#define RTMI_ABI_VERSION {_lib.ABI_VERSION}" in open(HEADER).read()
 
 
 def test_nodev_context_builds_scene_but_refuses_render():
