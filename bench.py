@@ -26,7 +26,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 # Algorithmic bytes per record touched: plane 40 B, sphere
 # 20 B, moving sphere 36 B, mesh AABB 24 B, triangle (v0,E1,E2) 36 B, BVH node
 # 32 B, and 12 B per output pixel.
-BYTES = {"plane": 40, "sphere": 20, "moving_sphere": 36, "box": 24, "tri": 36, "node": 32, "pixel": 12}
+BYTES = {"plane": 40, "sphere": 20, "moving_sphere": 36, "box": 24, "tri": 36, "node": 32, "pixel": 12,
+         # pathTrace: triangle-list entry 4 B + Kuchkuda planes (n,d,e1,d1,e2,d2,e3,d3) 64 B
+         "ktri": 68}
 
 
 # BASELINE.json configs: scene loader, default W, H, spp, depth.
@@ -34,7 +36,11 @@ SCENES = {
     "cornellbox1": ("cornell_box1", 512, 512, 128, 8, "CornellBox1 (6 planes + 2 cube_small.obj meshes, 24 triangles)"),
     "spheres": ("random_spheres", 1280, 720, 256, 10, "RTNW final scene (488 spheres, 388 moving; object BVH)"),
     "bunny": ("bunny_cornell_box", 1024, 1024, 512, 8, "bun_zipper.ply (69,451 triangles, SAH BVH) in CornellBox1 walls"),
+    # the reference's committed renderKernel configuration (pathTrace, main.cu:187;
+    # samplesPerPixel 32, 5 bounces); not a BASELINE config, reported separately
+    "materialball": ("materialball", 512, 512, 32, 5, "materialball.ply (46,816 triangles, COAT) + 6 spheres, pathTrace integrator"),
 }
+INTEGRATOR = {"materialball": "pathTrace"}
 
 
 def parse():
@@ -61,7 +67,8 @@ def parse():
     # CPU-baseline sample (a bounded slice of the same workload, ~1-10 s on 16
     # threads): the restatement scans meshes brute force like the reference's
     # TriangleMesh::hit, so the bunny sample is a 1/16-scale frame at 1 spp.
-    a.cpu_div, cpu_spp = {"cornellbox1": (1, 32), "spheres": (2, 4), "bunny": (16, 1)}[a.scene]
+    a.cpu_div, cpu_spp = {"cornellbox1": (1, 32), "spheres": (2, 4), "bunny": (16, 1),
+                          "materialball": (1, 32)}[a.scene]
     a.cpu_spp = a.cpu_spp or cpu_spp
     return a
 
@@ -84,15 +91,30 @@ def cpu_baseline(args, threads: int):
 
     scenes = os.path.join(REPO, "assets", "scenes")
     w, h = args.width // args.cpu_div, args.height // args.cpu_div
-    if args.scene == "spheres":
+    if args.scene == "materialball":
+        # pathTrace: the restatement traverses the reference's own `.bvh` cache
+        # (tests/golden) as BVH_IntersectTriangles does (full DFS, no pruning).
+        cam = orc.yaml_scene(os.path.join(scenes, "cornellbox2.yaml"), os.path.join(REPO, "assets", "models"), w, h)
+        pt = orc.OraclePathTrace()
+        pt.load_object(os.path.join(REPO, "assets", "models", "materialball", "materialball.ply"), "COAT")
+        pt.process((0.1, 0.0, -1.0))
+        with open(os.path.join(REPO, "tests", "golden", "bvh", "materialball.ply.bvh"), "rb") as fh:
+            pt.set_bvh(fh.read())
+        pt.render(cam, 16, 16, 1, args.depth, threads=threads)  # warm-up
+        t0 = time.perf_counter()
+        _, st = pt.render(cam, w, h, args.cpu_spp, args.depth, threads=threads)
+        dt = time.perf_counter() - t0
+        sc = None
+    elif args.scene == "spheres":
         sc = orc.json_scene(os.path.join(scenes, "random_spheres.json"), w, h)
     else:
         name = "cornellbox1.yaml" if args.scene == "cornellbox1" else "bunny_cornellbox.yaml"
         sc = orc.yaml_scene(os.path.join(scenes, name), os.path.join(REPO, "assets", "models"), w, h)
-    sc.render(16, 16, 1, args.depth, threads=threads)  # warm-up
-    t0 = time.perf_counter()
-    _, st = sc.render(w, h, args.cpu_spp, args.depth, threads=threads)
-    dt = time.perf_counter() - t0
+    if sc is not None:
+        sc.render(16, 16, 1, args.depth, threads=threads)  # warm-up
+        t0 = time.perf_counter()
+        _, st = sc.render(w, h, args.cpu_spp, args.depth, threads=threads)
+        dt = time.perf_counter() - t0
     frame_ms = dt * 1e3 * (args.width * args.height * args.spp) / (w * h * args.cpu_spp)
     return {
         "value": st["segments"] / dt / 1e6,
@@ -151,7 +173,8 @@ def main():
     rows = rtmi.owned_rows(H, block, rank, world)
     frame = RowShardedFrame(W, H, block,
                             device=torch.device("cpu") if rehearsal else torch.device("cuda", local))
-    params = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, world, args.lanes)
+    integrator = INTEGRATOR.get(args.scene, "rayColor")
+    params = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, world, args.lanes, integrator)
     stream = torch.cuda.current_stream()
     scratch = torch.empty(frame.tile.shape, dtype=torch.float32, device="cuda") if rehearsal else None
 
@@ -209,7 +232,9 @@ def main():
         # Roofline of the megakernel: algorithmic record bytes per launch
         # (rank 0's launch stands for the per-GPU launch).
         seg_launch = segs / K / world
-        alg_bytes = (seg_launch * object_bytes_per_segment(r) + tri_tests / K / world * BYTES["tri"]
+        pt = integrator == "pathTrace"
+        alg_bytes = (seg_launch * (6 * BYTES["sphere"] if pt else object_bytes_per_segment(r))
+                     + tri_tests / K / world * BYTES["ktri" if pt else "tri"]
                      + box_tests / K / world * BYTES["box"] + nodes / K / world * BYTES["node"]
                      + grp / K / world
                      + rows_tot / world * W * BYTES["pixel"])

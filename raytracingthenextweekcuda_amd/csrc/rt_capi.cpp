@@ -44,6 +44,7 @@ struct rt_ctx {
     std::vector<uint32_t> pt_materials;  // ReflectionType per triangle
     bool pt_ready = false;
     int pt_tris = 0;
+    float pt_scale = 0.0f;  // max |coordinate| of the processed triangles
     rt::CFBvh pt_bvh;  // host copy (the `.bvh` cache image source)
     rt::KTri* d_pt_tris = nullptr;
     rt::CFNode* d_pt_nodes = nullptr;
@@ -393,11 +394,16 @@ rt_status rt_process_triangle_data(rt_ctx* c, const float offset[3], float max_c
     if (c->device >= 0) RT_HIP(c, hipSetDevice(c->device));
     free_pathtrace(c);
     rt::PlyMesh m = c->pt_raw;
+    float scale_max = 0.0f;
     std::vector<rt::KTri> kt;
     rt::CFBvh b;
     if (!m.indices.empty()) {
         rt::process_ply_vertices(m, rt::v3{offset[0], offset[1], offset[2]}, max_coord);
         rt::kuchkuda_triangles(m, c->pt_materials, kt);
+        for (uint32_t i : m.indices) {
+            const rt::v3 v = m.vertices[i];
+            scale_max = std::max(scale_max, std::max(fabsf(v.x), std::max(fabsf(v.y), fabsf(v.z))));
+        }
         rt::build_cf_bvh(m.vertices, m.indices, b);
     }
     if (out_info) {
@@ -418,6 +424,7 @@ rt_status rt_process_triangle_data(rt_ctx* c, const float offset[3], float max_c
         RT_HIP(c, up(&c->d_pt_list, b.tri_index));
     }
     c->pt_tris = (int)kt.size();
+    c->pt_scale = scale_max;
     c->pt_bvh = std::move(b);
     c->pt_ready = true;
     return RT_OK;
@@ -525,6 +532,7 @@ static rt_status validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch
         return fail(c, RT_ERR_INVALID, "lanes_per_pixel must be 0 (auto) or a power of two <= 64");
     rt::choose_layout(L, s);
     L.pt_has_mesh = c->pt_tris > 0 ? 1 : 0;
+    L.pt_scale = c->pt_scale;
     return RT_OK;
 }
 

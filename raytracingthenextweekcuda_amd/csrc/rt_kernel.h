@@ -17,6 +17,7 @@ struct RenderLaunch {
     int32_t lanes_per_pixel;  // S: power of two in [1, 64]
     int32_t tile_w, tile_h;   // per-wave pixel tile, tile_w * tile_h = 64 / S
     int32_t pt_has_mesh;      // pathTrace: a triangle BVH is present
+    float pt_scale;           // pathTrace: max |coordinate| of the triangles
 };
 
 // Lane-layout choice: S = lanes_per_pixel (0 = auto). Auto raises S (power of

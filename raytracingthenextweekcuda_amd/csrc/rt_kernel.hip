@@ -105,15 +105,6 @@ __device__ __forceinline__ v3 moving_center(const float* f, float time) {
     return add(c0, scale(sub(c1, c0), (time - f[6]) / (f[7] - f[6])));
 }
 
-// In-rectangle test of Plane::hit for the plane's orientation.
-__device__ __forceinline__ bool plane_in_range(v3 p, const float* f, uint32_t orient) {
-    if (orient == 0u)
-        return (p.x > f[0] - f[6]) && (p.x < f[0] + f[6]) && (p.y > f[1] - f[7]) && (p.y < f[1] + f[7]);
-    if (orient == 1u)
-        return (p.y > f[1] - f[7]) && (p.y < f[1] + f[7]) && (p.z > f[2] - f[8]) && (p.z < f[2] + f[8]);
-    return (p.x > f[0] - f[6]) && (p.x < f[0] + f[6]) && (p.z > f[2] - f[8]) && (p.z < f[2] + f[8]);
-}
-
 // One triangle of TriangleMesh::hit (TriangleMesh.cu:40-108) without the
 // closestSoFar comparison: returns t if every other acceptance test passes,
 // else NaN (compares false with anything). The caller applies closestSoFar.
@@ -747,6 +738,187 @@ __device__ __forceinline__ bool pt_box(const CFNode& n, v3 o, v3 d, float& tnear
     return true;
 }
 
+// Per-segment ray data for the pathTrace traversal.
+struct PtRay {
+    v3 o, d;
+    v3 inv;        // v_rcp_f32(d) per axis (1 ulp)
+    v3 pad_t;      // eps * |inv|: widens each slab by eps for the pruning bound
+    bool exact;    // a direction component is tiny but non-zero: always divide
+};
+
+// Exact-decision box test: the same accept/reject as RayIntersectsBox
+// (pt_box). The slab parameters come from the reciprocal (relative error
+// < 2^-21 against the correctly rounded quotient); the decision reduces to
+// `tnear > tfar || tfar < 0` (the early-outs are monotone), the signs are
+// exact, and only a tnear/tfar gap inside the rounding band falls back to the
+// divisions. `tn` is a lower bound of the entry parameter of the box widened
+// by eps (pruning only); `order` is the unwidened entry (child ordering).
+__device__ __forceinline__ bool pt_box_decide(const CFNode& n, const PtRay& r, float& tn_prune,
+                                              float& order) {
+    float tn = -3.40282347e+38f, tf = 3.40282347e+38f, tw = -3.40282347e+38f;
+    bool miss = false;
+    const float oo[3] = {r.o.x, r.o.y, r.o.z}, dd[3] = {r.d.x, r.d.y, r.d.z};
+    const float iv[3] = {r.inv.x, r.inv.y, r.inv.z}, pt[3] = {r.pad_t.x, r.pad_t.y, r.pad_t.z};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float lo = n.bottom[c], hi = n.top[c];
+        if (dd[c] == 0.0f) {
+            miss |= (oo[c] < lo) | (oo[c] > hi);
+        } else {
+            const float t1 = (lo - oo[c]) * iv[c];
+            const float t2 = (hi - oo[c]) * iv[c];
+            const float tnear_c = fminf(t1, t2);
+            tn = fmaxf(tn, tnear_c);
+            tf = fminf(tf, fmaxf(t1, t2));
+            tw = fmaxf(tw, tnear_c - pt[c]);
+        }
+    }
+    tn_prune = tw;
+    order = tn;
+    if (miss) return false;
+    const float m = fmaxf(fabsf(tn), fabsf(tf));
+    if (!r.exact && m < 1e30f && fabsf(tn - tf) > 4e-6f * m) return tn <= tf && !(tf < 0.0f);
+    float tx;
+    return pt_box(n, r.o, r.d, tx);
+}
+
+// Entry-parameter bounds of a leaf box (leaves are never box-tested by the
+// reference: these only order and prune).
+__device__ __forceinline__ void pt_box_bounds(const CFNode& n, const PtRay& r, float& tn_prune,
+                                              float& order) {
+    float tn = -3.40282347e+38f, tw = -3.40282347e+38f;
+    const float oo[3] = {r.o.x, r.o.y, r.o.z}, dd[3] = {r.d.x, r.d.y, r.d.z};
+    const float iv[3] = {r.inv.x, r.inv.y, r.inv.z}, pt[3] = {r.pad_t.x, r.pad_t.y, r.pad_t.z};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        if (dd[c] != 0.0f && !r.exact) {
+            const float t1 = (n.bottom[c] - oo[c]) * iv[c];
+            const float t2 = (n.top[c] - oo[c]) * iv[c];
+            const float tnear_c = fminf(t1, t2);
+            tn = fmaxf(tn, tnear_c);
+            tw = fmaxf(tw, tnear_c - pt[c]);
+        }
+    }
+    tn_prune = tw;
+    order = tn;
+}
+
+struct PtBest {
+    float hz;      // distancesq of the best hit
+    float dist;    // sqrtf(hz)
+    int i;         // position in the DFS triangle list (tie-break)
+    int idx;       // triangle index
+    v3 hit;
+};
+
+// Kuchkuda triangle tests of one leaf (CUDAPathTracer.cu:258-345).
+__device__ __forceinline__ void pt_leaf(const KTri* __restrict__ ktris,
+                                        const int32_t* __restrict__ tri_list, uint32_t u0,
+                                        uint32_t u1, const PtRay& r, int avoid, PtBest& b,
+                                        Counters& cnt) {
+    const uint32_t n = u0 & 0x7FFFFFFFu;
+    cnt.tri_tests += n;
+    for (uint32_t i = u1; i < u1 + n; ++i) {
+        const int idx = tri_list[i];
+        if (avoid == idx) continue;
+        const float4* T = reinterpret_cast<const float4*>(ktris + idx);
+        const float4 q0 = T[0], q1 = T[1], q2 = T[2], q3 = T[3];
+        const v3 nn{q0.x, q0.y, q0.z};
+        const float k = dot(nn, r.d);
+        if (k == 0.0f) continue;
+        const float sd = fdiv(q0.w - dot(nn, r.o), k);
+        if (sd <= 0.0f) continue;
+        if (sd <= 1e-3f) continue;  // NUDGE_FACTOR
+        const v3 hit = add(scale(r.d, sd), r.o);
+        if (dot(v3{q1.x, q1.y, q1.z}, hit) - q1.w < 0.0f) continue;
+        if (dot(v3{q2.x, q2.y, q2.z}, hit) - q2.w < 0.0f) continue;
+        if (dot(v3{q3.x, q3.y, q3.z}, hit) - q3.w < 0.0f) continue;
+        const v3 df = sub(r.o, hit);
+        const float hz = df.x * df.x + df.y * df.y + df.z * df.z;  // distancesq
+        if (hz < b.hz || (hz == b.hz && (int)i < b.i)) {
+            b.hz = hz;
+            b.dist = fsqrt(hz);
+            b.i = (int)i;
+            b.idx = idx;
+            b.hit = hit;
+        }
+    }
+}
+
+// BVH_IntersectTriangles (CUDAPathTracer.cu:192-352) as an ordered traversal.
+// The result is the minimum over (distance^2, DFS list position) of the
+// triangles in the leaves the reference reaches: every inner node gets the
+// reference's exact box decision, leaves are never box-tested, and a subtree
+// is skipped only when every point of its eps-widened box lies beyond the
+// best hit. Children are tested at their parent and the nearer is descended
+// first, which changes the order but not the set of candidates that can win.
+__device__ __forceinline__ void pt_traverse(const KTri* __restrict__ ktris,
+                                            const CFNode* __restrict__ nodes,
+                                            const int32_t* __restrict__ tri_list,
+                                            uint32_t* stack, const PtRay& r, int avoid,
+                                            float len_d, float eps, PtBest& b, Counters& cnt) {
+    auto pruned = [&](float tw) { return tw > 0.0f && tw * len_d > b.dist * 1.0001f + eps; };
+    CFNode cur = nodes[0];
+    ++cnt.node_visits;
+    bool has_cur = true;
+    if (!(cur.u0 & 0x80000000u)) {
+        float tw, od;
+        has_cur = pt_box_decide(cur, r, tw, od);
+    }
+    int sp = 0;
+    for (;;) {
+        if (!has_cur) {
+            if (sp == 0) break;
+            const uint32_t ni = stack[(--sp) * 64];
+            cur = nodes[ni];
+            ++cnt.node_visits;
+            float tw, od;
+            pt_box_bounds(cur, r, tw, od);
+            if (pruned(tw)) continue;  // the best hit improved since the push
+            has_cur = true;
+        }
+        if (cur.u0 & 0x80000000u) {
+            pt_leaf(ktris, tri_list, cur.u0, cur.u1, r, avoid, b, cnt);
+            has_cur = false;
+            continue;
+        }
+        const uint32_t i0 = cur.u0, i1 = cur.u1;
+        const CFNode c0 = nodes[i0], c1 = nodes[i1];
+        cnt.node_visits += 2;
+        float w0, o0, w1, o1;
+        bool h0, h1;
+        if (c0.u0 & 0x80000000u) {
+            pt_box_bounds(c0, r, w0, o0);
+            h0 = true;
+        } else {
+            h0 = pt_box_decide(c0, r, w0, o0);
+        }
+        if (c1.u0 & 0x80000000u) {
+            pt_box_bounds(c1, r, w1, o1);
+            h1 = true;
+        } else {
+            h1 = pt_box_decide(c1, r, w1, o1);
+        }
+        h0 = h0 && !pruned(w0);
+        h1 = h1 && !pruned(w1);
+        if (h0 && h1) {
+            if (sp + 1 > kStackDepth) {
+                cnt.overflow = 1;
+                break;
+            }
+            const bool first0 = o0 <= o1;
+            stack[(sp++) * 64] = first0 ? i1 : i0;
+            cur = first0 ? c0 : c1;
+        } else if (h0) {
+            cur = c0;
+        } else if (h1) {
+            cur = c1;
+        } else {
+            has_cur = false;
+        }
+    }
+}
+
 }  // namespace
 
 template <bool kDummy>
@@ -802,60 +974,25 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
         // (distance^2, position in the DFS triangle list): the reference's
         // first-in-DFS-order tie rule, so subtrees can be pruned once their
         // entry distance exceeds the best hit without changing the result.
-        float best = 3.40282347e+38f;
-        int best_i = -1, best_idx = -1;
-        v3 best_hit{0.0f, 0.0f, 0.0f};
-        uint32_t best_mat = kDiffuse;
+        PtBest best{3.40282347e+38f, 3.40282347e+38f, 0x7FFFFFFF, -1, v3{0.0f, 0.0f, 0.0f}};
         if (has_mesh) {
-            const float dd = dot(d, d);
-            stack[0] = 0u;
-            int sp = 1;
-            while (sp > 0) {
-                const uint32_t ni = stack[(--sp) * 64];
-                const CFNode nd = nodes[ni];
-                ++cnt.node_visits;
-                if (!(nd.u0 & 0x80000000u)) {
-                    float tn;
-                    if (pt_box(nd, o, d, tn)) {
-                        if (tn > 0.0f && (tn * tn) * dd > best * 1.0001f) continue;  // cannot win
-                        if (sp + 2 > kStackDepth) {
-                            cnt.overflow = 1;
-                            break;
-                        }
-                        stack[(sp++) * 64] = nd.u1;  // right
-                        stack[(sp++) * 64] = nd.u0;  // left (popped first)
-                    }
-                } else {
-                    const uint32_t n = nd.u0 & 0x7FFFFFFFu;
-                    cnt.tri_tests += n;
-                    for (uint32_t i = nd.u1; i < nd.u1 + n; ++i) {
-                        const int idx = tri_list[i];
-                        if (avoid == idx) continue;
-                        const KTri T = ktris[idx];
-                        const v3 nn{T.n[0], T.n[1], T.n[2]};
-                        const float k = dot(nn, d);
-                        if (k == 0.0f) continue;
-                        const float sd = fdiv(T.d - dot(nn, o), k);
-                        if (sd <= 0.0f) continue;
-                        if (sd <= 1e-3f) continue;  // NUDGE_FACTOR
-                        const v3 hit = add(scale(d, sd), o);
-                        if (dot(v3{T.e1[0], T.e1[1], T.e1[2]}, hit) - T.d1 < 0.0f) continue;
-                        if (dot(v3{T.e2[0], T.e2[1], T.e2[2]}, hit) - T.d2 < 0.0f) continue;
-                        if (dot(v3{T.e3[0], T.e3[1], T.e3[2]}, hit) - T.d3 < 0.0f) continue;
-                        const v3 df = sub(o, hit);
-                        const float hz = df.x * df.x + df.y * df.y + df.z * df.z;  // distancesq
-                        if (hz < best || (hz == best && (int)i < best_i)) {
-                            best = hz;
-                            best_i = (int)i;
-                            best_idx = idx;
-                            best_hit = hit;
-                            best_mat = (uint32_t)T.material;
-                        }
-                    }
-                }
-            }
+            PtRay r;
+            r.o = o;
+            r.d = d;
+            const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+            r.exact = (ax > 0.0f && ax < 1e-30f) || (ay > 0.0f && ay < 1e-30f) || (az > 0.0f && az < 1e-30f);
+            r.inv = v3{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
+            // eps: a bound on how far an accepted Kuchkuda hit point can sit
+            // outside its triangle's box (rounding at the scale of the
+            // coordinates involved), with a 10x margin.
+            const float eps = 1e-5f * (1.0f + fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) + L.pt_scale);
+            r.pad_t = v3{eps * fabsf(r.inv.x), eps * fabsf(r.inv.y), eps * fabsf(r.inv.z)};
+            pt_traverse(ktris, nodes, tri_list, stack, r, avoid, fsqrt(dot(d, d)), eps, best, cnt);
         }
-        const float hitdistance = best_idx >= 0 ? fsqrt(best) : 1e20f;
+        const int best_idx = best.idx;
+        const v3 best_hit = best.hit;
+        const uint32_t best_mat = best_idx >= 0 ? (uint32_t)ktris[best_idx].material : kDiffuse;
+        const float hitdistance = best_idx >= 0 ? best.dist : 1e20f;
 
         // the six spheres, scanned i = 5 .. 0 (CUDAPathTracer.cu:400-404)
         float scene_t = 1e20f;
@@ -905,7 +1042,9 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
                 const v3 uu = normalize(cross(a, w));
                 const v3 vv = cross(w, uu);
                 const float r2s = fsqrt(r2);
-                const v3 dir = add(add(scale(scale(uu, pt_cosf(phi)), r2s), scale(scale(vv, pt_sinf(phi)), r2s)),
+                float sp, cp;
+                pt_sincosf(phi, &sp, &cp);
+                const v3 dir = add(add(scale(scale(uu, cp), r2s), scale(scale(vv, sp), r2s)),
                                    scale(w, fsqrt(1.0f - r2)));
                 return normalize(dir);
             };
@@ -926,7 +1065,9 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
                 const v3 a = ((double)fabsf(w.x) > 0.1) ? v3{0.0f, 1.0f, 0.0f} : v3{1.0f, 0.0f, 0.0f};
                 const v3 uu = normalize(cross(a, w));
                 const v3 vv = cross(w, uu);
-                next = normalize(add(add(scale(scale(uu, pt_cosf(phi)), sin_t), scale(scale(vv, pt_sinf(phi)), sin_t)),
+                float sp, cp;
+                pt_sincosf(phi, &sp, &cp);
+                next = normalize(add(add(scale(scale(uu, cp), sin_t), scale(scale(vv, sp), sin_t)),
                                      scale(w, cos_t)));
                 point = add(hitp, scale(w, 0.01f));
                 mask = mul(mask, f);

@@ -245,6 +245,14 @@ RT_HD float pt_cosf(float x) {
 
 // x^y for x >= 0 (powf at CUDAPathTracer.cu:486): exp(y * ln x) with an atanh
 // series for ln on [sqrt(1/2), sqrt(2)) and a Taylor exp after reduction by ln 2.
+// sinf and cosf of one argument from one reduction (same values as pt_sinf / pt_cosf).
+RT_HD void pt_sincosf(float x, float* sf, float* cf) {
+    double s, c;
+    sincos_d((double)x, &s, &c);
+    *sf = (float)s;
+    *cf = (float)c;
+}
+
 RT_HD float pt_powf(float xf, float yf) {
     if (!(xf > 0.0f)) return xf == 0.0f ? (yf > 0.0f ? 0.0f : 1.0f) : __builtin_nanf("");
     const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;

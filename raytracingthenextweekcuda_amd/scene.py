@@ -97,6 +97,19 @@ def bunny_cornell_box(r: Renderer, width: int, height: int, commit: bool = True)
                            commit=commit)
 
 
+def materialball(r: Renderer, width: int, height: int, commit: bool = True) -> Camera:
+    """The reference's committed renderKernel configuration: pathTrace
+    (main.cu:187) over materialball.ply as COAT at offset (0.1, 0, -1)
+    (prepareCUDAscene, main.cu:430-432), seen through the camera of the
+    cornellbox2.yaml scene initialize() loads (main.cu:629-638). Render with
+    integrator="pathTrace", max_depth=5 (CUDAPathTracer.cu:366)."""
+    cam = load_yaml_scene(r, os.path.join(SCENES_DIR, "cornellbox2.yaml"), width, height,
+                          commit=commit)
+    r.load_object(os.path.join(MODELS_DIR, "materialball", "materialball.ply"), "COAT")
+    r.process_triangle_data((0.1, 0.0, -1.0))
+    return cam
+
+
 def _material(r: Renderer, index: int, m: dict):
     kind = m["type"]
     if kind == "lambertian":

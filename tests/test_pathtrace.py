@@ -165,3 +165,21 @@ def test_gpu_pathtrace_requires_processed_scene():
     with pytest.raises(rtmi.RTError, match="RT_ERR_INVALID"):
         r.render(8, 8, 1, 0, integrator="pathTrace")
     r.close()
+
+
+@pytest.mark.gpu
+def test_gpu_materialball_committed_configuration():
+    # rtmi.materialball: cornellbox2.yaml camera + materialball COAT at (0.1, 0, -1)
+    import raytracingthenextweekcuda_amd as rtmi
+    from oracle import oracle as orc
+
+    w, h = 48, 40
+    cam = orc.yaml_scene(os.path.join(S.SCENES, "cornellbox2.yaml"), S.MODELS, w, h)
+    pt, _ = S.build_pathtrace_oracle("materialball")
+    want, _ = pt.render(cam, w, h, 4, 5, threads=8)
+    r = _product(0)
+    rtmi.materialball(r, w, h)
+    got = r.render(w, h, 4, 5, integrator="pathTrace")
+    r.close()
+    _assert_parity(got, want)
+    assert np.array_equal(got, want)  # bit-identical in practice (same IEEE op order)
