@@ -36,6 +36,7 @@ SCENES = {
     "cornellbox1": ("cornell_box1", 512, 512, 128, 8, "CornellBox1 (6 planes + 2 cube_small.obj meshes, 24 triangles)"),
     "spheres": ("random_spheres", 1280, 720, 256, 10, "RTNW final scene (488 spheres, 388 moving; object BVH)"),
     "bunny": ("bunny_cornell_box", 1024, 1024, 512, 8, "bun_zipper.ply (69,451 triangles, SAH BVH) in CornellBox1 walls"),
+    "media": ("cornell_box_media", 2048, 2048, 1024, 16, "CornellBox1 walls + 2 constant-medium boxes + glass sphere (media: build extension)"),
     # the reference's committed renderKernel configuration (pathTrace, main.cu:187;
     # samplesPerPixel 32, 5 bounces); not a BASELINE config, reported separately
     "materialball": ("materialball", 512, 512, 32, 5, "materialball.ply (46,816 triangles, COAT) + 6 spheres, pathTrace integrator"),
@@ -49,7 +50,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scene", default="cornellbox1", choices=sorted(SCENES),
-                    help="BASELINE config: cornellbox1 (2), spheres (3), bunny (4); the metric line is config 2")
+                    help="BASELINE config: cornellbox1 (2), spheres (3), bunny (4), media (5); materialball = "
+                         "the reference's committed pathTrace setup; the metric line is config 2")
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
@@ -68,7 +70,7 @@ def parse():
     # threads): the restatement scans meshes brute force like the reference's
     # TriangleMesh::hit, so the bunny sample is a 1/16-scale frame at 1 spp.
     a.cpu_div, cpu_spp = {"cornellbox1": (1, 32), "spheres": (2, 4), "bunny": (16, 1),
-                          "materialball": (1, 32)}[a.scene]
+                          "materialball": (1, 32), "media": (8, 64)}[a.scene]
     a.cpu_spp = a.cpu_spp or cpu_spp
     return a
 
@@ -108,7 +110,8 @@ def cpu_baseline(args, threads: int):
     elif args.scene == "spheres":
         sc = orc.json_scene(os.path.join(scenes, "random_spheres.json"), w, h)
     else:
-        name = "cornellbox1.yaml" if args.scene == "cornellbox1" else "bunny_cornellbox.yaml"
+        name = {"cornellbox1": "cornellbox1.yaml", "bunny": "bunny_cornellbox.yaml",
+                "media": "cornellbox_media.yaml"}[args.scene]
         sc = orc.yaml_scene(os.path.join(scenes, name), os.path.join(REPO, "assets", "models"), w, h)
     if sc is not None:
         sc.render(16, 16, 1, args.depth, threads=threads)  # warm-up

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define RTMI_ABI_VERSION 2
+#define RTMI_ABI_VERSION 3
 
 typedef int32_t rt_status;
 enum {
@@ -36,8 +36,9 @@ enum {
     RT_ERR_OVERFLOW = 7  /* BVH traversal stack overflow flagged by the kernel */
 };
 
-/* Material kinds (Material.h:8-13 MaterialType). */
-enum { RT_LAMBERTIAN = 0, RT_METAL = 1, RT_DIELECTRIC = 2, RT_EMISSION = 3 };
+/* Material kinds (Material.h:8-13 MaterialType) + the isotropic phase function
+ * of participating media (build extension, see rt_constant_medium). */
+enum { RT_LAMBERTIAN = 0, RT_METAL = 1, RT_DIELECTRIC = 2, RT_EMISSION = 3, RT_ISOTROPIC = 4 };
 /* Plane orientation (Plane.h:5-9 PlaneOrientation). */
 enum { RT_PLANE_XY = 0, RT_PLANE_YZ = 1, RT_PLANE_XZ = 2 };
 /* Integrator run by renderKernel: rayColor (main.cu:60-113, the Hitable scene)
@@ -101,6 +102,10 @@ rt_status rt_material_lambertian(rt_ctx* ctx, int32_t index, const float albedo[
 rt_status rt_material_metal(rt_ctx* ctx, int32_t index, const float albedo[3], float fuzz);
 rt_status rt_material_dielectric(rt_ctx* ctx, int32_t index, float index_of_refraction);
 rt_status rt_material_emission(rt_ctx* ctx, int32_t index, const float albedo[3], float intensity);
+/* Isotropic phase function (build extension for BASELINE config 5; the reference
+ * has no media): scatter = Ray(p, randomInUnitSphere(), time), attenuation =
+ * albedo (Ray Tracing: The Next Week's `isotropic`). */
+rt_status rt_material_isotropic(rt_ctx* ctx, int32_t index, const float albedo[3]);
 /* 1 if material slot `index` has been created (the `materials[id] == nullptr`
  * guards of main.cu:714,723,733,743), else 0. */
 int32_t rt_material_defined(const rt_ctx* ctx, int32_t index);
@@ -117,6 +122,14 @@ rt_status rt_plane(rt_ctx* ctx, int32_t index, const float position[3], const fl
                    int32_t two_side);
 rt_status rt_cube(rt_ctx* ctx, int32_t index, const float center[3], const float extend[3],
                   int32_t material);
+/* Constant-density medium bounded by an axis-aligned cube (build extension for
+ * BASELINE config 5; the reference has no media). Boundary = the six two-sided
+ * faces of rt_cube. Per segment: entry t1 (any t) and exit t2 (> t1 + 1e-4) of
+ * the boundary; t1 clamps to 0.001; free flight hd = -ln(u) / density with u
+ * from the medium's own counter-based draw (seed, pixel, sample, bounce, slot);
+ * hit at t1 + hd/|d| when hd <= (t2 - t1)|d|; closest rule strict like planes. */
+rt_status rt_constant_medium(rt_ctx* ctx, int32_t index, const float center[3],
+                             const float extend[3], float density, int32_t material);
 /* Triangle mesh from world-space vertices, 9 floats per triangle
  * (createTriangleMeshData + createMesh, main.cu:384-401, kernels.h:126-133). */
 rt_status rt_mesh(rt_ctx* ctx, int32_t index, const float* tri_vertices, int32_t n_tris,

@@ -230,6 +230,14 @@ inline void createEmissionMaterial(Material** materials, int32_t index, Vector3D
     c.markMaterial(index);
     (void)materials;
 }
+// Build extensions for participating media (rtmi.h rt_material_isotropic /
+// rt_constant_medium; the reference has no media).
+inline void createIsotropicMaterial(Material** materials, int32_t index, Vector3Df albedo) {
+    Context& c = *table_owner();
+    c.check(rt_material_isotropic(c.raw(), index, albedo.data()));
+    c.markMaterial(index);
+    (void)materials;
+}
 inline void createSphere(Hitable** spheres, int32_t index, Vector3Df center, float radius, Material* material,
                          bool bShading = true) {
     Context& c = *table_owner();
@@ -260,6 +268,14 @@ inline void createCube(Hitable** cubes, int32_t index, const Vector3Df& center, 
     c.check(rt_cube(c.raw(), index, center.data(), extend.data(), detail::mat_index(material)));
     c.markObject(index);
     (void)cubes;
+}
+inline void createConstantMedium(Hitable** objects, int32_t index, const Vector3Df& center,
+                                 const Vector3Df& extend, float density, Material* material) {
+    Context& c = *table_owner();
+    c.check(rt_constant_medium(c.raw(), index, center.data(), extend.data(), density,
+                               detail::mat_index(material)));
+    c.markObject(index);
+    (void)objects;
 }
 // createTriangleMeshData + createMesh (main.cu:384-401, kernels.h:126-133) from
 // world-space triangle vertices (loadModel(...).vertices, 3 per triangle).

@@ -45,6 +45,7 @@ def lib():
         L.orc_moving_sphere.argtypes = [vp, C.c_int, fp, fp, C.c_float, C.c_float, C.c_float, C.c_int]
         L.orc_plane.argtypes = [vp, C.c_int, fp, fp, fp, C.c_int, C.c_int, C.c_int]
         L.orc_cube.argtypes = [vp, C.c_int, fp, fp, C.c_int]
+        L.orc_constant_medium.argtypes = [vp, C.c_int, fp, fp, C.c_float, C.c_int]
         L.orc_mesh.argtypes = [vp, C.c_int, fp, C.c_int, C.c_int]
         L.orc_mesh_obj.argtypes = [vp, C.c_int, C.c_char_p, fp, fp, fp, C.c_int]
         L.orc_load_obj.argtypes = [C.c_char_p, fp, fp, fp, C.POINTER(fp)]
@@ -150,6 +151,9 @@ class OracleScene:
 
     def cube(self, idx, c, ext, mat):
         assert self.L.orc_cube(self.h, idx, f3(c), f3(ext), mat) == 0
+
+    def constant_medium(self, idx, c, ext, density, mat):
+        assert self.L.orc_constant_medium(self.h, idx, f3(c), f3(ext), density, mat) == 0
 
     def mesh(self, idx, verts, mat):
         v = np.ascontiguousarray(verts, np.float32).reshape(-1)
@@ -282,6 +286,8 @@ def yaml_scene(path: str, models_dir: str, width: int, height: int) -> OracleSce
                 sc.material(mid, 1, mat["albedo"], float(mat["fuzz"]))
             elif mtype == 3:
                 sc.material(mid, 3, mat["albedo"], float(mat["intensity"]))
+            elif mtype == 4:
+                sc.material(mid, 4, mat["albedo"], 0.0)
         ptype = int(next(iter(obj.values())))  # first key of the object map (main.cu:706, 749)
         if ptype == 0:
             sc.sphere(i, obj["center"], float(obj["radius"]), mid)
@@ -294,6 +300,12 @@ def yaml_scene(path: str, models_dir: str, width: int, height: int) -> OracleSce
                 sc.mesh(i, load_ply(model, obj.get("offset", (0, 0, 0)), float(obj.get("maxCoord", 1.0))), 3)
             else:
                 sc.mesh_obj(i, model, obj["scale"], obj["rotate"], obj["offset"], 3)
+        elif ptype == 3:  # build extension: cube
+            sc.cube(i, obj["center"], obj["extend"], mid)
+        elif ptype == 4:  # build extension: constant medium
+            sc.constant_medium(i, obj["center"], obj["extend"], float(obj["density"]), mid)
+        else:
+            raise ValueError(f"unknown primitive type {ptype}")
     return sc
 
 

@@ -214,7 +214,7 @@ static void set_face_normal(HitResult* h, const Ray* r, V3 outward) {
 }
 
 /* ---------------- Scene objects ---------------- */
-enum { O_SPHERE = 0, O_MOVING = 1, O_PLANE = 2, O_MESH = 3, O_CUBE = 4 };
+enum { O_SPHERE = 0, O_MOVING = 1, O_PLANE = 2, O_MESH = 3, O_CUBE = 4, O_MEDIUM = 5 };
 
 typedef struct {
     int defined;
@@ -238,7 +238,12 @@ typedef struct Object {
     int tri_count;
     float* tri_data;   /* 12 floats per tri: (v0, n.x), (E1, n.y), (E2, n.z) as main.cu:341-343 */
     V3 bounds[2];
+    /* constant medium (faces = its cube boundary) */
+    float neg_inv_density;
 } Object;
+
+/* Key of a segment's medium free-flight draws. */
+typedef struct { uint32_t seed, pixel, sample, bounce; } MediumKey;
 
 typedef struct {
     Material* mats;
@@ -359,40 +364,102 @@ static int mesh_hit(const Object* o, const Ray* ray, float tmin, float tmax, Hit
     return any;
 }
 
+/* ln x of a positive float in double (exact frexp split, atanh series, ln 2 in
+ * two parts): the build's own log, shared by pathTrace's powf and the media. */
+static double ln_pos_d(float xf) {
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    int e;
+    double m = frexp((double)xf, &e);
+    if (m < 0.70710678118654752440) { m = m * 2.0; e = e - 1; }
+    const double t = (m - 1.0) / (m + 1.0), t2 = t * t;
+    double p = 1.0 / 23.0;
+    p = p * t2 + 1.0 / 21.0;
+    p = p * t2 + 1.0 / 19.0;
+    p = p * t2 + 1.0 / 17.0;
+    p = p * t2 + 1.0 / 15.0;
+    p = p * t2 + 1.0 / 13.0;
+    p = p * t2 + 1.0 / 11.0;
+    p = p * t2 + 1.0 / 9.0;
+    p = p * t2 + 1.0 / 7.0;
+    p = p * t2 + 1.0 / 5.0;
+    p = p * t2 + 1.0 / 3.0;
+    p = p * t2 + 1.0;
+    const double ln_m = 2.0 * t * p;
+    const double de = (double)e;
+    return (de * ln2_hi + ln_m) + de * ln2_lo;
+}
+
+/* One uniform per (pixel, sample, bounce, medium slot) from its own Philox
+ * counter: independent of the order in which hit() meets the media. */
+static float medium_u01(const MediumKey* mk, uint32_t slot) {
+    uint32_t ctr[4] = {mk->sample, mk->bounce + 1u, slot, 0x6D656469u}, key[2] = {mk->seed, mk->pixel}, out[4];
+    philox(ctr, key, out);
+    const float inv = 2.3283064e-10f;
+    return (float)out[0] * inv + (inv / 2.0f);
+}
+
+/* Cube::hit over the six faces (Cube.cu:10-23). */
+static int cube_hit(const Object* o, const Ray* ray, float tmin, float tmax, HitResult* hr) {
+    HitResult tmp;
+    int any = 0;
+    float closest = tmax;
+    for (int f = 0; f < 6; ++f) {
+        if (plane_hit(&o->faces[f], ray, tmin, closest, &tmp)) {
+            any = 1;
+            closest = tmp.t;
+            *hr = tmp;
+        }
+    }
+    return any;
+}
+
+/* ConstantMedium::hit ("Ray Tracing: The Next Week") with the cube boundary and
+ * the build's order-independent draw (rtmi.h rt_constant_medium). */
+static int medium_hit(const Object* o, const Ray* ray, float tmin, float tmax, HitResult* hr,
+                      const MediumKey* mk, int slot) {
+    HitResult r1, r2;
+    if (!cube_hit(o, ray, -INFINITY, INFINITY, &r1)) return 0;
+    if (!cube_hit(o, ray, r1.t + 0.0001f, INFINITY, &r2)) return 0;
+    float t1 = r1.t < tmin ? tmin : r1.t;
+    float t2 = r2.t;
+    if (t1 >= t2) return 0;
+    if (t1 < 0) t1 = 0;
+    float len = vlen(ray->direction);
+    float inside = (t2 - t1) * len;
+    float hd = o->neg_inv_density * (float)ln_pos_d(medium_u01(mk, (uint32_t)slot));
+    if (hd > inside) return 0;
+    float t = t1 + hd / len;
+    if (!(t < tmax)) return 0;  /* closest rule: strict, like Plane::hit */
+    hr->t = t;
+    hr->normal = v3(1.0f, 0.0f, 0.0f);
+    hr->front_face = 1;
+    hr->material = o->material;
+    return 1;
+}
+
 static int object_hit(const Object* o, const Ray* ray, float tmin, float tmax, HitResult* hr,
-                      uint64_t* tri_tests) {
+                      uint64_t* tri_tests, const MediumKey* mk, int slot) {
     switch (o->type) {
     case O_SPHERE: return sphere_hit(o, o->center, ray, tmin, tmax, hr);
     case O_MOVING: return sphere_hit(o, moving_center(o, ray->time), ray, tmin, tmax, hr);
     case O_PLANE: return plane_hit(&o->plane, ray, tmin, tmax, hr);
     case O_MESH: return mesh_hit(o, ray, tmin, tmax, hr, tri_tests);
-    case O_CUBE: { /* Cube::hit (Cube.cu:10-23) */
-        HitResult tmp;
-        int any = 0;
-        float closest = tmax;
-        for (int f = 0; f < 6; ++f) {
-            if (plane_hit(&o->faces[f], ray, tmin, closest, &tmp)) {
-                any = 1;
-                closest = tmp.t;
-                *hr = tmp;
-            }
-        }
-        return any;
-    }
+    case O_CUBE: return cube_hit(o, ray, tmin, tmax, hr);
+    case O_MEDIUM: return medium_hit(o, ray, tmin, tmax, hr, mk, slot);
     }
     return 0;
 }
 
 /* hit (main.cu:43-57) */
 static int scene_hit(const Scene* s, const Ray* ray, float tmin, float tmax, HitResult* out,
-                     uint64_t* tri_tests) {
+                     uint64_t* tri_tests, const MediumKey* mk) {
     HitResult tmp;
     memset(&tmp, 0, sizeof(tmp));
     int any = 0;
     float closest = tmax;
     for (int i = 0; i < s->n_objs; ++i) {
         const Object* o = &s->objs[i];
-        if (o->defined && object_hit(o, ray, tmin, closest, &tmp, tri_tests)) {
+        if (o->defined && object_hit(o, ray, tmin, closest, &tmp, tri_tests, mk, i)) {
             any = 1;
             closest = tmp.t;
             *out = tmp;
@@ -441,6 +508,10 @@ static int scatter(const Material* m, const Ray* in, const HitResult* h, V3* att
         *sc = make_ray(ray_at(in, h->t), vnorm(dir), in->time);
         return 1;
     }
+    case 4: /* isotropic: Ray(p, randomInUnitSphere(), time), attenuation = albedo */
+        *sc = make_ray(ray_at(in, h->t), u_random_in_unit_sphere(rs), in->time);
+        *att = m->albedo;
+        return 1;
     default: /* Emission (Material.h:120-123) */
         *att = vmul(m->albedo, m->param);
         return 0;
@@ -448,7 +519,8 @@ static int scatter(const Material* m, const Ray* in, const HitResult* h, V3* att
 }
 
 /* rayColor (main.cu:63-94) */
-static V3 ray_color(const Scene* s, Ray ray, int bounces, RandState* rs, uint64_t* segs, uint64_t* tri_tests) {
+static V3 ray_color(const Scene* s, Ray ray, int bounces, RandState* rs, uint64_t* segs, uint64_t* tri_tests,
+                     uint32_t seed, uint32_t pixel, uint32_t sample) {
     V3 cur = v3(1.0f, 1.0f, 1.0f);
     for (int i = 0; i < bounces; ++i) {
         HitResult h;
@@ -456,7 +528,8 @@ static V3 ray_color(const Scene* s, Ray ray, int bounces, RandState* rs, uint64_
         h.t = -INFINITY;
         h.front_face = 1;
         ++*segs;
-        if (scene_hit(s, &ray, ORC_EPS, INFINITY, &h, tri_tests)) {
+        MediumKey mk = {seed, pixel, sample, (uint32_t)i};
+        if (scene_hit(s, &ray, ORC_EPS, INFINITY, &h, tri_tests, &mk)) {
             V3 att;
             Ray sc;
             if (scatter(&s->mats[h.material], &ray, &h, &att, &sc, rs)) {
@@ -522,7 +595,7 @@ static Object* obj_at(Scene* s, int idx) {
 /* type: 0 Lambertian(param=absorb), 1 Metal(fuzz), 2 Dieletric(ior), 3 Emission(intensity) */
 int orc_material(Scene* s, int idx, int type, const float albedo[3], float param) {
     Material* m = mat_at(s, idx);
-    if (!m || type < 0 || type > 3) return 1;
+    if (!m || type < 0 || type > 4) return 1;
     m->defined = 1;
     m->type = type;
     m->albedo = albedo ? v3(albedo[0], albedo[1], albedo[2]) : v3(1.0f, 1.0f, 1.0f);
@@ -565,9 +638,8 @@ int orc_plane(Scene* s, int idx, const float p[3], const float n[3], const float
     return 0;
 }
 
-int orc_cube(Scene* s, int idx, const float c[3], const float e[3], int mat) {
-    Object* o = obj_at(s, idx);
-    if (!o) return 1;
+/* createCube (kernels.h:139-154): six two-sided planes. */
+static void set_cube(Object* o, const float c[3], const float e[3], int mat) {
     V3 C = v3(c[0], c[1], c[2]), E = v3(e[0], e[1], e[2]);
     o->defined = 1; o->type = O_CUBE; o->material = mat; o->center = C;
     o->faces[0] = make_plane(v3(C.x - E.x, C.y, C.z), v3(-1, 0, 0), E, mat, 1, 1);
@@ -576,10 +648,25 @@ int orc_cube(Scene* s, int idx, const float c[3], const float e[3], int mat) {
     o->faces[3] = make_plane(v3(C.x, C.y - E.y, C.z), v3(0, -1, 0), E, mat, 2, 1);
     o->faces[4] = make_plane(v3(C.x, C.y, C.z + E.z), v3(0, 0, 1), E, mat, 0, 1);
     o->faces[5] = make_plane(v3(C.x, C.y, C.z - E.z), v3(0, 0, -1), E, mat, 0, 1);
+}
+
+int orc_cube(Scene* s, int idx, const float c[3], const float e[3], int mat) {
+    Object* o = obj_at(s, idx);
+    if (!o) return 1;
+    set_cube(o, c, e, mat);
     return 0;
 }
 
-/* createTriangleMeshData / prepareTriangleData / computeMeshAABB (main.cu:261-350, 384-401) */
+/* rt_constant_medium: cube boundary (faces as orc_cube) + density. */
+int orc_constant_medium(Scene* s, int idx, const float c[3], const float e[3], float density, int mat) {
+    Object* o = obj_at(s, idx);
+    if (!o || !(density > 0.0f)) return 1;
+    set_cube(o, c, e, mat);
+    o->type = O_MEDIUM;
+    o->neg_inv_density = -1.0f / density;
+    return 0;
+}
+
 int orc_mesh(Scene* s, int idx, const float* verts, int n_tris, int mat) {
     if (n_tris <= 0) return 0; /* empty meshes are not created (main.cu:777) */
     Object* o = obj_at(s, idx);
@@ -907,7 +994,8 @@ int orc_render(const Scene* s, int width, int height, int spp, int bounces, uint
                     float dx = ((float)x + rx) / (float)(width - 1);
                     float dy = ((float)y + ry) / (float)(height - 1);
                     Ray ray = camera_get_ray(s, dx, dy, &rs);
-                    part = vadd(part, ray_color(s, ray, bounces, &rs, &segs, &tris));
+                    part = vadd(part, ray_color(s, ray, bounces, &rs, &segs, &tris, seed, pixel,
+                                                sample_offset + (uint32_t)i));
                 }
                 color = c == 0 ? part : vadd(color, part);
             }
@@ -936,7 +1024,8 @@ int orc_trace(const Scene* s, const float o[3], const float d[3], float time, fl
     HitResult h;
     memset(&h, 0, sizeof h);
     uint64_t tt = 0;
-    int hit = scene_hit(s, &r, ORC_EPS, INFINITY, &h, &tt);
+    MediumKey mk = {0u, 0u, 0u, 0u};
+    int hit = scene_hit(s, &r, ORC_EPS, INFINITY, &h, &tt, &mk);
     if (hit) {
         *t = h.t; normal[0] = h.normal.x; normal[1] = h.normal.y; normal[2] = h.normal.z;
         *front = h.front_face; *material = h.material;
@@ -1038,25 +1127,7 @@ static float pt_cosf(float x) { double s, c; pt_sincos((double)x, &s, &c); retur
 static float pt_powf(float xf, float yf) {
     if (!(xf > 0.0f)) return xf == 0.0f ? (yf > 0.0f ? 0.0f : 1.0f) : NAN;
     const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
-    int e;
-    double m = frexp((double)xf, &e);
-    if (m < 0.70710678118654752440) { m = m * 2.0; e = e - 1; }
-    const double t = (m - 1.0) / (m + 1.0), t2 = t * t;
-    double p = 1.0 / 23.0;
-    p = p * t2 + 1.0 / 21.0;
-    p = p * t2 + 1.0 / 19.0;
-    p = p * t2 + 1.0 / 17.0;
-    p = p * t2 + 1.0 / 15.0;
-    p = p * t2 + 1.0 / 13.0;
-    p = p * t2 + 1.0 / 11.0;
-    p = p * t2 + 1.0 / 9.0;
-    p = p * t2 + 1.0 / 7.0;
-    p = p * t2 + 1.0 / 5.0;
-    p = p * t2 + 1.0 / 3.0;
-    p = p * t2 + 1.0;
-    const double ln_m = 2.0 * t * p;
-    const double de = (double)e;
-    const double lnx = (de * ln2_hi + ln_m) + de * ln2_lo;
+    const double lnx = ln_pos_d(xf);
     const double z = (double)yf * lnx;
     const double n = floor(z * 1.44269504088896338700 + 0.5);
     const double r = (z - n * ln2_hi) - n * ln2_lo;

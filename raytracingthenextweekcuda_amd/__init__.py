@@ -12,5 +12,5 @@ from .renderer import (  # noqa: F401
     createMovingSphere, createPlane, createSphere, gamma_u8, owned_row_ids, owned_rows,
 )
 from .scene import (  # noqa: F401
-    bunny_cornell_box, cornell_box1, load_json_scene, load_yaml_scene, materialball, random_spheres,
+    bunny_cornell_box, cornell_box1, cornell_box_media, load_json_scene, load_yaml_scene, materialball, random_spheres,
 )

@@ -23,12 +23,13 @@ STATUS_NAMES = {
 }
 
 # Every symbol include/rtmi.h declares (checked by tests/test_abi.py).
-ABI_VERSION = 2  # include/rtmi.h RTMI_ABI_VERSION
+ABI_VERSION = 3  # include/rtmi.h RTMI_ABI_VERSION
 
 EXPORTS = [
     "rt_abi_version", "rt_create", "rt_destroy", "rt_last_error", "rt_clear_scene",
     "rt_material_lambertian", "rt_material_metal", "rt_material_dielectric",
-    "rt_material_emission", "rt_material_defined", "rt_sphere", "rt_moving_sphere", "rt_plane",
+    "rt_material_emission", "rt_material_isotropic", "rt_material_defined", "rt_constant_medium",
+    "rt_sphere", "rt_moving_sphere", "rt_plane",
     "rt_cube", "rt_mesh", "rt_mesh_obj", "rt_mesh_triangle_count", "rt_mesh_vertices",
     "rt_mesh_ply", "rt_ply_bvh_image", "rt_load_object", "rt_process_triangle_data",
     "rt_pathtrace_bvh_image",
@@ -99,6 +100,8 @@ def lib():
     L.rt_material_dielectric.argtypes = [vp, i32, C.c_float]
     L.rt_material_emission.argtypes = [vp, i32, fp, C.c_float]
     L.rt_material_defined.argtypes = [vp, i32]
+    L.rt_material_isotropic.argtypes = [vp, i32, fp]
+    L.rt_constant_medium.argtypes = [vp, i32, fp, fp, C.c_float, i32]
     L.rt_sphere.argtypes = [vp, i32, fp, C.c_float, i32, i32]
     L.rt_moving_sphere.argtypes = [vp, i32, fp, fp, C.c_float, C.c_float, C.c_float, i32]
     L.rt_plane.argtypes = [vp, i32, fp, fp, fp, i32, i32, i32]

@@ -222,6 +222,16 @@ rt_status rt_material_emission(rt_ctx* c, int32_t index, const float albedo[3], 
     return RT_OK;
 }
 
+rt_status rt_material_isotropic(rt_ctx* c, int32_t index, const float albedo[3]) {
+    if (!c) return RT_ERR_INVALID;
+    if (!finite3(albedo)) return fail(c, RT_ERR_INVALID, "isotropic: albedo must be 3 finite floats");
+    rt::HostMaterial* m = mat_slot(c, index);
+    if (!m) return fail(c, RT_ERR_INVALID, "material index out of range");
+    m->defined = true;
+    m->rec = rt::MatRec{RT_ISOTROPIC, albedo[0], albedo[1], albedo[2], 0.0f, 0, 0, 0};
+    return RT_OK;
+}
+
 int32_t rt_material_defined(const rt_ctx* c, int32_t index) {
     if (!c || index < 0 || (size_t)index >= c->scene.materials.size()) return 0;
     return c->scene.materials[index].defined ? 1 : 0;
@@ -280,6 +290,23 @@ rt_status rt_plane(rt_ctx* c, int32_t index, const float pos[3], const float nor
     memcpy(o->f, pos, 3 * sizeof(float));
     memcpy(o->f + 3, normal, 3 * sizeof(float));
     memcpy(o->f + 6, extend, 3 * sizeof(float));
+    return RT_OK;
+}
+
+rt_status rt_constant_medium(rt_ctx* c, int32_t index, const float center[3],
+                             const float extend[3], float density, int32_t material) {
+    if (!c) return RT_ERR_INVALID;
+    if (!finite3(center) || !finite3(extend) || !isfinite(density) || !(density > 0.0f))
+        return fail(c, RT_ERR_INVALID, "constant medium: non-finite input or density <= 0");
+    rt::HostObject* o = obj_slot(c, index);
+    if (!o) return fail(c, RT_ERR_INVALID, "object index out of range");
+    *o = rt::HostObject();
+    o->defined = true;
+    o->type = rt::kObjMedium;
+    o->material = (uint32_t)material;
+    memcpy(o->f, center, 3 * sizeof(float));
+    memcpy(o->f + 3, extend, 3 * sizeof(float));
+    o->f[6] = density;
     return RT_OK;
 }
 

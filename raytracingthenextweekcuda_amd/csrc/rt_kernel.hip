@@ -368,9 +368,72 @@ __device__ __forceinline__ void sphere_group(const ObjRec* __restrict__ objs,
 // wave active; `live` masks lanes without a path. Records are fetched one
 // object ahead (scalar loads overlap the current object's VALU work), and the
 // per-object tests are branch-free candidates merged with Hit's tie rule.
+// Key of a segment's medium free-flight draws (medium_u01).
+struct MediumKey {
+    uint32_t seed, pixel, sample, bounce;
+};
+
+// Constant medium bounded by a cube (rt_constant_medium, rtmi.h; "Ray Tracing:
+// The Next Week" ConstantMedium::hit with the boundary = the six two-sided faces
+// of createCube, kernels.h:139-154, each tested like Plane::hit). Returns the
+// scattering distance t, or NaN.
+__device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, const MediumKey& mk) {
+    const float* f = ob.f;
+    const v3 c{f[0], f[1], f[2]}, e{f[3], f[4], f[5]};
+    const v3 pos[6] = {{c.x - e.x, c.y, c.z}, {c.x + e.x, c.y, c.z}, {c.x, c.y + e.y, c.z},
+                       {c.x, c.y - e.y, c.z}, {c.x, c.y, c.z + e.z}, {c.x, c.y, c.z - e.z}};
+    const v3 nrm[6] = {{-1.0f, 0.0f, 0.0f}, {1.0f, 0.0f, 0.0f}, {0.0f, 1.0f, 0.0f},
+                       {0.0f, -1.0f, 0.0f}, {0.0f, 0.0f, 1.0f}, {0.0f, 0.0f, -1.0f}};
+    float tf[6];
+    bool ok[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const v3 p = pos[k];
+        const float den = dot(nrm[k], d);
+        const float t = fdiv(dot(sub(p, o), nrm[k]), den);
+        const v3 q = add(o, scale(d, t));
+        bool in;
+        if (k < 2)  // YZ faces
+            in = (q.y > p.y - e.y) & (q.y < p.y + e.y) & (q.z > p.z - e.z) & (q.z < p.z + e.z);
+        else if (k < 4)  // XZ faces
+            in = (q.x > p.x - e.x) & (q.x < p.x + e.x) & (q.z > p.z - e.z) & (q.z < p.z + e.z);
+        else  // XY faces
+            in = (q.x > p.x - e.x) & (q.x < p.x + e.x) & (q.y > p.y - e.y) & (q.y < p.y + e.y);
+        ok[k] = (fabsf(den) > kTMin) & in;
+        tf[k] = t;
+    }
+    // rec1 = boundary.hit(-inf, inf); rec2 = boundary.hit(rec1.t + 0.0001, inf)
+    bool f1 = false, f2 = false;
+    float t1 = kInf, t2 = kInf;
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        if (ok[k] && tf[k] < t1) {
+            t1 = tf[k];
+            f1 = true;
+        }
+    if (!f1) return __builtin_nanf("");
+    const float lo = t1 + 0.0001f;
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        if (ok[k] && tf[k] >= lo && tf[k] < t2) {
+            t2 = tf[k];
+            f2 = true;
+        }
+    if (!f2) return __builtin_nanf("");
+    float t1c = t1 < kTMin ? kTMin : t1;
+    if (t1c >= t2) return __builtin_nanf("");
+    const float len = fsqrt(dot(d, d));
+    const float inside = (t2 - t1c) * len;
+    const float u = medium_u01(mk.seed, mk.pixel, mk.sample, mk.bounce, ob.u0);
+    const float hd = f[6] * (float)ln_pos_d(u);
+    if (hd > inside) return __builtin_nanf("");
+    return t1c + fdiv(hd, len);
+}
+
 template <bool kBvh>
 __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v3 inv, bool live,
-                                           WaveLds& W, uint32_t* stack, int lane, Counters& cnt
+                                           const MediumKey& mk, WaveLds& W, uint32_t* stack, int lane,
+                                           Counters& cnt
 #ifdef RT_STAMPS
                                            , uint64_t* tm
 #endif
@@ -418,6 +481,8 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             } else {
                 mesh_bvh(S.tris, S.tri_orig, S.nodes, root, want, o, d, inv, h, i, ob.order, stack, cnt);
             }
+        } else if (ob.type == kObjMedium) {
+            h.merge(live ? medium_candidate(ob, o, d, mk) : __builtin_nanf(""), ob.order, false, i, -1);
         } else if (kBvh) {  // kObjSphereGroup
             sphere_group(S.objs, S.nodes, ob.u2, live, ray, inv, h, stack, cnt);
         }
@@ -526,7 +591,8 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
         RT_ACC(0, t_a, t_b);
 
         const v3 inv = rcp(ray.d);
-        const Hit h = closest_hit<kBvh>(S, ray, inv, live, W, stack, lane, cnt
+        const MediumKey mk{L.seed, pixel, L.sample_offset + (uint32_t)s, (uint32_t)depth};
+        const Hit h = closest_hit<kBvh>(S, ray, inv, live, mk, W, stack, lane, cnt
 #ifdef RT_STAMPS
                                         , tm
 #endif
@@ -543,7 +609,9 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
             const float* f = ob.f;
             v3 p = add(ray.o, scale(ray.d, h.t));  // ray.at(t)
             v3 outward;
-            if (ob.type == kObjPlane) {
+            if (ob.type == kObjMedium) {
+                outward = v3{1.0f, 0.0f, 0.0f};  // arbitrary; isotropic scatter ignores it
+            } else if (ob.type == kObjPlane) {
                 outward = v3{f[3], f[4], f[5]};
             } else if (ob.type == kObjSphere) {
                 outward = divs(sub(p, v3{f[0], f[1], f[2]}), f[3]);
@@ -592,6 +660,11 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
                 }
                 v3 dir = refl ? reflect(ud, n) : refract(ud, n, ratio);
                 nd = normalize(dir);
+                scattered = true;
+            } else if (m.type == 4u) {
+                // isotropic::scatter: Ray(p, randomInUnitSphere(), time), attenuation = albedo.
+                nd = random_in_unit_sphere(rng);
+                att = v3{m.a0, m.a1, m.a2};
                 scattered = true;
             } else {
                 // Emission::scatter (Material.h:120-123): albedo * intensity, stop.

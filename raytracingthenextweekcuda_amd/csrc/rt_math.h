@@ -253,8 +253,9 @@ RT_HD void pt_sincosf(float x, float* sf, float* cf) {
     *cf = (float)c;
 }
 
-RT_HD float pt_powf(float xf, float yf) {
-    if (!(xf > 0.0f)) return xf == 0.0f ? (yf > 0.0f ? 0.0f : 1.0f) : __builtin_nanf("");
+// ln x for a positive float x, in double: exact frexp split, atanh series on
+// [sqrt(1/2), sqrt(2)), ln 2 in two parts.
+RT_HD double ln_pos_d(float xf) {
     const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
     int e;
     double m = frexp((double)xf, &e);  // exact: m in [0.5, 1)
@@ -277,7 +278,13 @@ RT_HD float pt_powf(float xf, float yf) {
     p = p * t2 + 1.0;
     const double ln_m = 2.0 * t * p;
     const double de = (double)e;
-    const double lnx = (de * ln2_hi + ln_m) + de * ln2_lo;
+    return (de * ln2_hi + ln_m) + de * ln2_lo;
+}
+
+RT_HD float pt_powf(float xf, float yf) {
+    if (!(xf > 0.0f)) return xf == 0.0f ? (yf > 0.0f ? 0.0f : 1.0f) : __builtin_nanf("");
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    const double lnx = ln_pos_d(xf);
     const double z = (double)yf * lnx;
     const double n = floor(z * 1.44269504088896338700 + 0.5);
     const double r = (z - n * ln2_hi) - n * ln2_lo;
@@ -296,6 +303,14 @@ RT_HD float pt_powf(float xf, float yf) {
     q = q * r + 1.0;
     q = q * r + 1.0;
     return (float)ldexp(q, (int)n);
+}
+
+// Free-flight draw of a constant medium: one uniform per (pixel, sample,
+// bounce, medium slot) from its own Philox counter, so the draw does not
+// depend on the order in which the closest-hit scan meets the media.
+RT_HD float medium_u01(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce,
+                       uint32_t slot) {
+    return u01(philox4x32_10(u4{sample, bounce + 1u, slot, 0x6D656469u}, seed, pixel).x);
 }
 
 }  // namespace rt

@@ -281,7 +281,10 @@ std::string HostScene::flatten() {
         r.material = o.material;
         r.u2 = kNoBvh;
         memcpy(r.f, o.f, sizeof(r.f));
-        if (o.type == kObjPlane) {
+        if (o.type == kObjMedium) {
+            r.u0 = (uint32_t)i;             // slot: keys the free-flight draw
+            r.f[6] = -1.0f / o.f[6];        // neg_inv_density
+        } else if (o.type == kObjPlane) {
             r.u0 = o.orientation;
             r.u1 = o.two_side;
         } else if (o.type == kObjMesh) {

@@ -23,7 +23,8 @@ enum ObjType : uint32_t {
     kObjMovingSphere = 1,
     kObjPlane = 2,
     kObjMesh = 3,
-    kObjSphereGroup = 4  // BVH over (moving) spheres: u0 = first member, u1 = count, u2 = root
+    kObjSphereGroup = 4,  // BVH over (moving) spheres: u0 = first member, u1 = count, u2 = root
+    kObjMedium = 5        // constant medium in a cube: f = center xyz, extend xyz, -1/density; u0 = slot
 };
 
 // One hitable (Sphere.h, Plane.h, TriangleMesh.h). Cube is flattened into its
@@ -76,7 +77,7 @@ struct alignas(16) BvhNode {
 static_assert(sizeof(BvhNode) == 32, "BvhNode must be 32 B");
 
 struct alignas(16) MatRec {
-    uint32_t type;  // RT_LAMBERTIAN..RT_EMISSION
+    uint32_t type;  // RT_LAMBERTIAN..RT_ISOTROPIC
     float a0, a1, a2;  // albedo (emission: albedo * intensity, Material.h:121)
     float p0;          // metal: fuzz (clamped to 1, Material.h:40) | dielectric: ior
     float pad0, pad1, pad2;

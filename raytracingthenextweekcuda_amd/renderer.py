@@ -134,6 +134,10 @@ class Renderer:
     def emission(self, index, albedo, intensity=1.0):
         self._check(self.L.rt_material_emission(self.ctx, index, _v(albedo), intensity))
 
+    def isotropic(self, index, albedo):
+        """Phase function of participating media (build extension, rtmi.h)."""
+        self._check(self.L.rt_material_isotropic(self.ctx, index, _v(albedo)))
+
     def sphere(self, index, center, radius, material, shading=True):
         self._check(self.L.rt_sphere(self.ctx, index, _v(center), radius, _mat_index(material), int(shading)))
 
@@ -147,6 +151,11 @@ class Renderer:
 
     def cube(self, index, center, extend, material):
         self._check(self.L.rt_cube(self.ctx, index, _v(center), _v(extend), _mat_index(material)))
+
+    def constant_medium(self, index, center, extend, density, material):
+        """Constant-density medium in an axis-aligned cube (build extension, rtmi.h)."""
+        self._check(self.L.rt_constant_medium(self.ctx, index, _v(center), _v(extend), density,
+                                              _mat_index(material)))
 
     def mesh(self, index, tri_vertices, material):
         v = np.ascontiguousarray(tri_vertices, np.float32).reshape(-1)

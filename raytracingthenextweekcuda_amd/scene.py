@@ -68,6 +68,8 @@ def load_yaml_scene(r: Renderer, path: str, width: int, height: int, models_dir:
                 r.metal(mid, mat["albedo"], float(mat["fuzz"]))
             elif mtype == 3:
                 r.emission(mid, mat["albedo"], float(mat["intensity"]))
+            elif mtype == 4:  # build extension: isotropic phase function
+                r.isotropic(mid, mat["albedo"])
         ptype = int(next(iter(obj.values())))
         if ptype == 0:
             r.sphere(i, obj["center"], float(obj["radius"]), r.materials[mid])
@@ -83,6 +85,10 @@ def load_yaml_scene(r: Renderer, path: str, width: int, height: int, models_dir:
                            r.materials[3])
             else:
                 r.mesh_obj(i, model, obj["scale"], obj["rotate"], obj["offset"], r.materials[3])
+        elif ptype == 3:  # build extension: cube (createCube, kernels.h:139-154)
+            r.cube(i, obj["center"], obj["extend"], r.materials[mid])
+        elif ptype == 4:  # build extension: constant medium in a cube
+            r.constant_medium(i, obj["center"], obj["extend"], float(obj["density"]), r.materials[mid])
         else:
             raise ValueError(f"unknown primitive type {ptype} in {path}")
     if commit:
@@ -94,6 +100,13 @@ def bunny_cornell_box(r: Renderer, width: int, height: int, commit: bool = True)
     """BASELINE config 4: bun_zipper.ply (69,451 triangles) inside the CornellBox1
     walls (build-defined placement, assets/scenes/bunny_cornellbox.yaml)."""
     return load_yaml_scene(r, os.path.join(SCENES_DIR, "bunny_cornellbox.yaml"), width, height,
+                           commit=commit)
+
+
+def cornell_box_media(r: Renderer, width: int, height: int, commit: bool = True) -> Camera:
+    """BASELINE config 5: CornellBox1 walls + two constant-medium boxes + a glass
+    sphere (assets/scenes/cornellbox_media.yaml; media are a build extension)."""
+    return load_yaml_scene(r, os.path.join(SCENES_DIR, "cornellbox_media.yaml"), width, height,
                            commit=commit)
 
 
