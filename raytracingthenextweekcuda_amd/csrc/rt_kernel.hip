@@ -70,12 +70,13 @@ __device__ __forceinline__ bool box_hit(const float* f, v3 o, v3 inv) {
 
 // Conservative BVH node test (boxes are inflated at build time; NaN slabs from
 // 0 * inf are ignored by fminf/fmaxf, i.e. never cull): entry <= min(exit, tmax).
-__device__ __forceinline__ bool node_hit(const BvhNode& n, v3 o, v3 inv, float tmax) {
+__device__ __forceinline__ bool node_hit(const BvhNode& n, v3 o, v3 inv, float tmax, float& tnear) {
     const float tx0 = (n.lo[0] - o.x) * inv.x, tx1 = (n.hi[0] - o.x) * inv.x;
     const float ty0 = (n.lo[1] - o.y) * inv.y, ty1 = (n.hi[1] - o.y) * inv.y;
     const float tz0 = (n.lo[2] - o.z) * inv.z, tz1 = (n.hi[2] - o.z) * inv.z;
     const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
     const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    tnear = tn;
     return tn <= fminf(tf, tmax * 1.00001f + 1e-30f);
 }
 
@@ -249,6 +250,10 @@ __device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, ui
 // BVH mesh: per-lane traversal of the reference's SAH tree (DFS node order,
 // leaves own contiguous ranges of `tris`, `tri_orig` holds the mesh-local
 // triangle index for the lowest-index tie rule of the sequential scan).
+// Ordered traversal: both children are tested at their parent, the nearer one
+// is descended first (kept in registers), the farther one waits on the LDS
+// stack and is re-tested against the best t when popped. The candidate set and
+// the (t, original index) merge make the result independent of the order.
 __device__ __forceinline__ void mesh_bvh(const TriRec* __restrict__ tris,
                                          const uint32_t* __restrict__ tri_orig,
                                          const BvhNode* __restrict__ nodes, uint32_t root, bool want,
@@ -258,16 +263,23 @@ __device__ __forceinline__ void mesh_bvh(const TriRec* __restrict__ tris,
     const float t0 = h.t;
     float best = t0;
     uint32_t best_orig = 0xFFFFFFFFu, best_k = 0;
-    stack[0] = root;
-    int sp = 1;
-    while (sp > 0) {
-        const uint32_t ni = stack[(--sp) * 64];
-        const BvhNode nd = nodes[ni];
-        ++cnt.node_visits;
-        if (nd.b & 0x80000000u) {
-            const uint32_t nt = nd.b & 0x7FFFFFFFu;
+    BvhNode cur = nodes[root];
+    ++cnt.node_visits;
+    bool has = true;
+    int sp = 0;
+    for (;;) {
+        if (!has) {
+            if (sp == 0) break;
+            cur = nodes[stack[(--sp) * 64]];
+            ++cnt.node_visits;
+            float tn;
+            if (!node_hit(cur, o, inv, best, tn)) continue;  // best improved since the push
+            has = true;
+        }
+        if (cur.b & 0x80000000u) {
+            const uint32_t nt = cur.b & 0x7FFFFFFFu;
             cnt.tri_tests += nt;
-            for (uint32_t k = nd.a; k < nd.a + nt; ++k) {
+            for (uint32_t k = cur.a; k < cur.a + nt; ++k) {
                 const float t = tri_t(tris[k], o, d);
                 if (t <= t0) {
                     const uint32_t orig = tri_orig[k];
@@ -278,15 +290,29 @@ __device__ __forceinline__ void mesh_bvh(const TriRec* __restrict__ tris,
                     }
                 }
             }
-        } else {
-            const bool hl = node_hit(nodes[nd.a], o, inv, best);
-            const bool hr = node_hit(nodes[nd.b], o, inv, best);
-            if (sp + 2 > kStackDepth) {
+            has = false;
+            continue;
+        }
+        const uint32_t il = cur.a, ir = cur.b;
+        const BvhNode nl = nodes[il], nr = nodes[ir];
+        cnt.node_visits += 2;
+        float tl, tr;
+        const bool hl = node_hit(nl, o, inv, best, tl);
+        const bool hr = node_hit(nr, o, inv, best, tr);
+        if (hl && hr) {
+            if (sp + 1 > kStackDepth) {
                 cnt.overflow = 1;
                 break;
             }
-            if (hr) stack[(sp++) * 64] = nd.b;
-            if (hl) stack[(sp++) * 64] = nd.a;
+            const bool left_first = tl <= tr;
+            stack[(sp++) * 64] = left_first ? ir : il;
+            cur = left_first ? nl : nr;
+        } else if (hl) {
+            cur = nl;
+        } else if (hr) {
+            cur = nr;
+        } else {
+            has = false;
         }
     }
     if (best_orig != 0xFFFFFFFFu) h.merge(best, order, false, obj, (int32_t)best_k);
@@ -337,37 +363,54 @@ __device__ __forceinline__ void sphere_group(const ObjRec* __restrict__ objs,
                                              uint32_t* stack, Counters& cnt) {
     if (!live) return;
     const v3 o = ray.o, d = ray.d;
-    stack[0] = root;
-    int sp = 1;
-    while (sp > 0) {
-        const uint32_t ni = stack[(--sp) * 64];
-        const BvhNode nd = nodes[ni];
-        ++cnt.node_visits;
-        if (nd.b & 0x80000000u) {
-            const uint32_t n = nd.b & 0x7FFFFFFFu;
-            for (uint32_t k = nd.a; k < nd.a + n; ++k) {
+    BvhNode cur = nodes[root];
+    ++cnt.node_visits;
+    bool has = true;
+    int sp = 0;
+    for (;;) {  // ordered as mesh_bvh
+        if (!has) {
+            if (sp == 0) break;
+            cur = nodes[stack[(--sp) * 64]];
+            ++cnt.node_visits;
+            float tn;
+            if (!node_hit(cur, o, inv, h.t, tn)) continue;
+            has = true;
+        }
+        if (cur.b & 0x80000000u) {
+            const uint32_t n = cur.b & 0x7FFFFFFFu;
+            for (uint32_t k = cur.a; k < cur.a + n; ++k) {
                 const ObjRec ob = load_obj(objs, (int)k);
                 if (ob.type == kObjMovingSphere) ++cnt.grp_moving;
                 else ++cnt.grp_spheres;
                 h.merge(sphere_candidate(ob, o, d, ray.time), ob.order, true, (int32_t)k, -1);
             }
-        } else {
-            const bool hl = node_hit(nodes[nd.a], o, inv, h.t);
-            const bool hr = node_hit(nodes[nd.b], o, inv, h.t);
-            if (sp + 2 > kStackDepth) {
+            has = false;
+            continue;
+        }
+        const uint32_t il = cur.a, ir = cur.b;
+        const BvhNode nl = nodes[il], nr = nodes[ir];
+        cnt.node_visits += 2;
+        float tl, tr;
+        const bool hl = node_hit(nl, o, inv, h.t, tl);
+        const bool hr = node_hit(nr, o, inv, h.t, tr);
+        if (hl && hr) {
+            if (sp + 1 > kStackDepth) {
                 cnt.overflow = 1;
                 break;
             }
-            if (hr) stack[(sp++) * 64] = nd.b;
-            if (hl) stack[(sp++) * 64] = nd.a;
+            const bool left_first = tl <= tr;
+            stack[(sp++) * 64] = left_first ? ir : il;
+            cur = left_first ? nl : nr;
+        } else if (hl) {
+            cur = nl;
+        } else if (hr) {
+            cur = nr;
+        } else {
+            has = false;
         }
     }
 }
 
-// hit() over the flattened object table (main.cu:43-57). Called with the whole
-// wave active; `live` masks lanes without a path. Records are fetched one
-// object ahead (scalar loads overlap the current object's VALU work), and the
-// per-object tests are branch-free candidates merged with Hit's tie rule.
 // Key of a segment's medium free-flight draws (medium_u01).
 struct MediumKey {
     uint32_t seed, pixel, sample, bounce;
@@ -430,6 +473,10 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
     return t1c + fdiv(hd, len);
 }
 
+// hit() over the flattened object table (main.cu:43-57). Called with the whole
+// wave active; `live` masks lanes without a path. Records are fetched one
+// object ahead (scalar loads overlap the current object's VALU work), and the
+// per-object tests are branch-free candidates merged with Hit's tie rule.
 template <bool kBvh>
 __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v3 inv, bool live,
                                            const MediumKey& mk, WaveLds& W, uint32_t* stack, int lane,
