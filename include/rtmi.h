@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define RTMI_ABI_VERSION 3
+#define RTMI_ABI_VERSION 4
 
 typedef int32_t rt_status;
 enum {
@@ -195,6 +195,20 @@ rt_status rt_render(rt_ctx* ctx, const rt_render_params* params, float* out_rgb_
 rt_status rt_render_device(rt_ctx* ctx, const rt_render_params* params, float* out_rgb_device,
                            void* hip_stream);
 rt_status rt_sync_stats(rt_ctx* ctx, rt_render_stats* out);
+/* renderKernel's offline output (Canvas::writePixel(index, color / spp), Canvas.h:58-71):
+ * gamma-corrected uint8 RGB of the owned rows, computed on the device. */
+rt_status rt_render_u8(rt_ctx* ctx, const rt_render_params* params, uint8_t* out_rgb8_host);
+/* GPU_REALTIME progressive mode (renderKernel -> Canvas::accumulatePixel, Canvas.h:73-98,
+ * main.cu:876-888): adds each owned pixel's sample SUM over params->spp samples
+ * (reference: 1 per frame) to the caller's device buffer `accum_device` (float RGB,
+ * same layout as the output) and, when `pixels_device` is not NULL, writes
+ * gamma(acc * (1.0f / sample_count)) to it as uint8 RGB. `sample_count` is the
+ * canvas's count after incrementSampleCount (total samples per pixel so far);
+ * use params->sample_offset = samples already accumulated so each frame draws
+ * fresh samples. Clearing the buffer (clearAccumulationBuffer on a camera
+ * change) is the caller's: it owns the memory. Asynchronous on `hip_stream`. */
+rt_status rt_accumulate(rt_ctx* ctx, const rt_render_params* params, float* accum_device,
+                        uint32_t sample_count, uint8_t* pixels_device, void* hip_stream);
 
 /* Canvas::gamma (Canvas.h:198-200): u8 = uint(255.99 * clamp(sqrt(c), 0, 0.999)). */
 rt_status rt_gamma_u8(const float* rgb, int64_t n, uint8_t* out);

@@ -23,7 +23,7 @@ STATUS_NAMES = {
 }
 
 # Every symbol include/rtmi.h declares (checked by tests/test_abi.py).
-ABI_VERSION = 3  # include/rtmi.h RTMI_ABI_VERSION
+ABI_VERSION = 4  # include/rtmi.h RTMI_ABI_VERSION
 
 EXPORTS = [
     "rt_abi_version", "rt_create", "rt_destroy", "rt_last_error", "rt_clear_scene",
@@ -33,7 +33,8 @@ EXPORTS = [
     "rt_cube", "rt_mesh", "rt_mesh_obj", "rt_mesh_triangle_count", "rt_mesh_vertices",
     "rt_mesh_ply", "rt_ply_bvh_image", "rt_load_object", "rt_process_triangle_data",
     "rt_pathtrace_bvh_image",
-    "rt_camera", "rt_commit", "rt_scene_info", "rt_render", "rt_render_device", "rt_sync_stats", "rt_gamma_u8",
+    "rt_camera", "rt_commit", "rt_scene_info", "rt_render", "rt_render_device", "rt_sync_stats",
+    "rt_render_u8", "rt_accumulate", "rt_gamma_u8",
 ]
 
 
@@ -122,6 +123,8 @@ def lib():
     L.rt_render.argtypes = [vp, C.POINTER(RenderParams), fp]
     L.rt_render_device.argtypes = [vp, C.POINTER(RenderParams), vp, vp]
     L.rt_sync_stats.argtypes = [vp, C.POINTER(RenderStats)]
+    L.rt_render_u8.argtypes = [vp, C.POINTER(RenderParams), C.POINTER(C.c_uint8)]
+    L.rt_accumulate.argtypes = [vp, C.POINTER(RenderParams), vp, C.c_uint32, vp, vp]
     L.rt_gamma_u8.argtypes = [fp, C.c_int64, C.POINTER(C.c_uint8)]
     _lib = L
     return L

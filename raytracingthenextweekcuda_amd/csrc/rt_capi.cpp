@@ -34,6 +34,8 @@ struct rt_ctx {
     unsigned long long* d_counters = nullptr;
     float* d_out = nullptr;   // staging buffer for rt_render (host output)
     size_t d_out_bytes = 0;
+    uint8_t* d_u8 = nullptr;  // staging buffer for rt_render_u8
+    size_t d_u8_bytes = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool have_events = false;
     rt_render_stats last{};
@@ -154,6 +156,7 @@ void rt_destroy(rt_ctx* c) {
         free_pathtrace(c);
         (void)hipFree(c->d_counters);
         (void)hipFree(c->d_out);
+        (void)hipFree(c->d_u8);
         if (c->have_events) {
             (void)hipEventDestroy(c->ev0);
             (void)hipEventDestroy(c->ev1);
@@ -558,18 +561,16 @@ static rt_status validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch
     if (s < 0 || s > 64 || (s & (s - 1)) != 0)
         return fail(c, RT_ERR_INVALID, "lanes_per_pixel must be 0 (auto) or a power of two <= 64");
     rt::choose_layout(L, s);
+    L.accumulate = 0;
+    L.accum_scale = 0.0f;
+    L.u8 = nullptr;
     L.pt_has_mesh = c->pt_tris > 0 ? 1 : 0;
     L.pt_scale = c->pt_scale;
     return RT_OK;
 }
 
-rt_status rt_render_device(rt_ctx* c, const rt_render_params* p, float* out, void* stream) {
-    if (!c) return RT_ERR_INVALID;
-    rt::RenderLaunch L;
-    rt_status s = validate(c, p, L);
-    if (s != RT_OK) return s;
-    if (!out && L.local_rows > 0) return fail(c, RT_ERR_INVALID, "null output");
-    hipStream_t st = (hipStream_t)stream;
+static rt_status launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaunch& L, float* out,
+                        hipStream_t st) {
     RT_HIP(c, hipSetDevice(c->device));
     RT_HIP(c, hipMemsetAsync(c->d_counters, 0, rt::kNumCounters * sizeof(unsigned long long), st));
     RT_HIP(c, hipEventRecord(c->ev0, st));
@@ -587,6 +588,30 @@ rt_status rt_render_device(rt_ctx* c, const rt_render_params* p, float* out, voi
     c->last.lanes_per_pixel = (uint32_t)L.lanes_per_pixel;
     c->stats_pending = true;
     return RT_OK;
+}
+
+rt_status rt_render_device(rt_ctx* c, const rt_render_params* p, float* out, void* stream) {
+    if (!c) return RT_ERR_INVALID;
+    rt::RenderLaunch L;
+    rt_status s = validate(c, p, L);
+    if (s != RT_OK) return s;
+    if (!out && L.local_rows > 0) return fail(c, RT_ERR_INVALID, "null output");
+    return launch(c, p, L, out, (hipStream_t)stream);
+}
+
+rt_status rt_accumulate(rt_ctx* c, const rt_render_params* p, float* accum, uint32_t sample_count,
+                        uint8_t* pixels, void* stream) {
+    if (!c) return RT_ERR_INVALID;
+    rt::RenderLaunch L;
+    rt_status s = validate(c, p, L);
+    if (s != RT_OK) return s;
+    if (!accum && L.local_rows > 0) return fail(c, RT_ERR_INVALID, "null accumulation buffer");
+    if (pixels && sample_count == 0) return fail(c, RT_ERR_INVALID, "sample_count must be >= 1");
+    L.accumulate = 1;
+    L.u8 = pixels;
+    // Canvas::incrementSampleCount: scale = 1.0f / sampleCount (Canvas.h:166-169).
+    L.accum_scale = sample_count ? 1.0f / (float)sample_count : 0.0f;
+    return launch(c, p, L, accum, (hipStream_t)stream);
 }
 
 rt_status rt_sync_stats(rt_ctx* c, rt_render_stats* out) {
@@ -632,6 +657,39 @@ rt_status rt_render(rt_ctx* c, const rt_render_params* p, float* out_host) {
     if (s != RT_OK) return s;
     RT_HIP(c, hipStreamSynchronize(nullptr));
     if (bytes) RT_HIP(c, hipMemcpy(out_host, c->d_out, bytes, hipMemcpyDeviceToHost));
+    s = rt_sync_stats(c, nullptr);
+    if (s != RT_OK) return s;
+    if (c->last.overflow) return fail(c, RT_ERR_OVERFLOW, "BVH traversal stack overflow");
+    return RT_OK;
+}
+
+rt_status rt_render_u8(rt_ctx* c, const rt_render_params* p, uint8_t* out_host) {
+    if (!c) return RT_ERR_INVALID;
+    rt::RenderLaunch L;
+    rt_status s = validate(c, p, L);
+    if (s != RT_OK) return s;
+    const size_t n = (size_t)L.local_rows * L.width * 3;
+    if (!out_host && n) return fail(c, RT_ERR_INVALID, "null output");
+    RT_HIP(c, hipSetDevice(c->device));
+    if (n * sizeof(float) > c->d_out_bytes) {
+        (void)hipFree(c->d_out);
+        c->d_out = nullptr;
+        c->d_out_bytes = 0;
+        RT_HIP(c, hipMalloc(&c->d_out, n * sizeof(float)));
+        c->d_out_bytes = n * sizeof(float);
+    }
+    if (n > c->d_u8_bytes) {
+        (void)hipFree(c->d_u8);
+        c->d_u8 = nullptr;
+        c->d_u8_bytes = 0;
+        RT_HIP(c, hipMalloc(&c->d_u8, n));
+        c->d_u8_bytes = n;
+    }
+    L.u8 = c->d_u8;
+    s = launch(c, p, L, c->d_out, nullptr);
+    if (s != RT_OK) return s;
+    RT_HIP(c, hipStreamSynchronize(nullptr));
+    if (n) RT_HIP(c, hipMemcpy(out_host, c->d_u8, n, hipMemcpyDeviceToHost));
     s = rt_sync_stats(c, nullptr);
     if (s != RT_OK) return s;
     if (c->last.overflow) return fail(c, RT_ERR_OVERFLOW, "BVH traversal stack overflow");

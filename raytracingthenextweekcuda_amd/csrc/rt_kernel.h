@@ -18,6 +18,13 @@ struct RenderLaunch {
     int32_t tile_w, tile_h;   // per-wave pixel tile, tile_w * tile_h = 64 / S
     int32_t pt_has_mesh;      // pathTrace: a triangle BVH is present
     float pt_scale;           // pathTrace: max |coordinate| of the triangles
+    // Pixel output (Canvas.h:58-98): accumulate = 0 writes the mean color/spp to
+    // `out` (and gamma(mean) to u8 when set: writePixel); accumulate = 1 adds the
+    // sample sum to `out` (accumulatePixel) and, when u8 is set, writes
+    // gamma(acc * accum_scale) with accum_scale = 1.0f / sampleCount.
+    int32_t accumulate;
+    float accum_scale;
+    uint8_t* u8;
 };
 
 // Lane-layout choice: S = lanes_per_pixel (0 = auto). Auto raises S (power of

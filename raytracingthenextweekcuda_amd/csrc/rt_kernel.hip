@@ -575,6 +575,38 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 
 // kBvh: the scene has BVH meshes (needs the 32 KB/block LDS traversal stacks,
 // which would otherwise cap occupancy for scenes that never use them).
+// Canvas::gamma (Canvas.h:198-200) with clamp = fmaxf(a, fminf(f, b)).
+__device__ __forceinline__ uint8_t gamma_u8(float c) {
+    const float v = fmaxf(0.0f, fminf(fsqrt(c), 0.999f));
+    return (uint8_t)(uint32_t)(255.99f * v);
+}
+
+// writePixel / accumulatePixel (Canvas.h:58-98) for one pixel's sample sum.
+__device__ __forceinline__ void write_pixel(const RenderLaunch& L, float* __restrict__ out, size_t o,
+                                            v3 sum, float fs) {
+    if (L.accumulate) {
+        const v3 acc{out[o + 0] + sum.x, out[o + 1] + sum.y, out[o + 2] + sum.z};
+        out[o + 0] = acc.x;
+        out[o + 1] = acc.y;
+        out[o + 2] = acc.z;
+        if (L.u8) {
+            L.u8[o + 0] = gamma_u8(acc.x * L.accum_scale);
+            L.u8[o + 1] = gamma_u8(acc.y * L.accum_scale);
+            L.u8[o + 2] = gamma_u8(acc.z * L.accum_scale);
+        }
+    } else {
+        const v3 m{sum.x / fs, sum.y / fs, sum.z / fs};
+        out[o + 0] = m.x;
+        out[o + 1] = m.y;
+        out[o + 2] = m.z;
+        if (L.u8) {
+            L.u8[o + 0] = gamma_u8(m.x);
+            L.u8[o + 1] = gamma_u8(m.y);
+            L.u8[o + 2] = gamma_u8(m.z);
+        }
+    }
+}
+
 template <bool kBvh>
 __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
@@ -764,10 +796,7 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
 
     if (valid && c == 0) {
         const float fs = (float)L.spp;
-        const size_t o = ((size_t)lrow * (size_t)L.width + (size_t)px) * 3;
-        out[o + 0] = sum.x / fs;
-        out[o + 1] = sum.y / fs;
-        out[o + 2] = sum.z / fs;
+        write_pixel(L, out, ((size_t)lrow * (size_t)L.width + (size_t)px) * 3, sum, fs);
     }
 
     const uint64_t ws = wave_sum_u64(cnt.segs);
@@ -1263,10 +1292,7 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
     }
     if (valid && c == 0) {
         const float fs = (float)L.spp;
-        const size_t oi = ((size_t)lrow * (size_t)L.width + (size_t)px) * 3;
-        out[oi + 0] = sum.x / fs;
-        out[oi + 1] = sum.y / fs;
-        out[oi + 2] = sum.z / fs;
+        write_pixel(L, out, ((size_t)lrow * (size_t)L.width + (size_t)px) * 3, sum, fs);
     }
     const uint64_t ws = wave_sum_u64(cnt.segs);
     const uint64_t wt = wave_sum_u64(cnt.tri_tests);

@@ -238,6 +238,26 @@ class Renderer:
         self._check(self.L.rt_render(self.ctx, C.byref(p), out.ctypes.data_as(C.POINTER(C.c_float))))
         return out
 
+    def render_u8(self, width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,
+                  row_rank=0, row_world=1, lanes_per_pixel=1, integrator="rayColor") -> np.ndarray:
+        """renderKernel's offline uint8 output: gamma(color / spp) per channel
+        (Canvas::writePixel), computed on the device. Shape (rows, width, 3), y = 0 bottom."""
+        p = self.params(width, height, spp, max_depth, seed, sample_offset, row_block, row_rank,
+                        row_world, lanes_per_pixel, integrator)
+        rows = owned_rows(height, row_block, row_rank, row_world)
+        out = np.zeros((rows, width, 3), np.uint8)
+        self._check(self.L.rt_render_u8(self.ctx, C.byref(p), out.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return out
+
+    def accumulate_device(self, params: RenderParams, accum_ptr: int, sample_count: int,
+                          pixels_ptr: int = 0, stream_ptr: int = 0):
+        """GPU_REALTIME progressive frame (Canvas::accumulatePixel): add this call's
+        per-pixel sample sums to a caller-owned device float buffer and, if
+        pixels_ptr is set, write gamma(acc * (1 / sample_count)) as uint8."""
+        self._check(self.L.rt_accumulate(self.ctx, C.byref(params), C.c_void_p(accum_ptr),
+                                         int(sample_count), C.c_void_p(pixels_ptr or None),
+                                         C.c_void_p(stream_ptr)))
+
     def render_device(self, params: RenderParams, out_ptr: int, stream_ptr: int = 0):
         """Enqueue a render into a caller-owned device buffer (e.g. a torch tensor's
         data_ptr()) on a HIP stream (torch.cuda.Stream.cuda_stream)."""

@@ -228,3 +228,48 @@ def test_exact_ties_follow_sequential_rule(rtmi, n_extra):
     ref, ref_st = S.build_oracle(spec).render(w, h, spp, depth)
     _check(img, ref, st, ref_st, f"ties{n_extra}")
     assert np.array_equal(img, ref)
+
+
+@pytest.mark.gpu
+def test_render_u8_is_gamma_of_the_mean():
+    # renderKernel's offline path: writePixel(index, color / spp) -> Canvas::gamma
+    import raytracingthenextweekcuda_amd as rtmi
+    from oracle import oracle as orc
+
+    w, h = 32, 24
+    r = rtmi.Renderer(0)
+    rtmi.cornell_box1(r, w, h)
+    got = r.render_u8(w, h, 4, 4)
+    r.close()
+    sc = orc.yaml_scene(os.path.join(S.SCENES, "cornellbox1.yaml"), S.MODELS, w, h)
+    want, _ = sc.render(w, h, 4, 4, threads=8)
+    assert np.array_equal(got, orc.gamma_u8(want))
+
+
+@pytest.mark.gpu
+def test_realtime_accumulation_matches_per_frame_sums():
+    # GPU_REALTIME: 1 spp per frame, acc += color, display gamma(acc * (1.0f / n))
+    import torch
+
+    import raytracingthenextweekcuda_amd as rtmi
+    from oracle import oracle as orc
+
+    w, h, frames = 24, 16, 5
+    r = rtmi.Renderer(0)
+    rtmi.cornell_box1(r, w, h)
+    acc = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda")
+    pix = torch.zeros((h, w, 3), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for n in range(frames):
+        p = r.params(w, h, 1, 6, 1984, n)
+        r.accumulate_device(p, acc.data_ptr(), n + 1, pix.data_ptr(), stream)
+    torch.cuda.synchronize()
+    r.close()
+    sc = orc.yaml_scene(os.path.join(S.SCENES, "cornellbox1.yaml"), S.MODELS, w, h)
+    want = np.zeros((h, w, 3), np.float32)
+    for n in range(frames):
+        frame, _ = sc.render(w, h, 1, 6, sample_offset=n, threads=8)
+        want = want + frame
+    assert np.array_equal(acc.cpu().numpy(), want)
+    scale = np.float32(1.0) / np.float32(frames)
+    assert np.array_equal(pix.cpu().numpy(), orc.gamma_u8(want * scale))
