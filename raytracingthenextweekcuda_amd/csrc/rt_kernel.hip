@@ -668,6 +668,11 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
         const bool live = alive && !need_cam;
         RT_STAMP(t_b);
         RT_ACC(0, t_a, t_b);
+#ifdef RT_STAMPS
+        tm[4] += 1;                                  // loop trips (per wave)
+        tm[5] += (uint64_t)__popcll(__ballot(live));  // lanes tracing a segment this trip
+        tm[6] += (uint64_t)__popcll(__ballot(valid)); // lanes that own a pixel
+#endif
 
         const v3 inv = rcp(ray.d);
         const MediumKey mk{L.seed, pixel, L.sample_offset + (uint32_t)s, (uint32_t)depth};

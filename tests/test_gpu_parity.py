@@ -170,13 +170,32 @@ def test_lanes_per_pixel_parity(rtmi, lanes):
     assert np.max(np.abs(img - seq)) <= 1e-5
 
 
-def test_auto_lane_layout_fills_small_shards(rtmi):
+def test_auto_lane_layout(rtmi):
+    # largest power of two S <= min(32, spp) with pixels * S <= 2^24 (rt_kernel.h choose_layout)
     with rtmi.Renderer(0) as r:
         rtmi.cornell_box1(r, 64, 64)
         r.render(64, 64, 32, 4, lanes_per_pixel=0)
-        assert r.stats()["lanes_per_pixel"] == 16
-        r.render(512, 512, 2, 1, lanes_per_pixel=0)
-        assert r.stats()["lanes_per_pixel"] == 1
+        assert r.stats()["lanes_per_pixel"] == 32
+        r.render(64, 64, 8, 4, lanes_per_pixel=0)
+        assert r.stats()["lanes_per_pixel"] == 8
+        r.render(2048, 2048, 64, 1, lanes_per_pixel=0)
+        assert r.stats()["lanes_per_pixel"] == 4
+
+
+def test_auto_layout_within_north_star_tolerance_of_sequential_sum(rtmi):
+    # the bench's auto layout sums samples in S sub-streams: bit-exact against the
+    # oracle with the same S, and within 1e-4 of the reference's sequential sum
+    w, h, spp, depth = 48, 40, 64, 6
+    with rtmi.Renderer(0) as r:
+        rtmi.cornell_box1(r, w, h)
+        img = r.render(w, h, spp, depth, lanes_per_pixel=0)
+        lanes = r.stats()["lanes_per_pixel"]
+    assert lanes == 32
+    sc = _oracle_yaml("cornellbox1.yaml", w, h)
+    same_s, _ = sc.render(w, h, spp, depth, lanes_per_pixel=lanes)
+    assert np.array_equal(img, same_s)
+    seq, _ = sc.render(w, h, spp, depth)
+    assert np.max(np.abs(img - seq)) <= 1e-4
 
 
 @pytest.mark.parametrize("name,w,h,spp", [("bunny_small_cornellbox.yaml", 48, 48, 4),

@@ -1,0 +1,23 @@
+"""Kernel time of rank 0's row shard vs lanes_per_pixel (CornellBox1 512², 128 spp, d8).
+Usage: python tools/lanes_sweep.py  (prints world, S, kernel ms; best of 3)"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402,F401
+
+import raytracingthenextweekcuda_amd as rtmi  # noqa: E402
+
+W = H = 512
+r = rtmi.Renderer(0)
+rtmi.cornell_box1(r, W, H)
+out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+stream = torch.cuda.current_stream().cuda_stream
+for world, lanes in [(1, 1), (1, 2), (1, 4), (2, 2), (2, 4), (2, 8), (4, 4), (4, 8), (4, 16),
+                     (8, 8), (8, 16), (8, 32), (8, 64)]:
+    p = r.params(W, H, 128, 8, 1984, 0, 8, 0, world, lanes)
+    best = 1e9
+    for _ in range(3):
+        r.render_device(p, out.data_ptr(), stream)
+        best = min(best, r.stats()["kernel_ms"])
+    print(f"world {world} S {lanes} kernel_ms {best:.3f}", flush=True)
