@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define RTMI_ABI_VERSION 4
+#define RTMI_ABI_VERSION 5
 
 typedef int32_t rt_status;
 enum {
@@ -72,15 +72,19 @@ typedef struct rt_render_params {
                                given value; 1 = the reference's sequential sum. */
     int32_t integrator;     /* RT_INTEGRATOR_RAYCOLOR (0) or RT_INTEGRATOR_PATHTRACE (1).
                                pathTrace bounces max_depth times (reference: 5). */
+    uint32_t flags;         /* RT_RENDER_KEEP_COUNTERS: add this launch's counters to the
+                               previous ones instead of resetting them (one rt_sync_stats
+                               after many launches, no per-launch host sync) */
 } rt_render_params;
+enum { RT_RENDER_KEEP_COUNTERS = 1 };
 
 typedef struct rt_render_stats {
     uint64_t segments;      /* closest-hit queries traced (camera ray = 1, +1 per scatter) */
-    uint64_t samples;       /* camera samples = owned pixels * spp */
+    uint64_t samples;       /* camera samples = owned pixels * spp (summed over kept launches) */
     uint64_t node_visits;   /* BVH node visits (0 for linear-scan scenes) */
     uint64_t tri_tests;     /* triangle records tested */
     uint64_t box_tests;     /* mesh bounding boxes tested */
-    double kernel_ms;       /* duration of the render kernel (hipEvent) */
+    double kernel_ms;       /* duration of the last render kernel (hipEvent) */
     uint32_t overflow;      /* 1 if any lane overflowed the traversal stack */
     uint32_t lanes_per_pixel; /* lane layout used by the last render */
     uint64_t group_sphere_tests;        /* spheres tested in object-BVH leaves */

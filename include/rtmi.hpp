@@ -150,7 +150,7 @@ public:
                      uint32_t sampleOffset = 0) {
         commit();
         rt_render_params p{canvas.getWidth(), canvas.getHeight(), spp, bounces, seed, sampleOffset,
-                           1, 0, 1, 0, RT_INTEGRATOR_RAYCOLOR};
+                           1, 0, 1, 0, RT_INTEGRATOR_RAYCOLOR, 0};
         check(rt_render(ctx_, &p, canvas.data()));
     }
 
@@ -166,7 +166,7 @@ public:
     void pathTraceFrame(Canvas& canvas, int32_t spp, int32_t bounces = 5, uint32_t seed = 1984,
                         uint32_t sampleOffset = 0) {
         rt_render_params p{canvas.getWidth(), canvas.getHeight(), spp, bounces, seed, sampleOffset,
-                           1, 0, 1, 0, RT_INTEGRATOR_PATHTRACE};
+                           1, 0, 1, 0, RT_INTEGRATOR_PATHTRACE, 0};
         check(rt_render(ctx_, &p, canvas.data()));
     }
 

@@ -23,7 +23,7 @@ STATUS_NAMES = {
 }
 
 # Every symbol include/rtmi.h declares (checked by tests/test_abi.py).
-ABI_VERSION = 4  # include/rtmi.h RTMI_ABI_VERSION
+ABI_VERSION = 5  # include/rtmi.h RTMI_ABI_VERSION
 
 EXPORTS = [
     "rt_abi_version", "rt_create", "rt_destroy", "rt_last_error", "rt_clear_scene",
@@ -49,7 +49,7 @@ class RenderParams(C.Structure):
         ("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32),
         ("max_depth", C.c_int32), ("seed", C.c_uint32), ("sample_offset", C.c_uint32),
         ("row_block", C.c_int32), ("row_rank", C.c_int32), ("row_world", C.c_int32),
-        ("lanes_per_pixel", C.c_int32), ("integrator", C.c_int32),
+        ("lanes_per_pixel", C.c_int32), ("integrator", C.c_int32), ("flags", C.c_uint32),
     ]
 
 

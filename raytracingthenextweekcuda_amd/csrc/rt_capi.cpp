@@ -533,6 +533,7 @@ rt_status rt_scene_info(const rt_ctx* c, int32_t out[8]) {
 static rt_status validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& L) {
     if (!p) return fail(c, RT_ERR_INVALID, "null params");
     if (c->device < 0) return fail(c, RT_ERR_NODEV, "context has no device");
+    if (p->flags & ~(uint32_t)RT_RENDER_KEEP_COUNTERS) return fail(c, RT_ERR_INVALID, "unknown flags");
     if (p->integrator != RT_INTEGRATOR_RAYCOLOR && p->integrator != RT_INTEGRATOR_PATHTRACE)
         return fail(c, RT_ERR_INVALID, "unknown integrator");
     if (p->integrator == RT_INTEGRATOR_RAYCOLOR && !c->committed)
@@ -572,7 +573,8 @@ static rt_status validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch
 static rt_status launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaunch& L, float* out,
                         hipStream_t st) {
     RT_HIP(c, hipSetDevice(c->device));
-    RT_HIP(c, hipMemsetAsync(c->d_counters, 0, rt::kNumCounters * sizeof(unsigned long long), st));
+    const bool keep = (p->flags & RT_RENDER_KEEP_COUNTERS) != 0;
+    if (!keep) RT_HIP(c, hipMemsetAsync(c->d_counters, 0, rt::kNumCounters * sizeof(unsigned long long), st));
     RT_HIP(c, hipEventRecord(c->ev0, st));
     if (p->integrator == RT_INTEGRATOR_PATHTRACE) {
         rt::PtSceneArgs pt{c->d_pt_tris, c->d_pt_nodes, c->d_pt_list};
@@ -583,8 +585,9 @@ static rt_status launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLa
         RT_HIP(c, rt::launch_render(sc, c->scene.camera, L, out, c->d_counters, st));
     }
     RT_HIP(c, hipEventRecord(c->ev1, st));
+    const uint64_t prev_samples = keep ? c->last.samples : 0;
     c->last = rt_render_stats{};
-    c->last.samples = (uint64_t)L.local_rows * (uint64_t)L.width * (uint64_t)L.spp;
+    c->last.samples = prev_samples + (uint64_t)L.local_rows * (uint64_t)L.width * (uint64_t)L.spp;
     c->last.lanes_per_pixel = (uint32_t)L.lanes_per_pixel;
     c->stats_pending = true;
     return RT_OK;

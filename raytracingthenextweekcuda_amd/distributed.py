@@ -53,28 +53,37 @@ class RowShardedFrame:
         self.rows = owned_rows(height, row_block, self.rank, self.world)
         self.max_rows = max_tile_rows(height, row_block, self.world)
         self.device = device if device is not None else torch.device("cpu")
-        self.tile = torch.zeros((self.max_rows, width, 3), dtype=torch.float32, device=self.device)
         self.frame = None
         self.gather_list = None
-        self.index = None
+        self.src_rows = None
+        if self.world == 1:
+            # one rank owns every row in order: render straight into the frame
+            self.frame = torch.zeros((height, width, 3), dtype=torch.float32, device=self.device)
+            self.tile = self.frame
+            return
+        self.tile = torch.zeros((self.max_rows, width, 3), dtype=torch.float32, device=self.device)
         if self.rank == 0:
             self.frame = torch.zeros((height, width, 3), dtype=torch.float32, device=self.device)
-            if self.world > 1:
-                self.gather_list = [torch.empty_like(self.tile) for _ in range(self.world)]
-                ids = tile_rows(height, row_block, self.world)
-                self.index = [torch.as_tensor(r, dtype=torch.long, device=self.device) for r in ids]
+            # the gather lands in one (world * max_rows) block; frame row y is
+            # block row rank(y) * max_rows + (its position in that rank's tile)
+            self.gathered = torch.empty((self.world * self.max_rows, width, 3), dtype=torch.float32,
+                                        device=self.device)
+            self.gather_list = list(self.gathered.view(self.world, self.max_rows, width, 3).unbind(0))
+            src = [0] * height
+            for k, ids in enumerate(tile_rows(height, row_block, self.world)):
+                for j, y in enumerate(ids):
+                    src[int(y)] = k * self.max_rows + j
+            self.src_rows = torch.as_tensor(src, dtype=torch.long, device=self.device)
 
     def gather(self) -> Optional["object"]:
-        """One gather of every rank's tile to rank 0, then de-interleave."""
+        """One gather of every rank's tile to rank 0, then one row permutation."""
         if self.world == 1:
-            self.frame[: self.rows] = self.tile[: self.rows]
             return self.frame
         self.dist.gather(self.tile, self.gather_list if self.rank == 0 else None, dst=0,
                          group=self.group)
         if self.rank != 0:
             return None
-        for k, rows in enumerate(self.index):
-            self.frame.index_copy_(0, rows, self.gather_list[k][: rows.numel()])
+        self.torch.index_select(self.gathered, 0, self.src_rows, out=self.frame)
         return self.frame
 
     def render(self, render_into: Callable[["object"], None]):

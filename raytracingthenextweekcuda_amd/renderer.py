@@ -220,9 +220,11 @@ class Renderer:
     # ---- render ----
     @staticmethod
     def params(width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,
-               row_rank=0, row_world=1, lanes_per_pixel=1, integrator="rayColor") -> RenderParams:
+               row_rank=0, row_world=1, lanes_per_pixel=1, integrator="rayColor",
+               keep_counters=False) -> RenderParams:
         return RenderParams(width, height, spp, max_depth, seed, sample_offset, row_block,
-                            row_rank, row_world, lanes_per_pixel, _integrator(integrator))
+                            row_rank, row_world, lanes_per_pixel, _integrator(integrator),
+                            KEEP_COUNTERS if keep_counters else 0)
 
     def render(self, width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,
                row_rank=0, row_world=1, lanes_per_pixel=1, integrator="rayColor") -> np.ndarray:
@@ -274,6 +276,7 @@ class Renderer:
 
 REFLECTION_TYPES = {"DIFFUSE": 0, "METAL": 1, "SPECULAR": 2, "REFRACTION": 3, "COAT": 4}
 INTEGRATORS = {"rayColor": 0, "pathTrace": 1}
+KEEP_COUNTERS = 1  # rtmi.h RT_RENDER_KEEP_COUNTERS
 
 
 def _reflection_type(t) -> int:
