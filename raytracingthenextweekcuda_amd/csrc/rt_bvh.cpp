@@ -8,6 +8,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <fstream>
 #include <memory>
 
@@ -45,6 +46,90 @@ struct Builder {
         return (int)pool.size() - 1;
     }
 
+    bool reference_search = false;  // true: the reference's O(N x bins) split search
+
+    // Split search of Recurse (BVH.cpp:136-260) in O(N log N + bins log N) per
+    // axis, same result bit for bit: the left set of a candidate split is
+    // {center < split}, a prefix of the entries sorted by center, so its count
+    // is a lower_bound and its box a prefix reduction (the right set a
+    // suffix). min3/max3 keep, among equal values, the LAST entry in work order
+    // (r < v ? r : v), which only shows for -0.0 vs +0.0; the reductions below
+    // break ties on work order the same way. Costs and the strict `<` argmin run
+    // over the same (axis, split) sequence as the reference.
+    struct Ext {
+        float v;
+        uint32_t w;  // work index of the entry that supplied v
+    };
+    static Ext take_min(Ext a, Ext b) { return a.v < b.v ? a : (b.v < a.v ? b : (a.w > b.w ? a : b)); }
+    static Ext take_max(Ext a, Ext b) { return a.v > b.v ? a : (b.v > a.v ? b : (a.w > b.w ? a : b)); }
+    struct Box6 {
+        Ext lo[3], hi[3];
+    };
+    static Box6 empty_box() {
+        Box6 b;
+        for (int a = 0; a < 3; ++a) {
+            b.lo[a] = Ext{FLT_MAX, 0};
+            b.hi[a] = Ext{-FLT_MAX, 0};
+        }
+        return b;
+    }
+
+    void search_fast(const std::vector<Entry>& work, v3 bottom, v3 top, int depth, float& min_cost,
+                     float& best_split, int& best_axis) {
+        const size_t n = work.size();
+        std::vector<uint32_t> order(n);
+        std::vector<float> keys(n);
+        std::vector<Box6> pre(n), suf(n + 1);
+        for (int axis = 0; axis < 3; ++axis) {
+            const float start = axis_of(bottom, axis), stop = axis_of(top, axis);
+            if ((double)fabsf(stop - start) < 1e-4) continue;
+            const float step = (stop - start) / (1024.0f / ((float)depth + 1.0f));
+            for (size_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
+            std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+                const float ca = axis_of(work[a].center, axis), cb = axis_of(work[b].center, axis);
+                return ca < cb || (!(cb < ca) && a < b);
+            });
+            Box6 acc = empty_box();
+            for (size_t i = 0; i < n; ++i) {
+                const Entry& e = work[order[i]];
+                keys[i] = axis_of(e.center, axis);
+                for (int a = 0; a < 3; ++a) {
+                    acc.lo[a] = take_min(acc.lo[a], Ext{axis_of(e.bottom, a), order[i]});
+                    acc.hi[a] = take_max(acc.hi[a], Ext{axis_of(e.top, a), order[i]});
+                }
+                pre[i] = acc;
+            }
+            acc = empty_box();
+            suf[n] = acc;
+            for (size_t i = n; i-- > 0;) {
+                const Entry& e = work[order[i]];
+                for (int a = 0; a < 3; ++a) {
+                    acc.lo[a] = take_min(acc.lo[a], Ext{axis_of(e.bottom, a), order[i]});
+                    acc.hi[a] = take_max(acc.hi[a], Ext{axis_of(e.top, a), order[i]});
+                }
+                suf[i] = acc;
+            }
+            for (float split = start + step; split < stop - step; split += step) {
+                const size_t nl = (size_t)(std::lower_bound(keys.begin(), keys.begin() + n, split) -
+                                           keys.begin());
+                const size_t nr = n - nl;
+                if (nl <= 1 || nr <= 1) continue;
+                const Box6& L = pre[nl - 1];
+                const Box6& R = suf[nl];
+                const float l1 = L.hi[0].v - L.lo[0].v, l2 = L.hi[1].v - L.lo[1].v, l3 = L.hi[2].v - L.lo[2].v;
+                const float r1 = R.hi[0].v - R.lo[0].v, r2 = R.hi[1].v - R.lo[1].v, r3 = R.hi[2].v - R.lo[2].v;
+                const float sl = l1 * l2 + l2 * l3 + l3 * l1;
+                const float sr = r1 * r2 + r2 * r3 + r3 * r1;
+                const float cost = sl * (float)(int)nl + sr * (float)(int)nr;
+                if (cost < min_cost) {
+                    min_cost = cost;
+                    best_split = split;
+                    best_axis = axis;
+                }
+            }
+        }
+    }
+
     // Recurse (BVH.cpp:94-333).
     int recurse(std::vector<Entry>& work, int depth) {
         if (work.size() < 4) return make_leaf(work);
@@ -59,7 +144,8 @@ struct Builder {
         float best_split = FLT_MAX;
         int best_axis = -1;
 
-        for (int axis = 0; axis < 3; ++axis) {
+        if (!reference_search) search_fast(work, bottom, top, depth, min_cost, best_split, best_axis);
+        for (int axis = 0; reference_search && axis < 3; ++axis) {
             const float start = axis_of(bottom, axis), stop = axis_of(top, axis);
             // fabsf(stop - start) < 1e-4 compares in double (BVH.cpp:164).
             if ((double)fabsf(stop - start) < 1e-4) continue;
@@ -239,6 +325,8 @@ void build_cf_bvh_boxes(const std::vector<v3>& bottoms, const std::vector<v3>& t
         work.push_back(b);
     }
     Builder B;
+    // test knob: the reference's own O(N x bins) search (tests/test_bvh.py compares both)
+    B.reference_search = getenv("RTMI_BVH_REFERENCE_SEARCH") != nullptr;
     B.pool.reserve(nt);
     const int root = B.recurse(work, 0);
     B.pool[root].bottom = bottom;
