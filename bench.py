@@ -286,6 +286,9 @@ def main():
                 "traffic": traffic,
                 "kernel_ms": round(kmean, 4),
                 "algorithmic_bytes_per_launch": int(alg_bytes),
+                "note": ("achieved = record bytes the traversal reads (SURVEY §8d) / kernel time; the "
+                         "scene is cache-resident, so frac can pass 1 - traffic is the L2-miss "
+                         "bytes from rocprofv3 FETCH_SIZE/WRITE_SIZE (profiles/pmc_traffic.json)"),
             },
             "cpu_baseline": cpu,
         }

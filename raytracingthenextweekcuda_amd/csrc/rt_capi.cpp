@@ -7,6 +7,7 @@
 
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -36,6 +37,10 @@ struct rt_ctx {
     size_t d_out_bytes = 0;
     uint8_t* d_u8 = nullptr;  // staging buffer for rt_render_u8
     size_t d_u8_bytes = 0;
+    int n_cu = 0;                 // compute units (persistent work-queue grid)
+    uint32_t* d_queue = nullptr;  // work-queue head
+    float* d_partial = nullptr;   // work-queue partial sums
+    size_t d_partial_bytes = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool have_events = false;
     rt_render_stats last{};
@@ -143,6 +148,11 @@ rt_status rt_create(int32_t device, rt_ctx** out) {
             return RT_ERR_HIP;
         }
         c->have_events = true;
+        if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+            hipMalloc(&c->d_queue, 8 * 32 * sizeof(uint32_t)) != hipSuccess) {
+            rt_destroy(c);
+            return RT_ERR_HIP;
+        }
     }
     *out = c;
     return RT_OK;
@@ -157,6 +167,8 @@ void rt_destroy(rt_ctx* c) {
         (void)hipFree(c->d_counters);
         (void)hipFree(c->d_out);
         (void)hipFree(c->d_u8);
+        (void)hipFree(c->d_queue);
+        (void)hipFree(c->d_partial);
         if (c->have_events) {
             (void)hipEventDestroy(c->ev0);
             (void)hipEventDestroy(c->ev1);
@@ -561,18 +573,48 @@ static rt_status validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch
     const int32_t s = p->lanes_per_pixel;
     if (s < 0 || s > 64 || (s & (s - 1)) != 0)
         return fail(c, RT_ERR_INVALID, "lanes_per_pixel must be 0 (auto) or a power of two <= 64");
-    rt::choose_layout(L, s);
+    const char* qenv = getenv("RTMI_QUEUE");
+    const bool queue = !(qenv && qenv[0] == '0');  // RTMI_QUEUE=0: static grid (A/B only)
+    rt::choose_layout(L, s, queue);
     L.accumulate = 0;
     L.accum_scale = 0.0f;
     L.u8 = nullptr;
+    L.queue = 0;
+    L.tiles_x = (p->width + 7) / 8;
+    L.n_items = 0;
+    L.q_counter = c->d_queue;
+    L.partial = nullptr;
     L.pt_has_mesh = c->pt_tris > 0 ? 1 : 0;
     L.pt_scale = c->pt_scale;
     return RT_OK;
 }
 
-static rt_status launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaunch& L, float* out,
+static rt_status launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaunch& L0, float* out,
                         hipStream_t st) {
     RT_HIP(c, hipSetDevice(c->device));
+    rt::RenderLaunch L = L0;
+    // Work-queue mode (rt_kernel.h): persistent grid + partial sums, bit-identical
+    // to the static layout with the same lanes_per_pixel. RTMI_QUEUE=0 selects the
+    // static grid (A/B measurements only).
+    const char* qenv = getenv("RTMI_QUEUE");
+    if (!(qenv && qenv[0] == '0') && L.local_rows > 0) {
+        const uint64_t tiles = (uint64_t)L.tiles_x * (uint64_t)((L.local_rows + 7) / 8);
+        const uint64_t items = tiles * 64u * (uint64_t)L.lanes_per_pixel;
+        const size_t bytes = (size_t)items * 3 * sizeof(float);
+        if (items < 0xFFFFFFFFull && bytes <= ((size_t)1 << 30)) {
+            if (bytes > c->d_partial_bytes) {
+                (void)hipFree(c->d_partial);
+                c->d_partial = nullptr;
+                c->d_partial_bytes = 0;
+                RT_HIP(c, hipMalloc(&c->d_partial, bytes));
+                c->d_partial_bytes = bytes;
+            }
+            L.queue = rt::queue_blocks(c->n_cu);
+            L.n_items = (uint32_t)items;
+            L.partial = c->d_partial;
+            RT_HIP(c, hipMemsetAsync(c->d_queue, 0, 8 * 32 * sizeof(uint32_t), st));
+        }
+    }
     const bool keep = (p->flags & RT_RENDER_KEEP_COUNTERS) != 0;
     if (!keep) RT_HIP(c, hipMemsetAsync(c->d_counters, 0, rt::kNumCounters * sizeof(unsigned long long), st));
     RT_HIP(c, hipEventRecord(c->ev0, st));

@@ -25,22 +25,34 @@ struct RenderLaunch {
     int32_t accumulate;
     float accum_scale;
     uint8_t* u8;
+    // Work-queue mode (queue = 1): a persistent grid whose lanes take items
+    // (pixel, sub-stream c) from a global counter; each item's sample sum goes
+    // to partial[item] and a combine pass sums the S partials of a pixel in
+    // the fixed order of the static layout. Items are numbered in 8x8 pixel
+    // tiles (tiles_x per tile row), S per pixel.
+    int32_t queue;
+    int32_t tiles_x;
+    uint32_t n_items;
+    uint32_t* q_counter;
+    float* partial;
 };
 
 // Lane-layout choice: S = lanes_per_pixel (0 = auto). Adjacent lanes that
 // share a pixel trace nearly identical camera rays, so larger S means more
-// coherent waves (less divergence in BVH traversal and mesh compaction) and,
-// for small shards, more lanes to fill the chip. Auto takes the largest power
-// of two S <= min(32, spp) with pixels * S <= 2^24 lanes. Measured on one
-// MI355X (ms/frame, S = 1 -> auto): CornellBox1 11.9 -> 10.8, random spheres
-// 245 -> 164, materialball 34.5 -> 14.3, bunny 999 -> 938, media 1982 -> 2019;
-// a 1/8 CornellBox1 shard 1.56 (S = 8) -> 1.46 (S = 32).
-inline void choose_layout(RenderLaunch& L, int32_t requested) {
+// coherent waves (less divergence in BVH traversal and mesh compaction).
+// Work-queue launches (the default) take the largest power of two
+// S <= min(32, spp) with pixels * S <= 2^25 items (the partial-sum buffer stays
+// <= 400 MB); static launches the largest with pixels * S <= 2^24 lanes.
+// Measured on one MI355X, ms/frame (static S=1 -> static auto -> queue auto):
+// CornellBox1 11.9 -> 10.7 -> 8.9, random spheres 245 -> 164 -> 113,
+// materialball 34.5 -> 14.5 -> 11.7, bunny 999 -> 950 -> 765, media 1982 -> 2015 -> 1883.
+inline void choose_layout(RenderLaunch& L, int32_t requested, bool queue) {
     int32_t s = requested;
     if (s <= 0) {
         s = 1;
         const int64_t px = (int64_t)L.local_rows * L.width;
-        while (2 * s <= 32 && 2 * s <= L.spp && px * 2 * s <= (int64_t(1) << 24)) s *= 2;
+        const int64_t cap = queue ? (int64_t(1) << 25) : (int64_t(1) << 24);
+        while (2 * s <= 32 && 2 * s <= L.spp && px * 2 * s <= cap) s *= 2;
     }
     L.lanes_per_pixel = s;
     const int32_t p = 64 / s;
@@ -65,6 +77,9 @@ struct PtSceneArgs {
 
 hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec& cam, const RenderLaunch& L,
                             float* out, unsigned long long* counters, hipStream_t stream);
+
+// Workgroups of the persistent work-queue grid (n_cu x resident blocks per CU).
+int queue_blocks(int n_cu);
 
 hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLaunch& L,
                          float* out, unsigned long long* counters, hipStream_t stream);

@@ -28,6 +28,8 @@
 // bit-identical to the CPU restatement in oracle/.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "rt_bvh.h"
 #include "rt_kernel.h"
 
@@ -607,7 +609,82 @@ __device__ __forceinline__ void write_pixel(const RenderLaunch& L, float* __rest
     }
 }
 
-template <bool kBvh>
+__device__ __forceinline__ void store_partial(const RenderLaunch& L, uint32_t item, v3 sum) {
+    float* p = L.partial + (size_t)item * 3;
+    p[0] = sum.x;
+    p[1] = sum.y;
+    p[2] = sum.z;
+}
+
+// Work-queue item -> (sub-stream, local pixel); false for items past the shard edge.
+__device__ __forceinline__ bool queue_item(const RenderLaunch& L, uint32_t item, int& c, int& px,
+                                           int& lrow) {
+    const int SP = L.lanes_per_pixel;
+    c = (int)(item & (uint32_t)(SP - 1));
+    const uint32_t pl = item / (uint32_t)SP;
+    const uint32_t tile = pl >> 6, w = pl & 63u;
+    px = (int)(tile % (uint32_t)L.tiles_x) * 8 + (int)(w & 7u);
+    lrow = (int)(tile / (uint32_t)L.tiles_x) * 8 + (int)(w >> 3);
+    return px < L.width && lrow < L.local_rows;
+}
+
+// Work-queue shards: the item range is split into kQueueShards contiguous
+// chunks, each with its own head on its own 128 B line (one device word
+// saturates near 90 dequeues/us, MI355X_MICROARCH.md). A wave starts on
+// shard blockIdx % kQueueShards and moves on when its shard runs dry.
+constexpr int kQueueShards = 8;
+constexpr int kQueueStride = 32;  // u32 words between heads
+#ifndef RT_QUEUE_REFILL
+#define RT_QUEUE_REFILL 4  // idle lanes that trigger a refill (or all lanes idle); measured 1/2/4/8/16/32
+#endif
+
+// Wave-wide dequeue from shard `sh`: every lane in `need` gets an item index,
+// or ~0u if the shard ran out (one atomic per wave).
+__device__ __forceinline__ uint32_t queue_take(const RenderLaunch& L, int sh, uint64_t need, int lane) {
+    const uint32_t lo = (uint32_t)(((uint64_t)L.n_items * (uint64_t)sh) / kQueueShards);
+    const uint32_t hi = (uint32_t)(((uint64_t)L.n_items * (uint64_t)(sh + 1)) / kQueueShards);
+    const int first = __builtin_ctzll(need);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(L.q_counter + sh * kQueueStride, (unsigned)__popcll(need));
+    base = (uint32_t)__shfl((int)base, first, 64);
+    const uint32_t it = lo + base + (uint32_t)lane_rank(need);
+    return it < hi ? it : ~0u;
+}
+
+// Refill of a wave's idle lanes (wave-uniform: called by all 64 lanes). A lane
+// that wants work and gets an item calls start(item); `exhausted` is set once
+// every shard ran dry.
+template <typename Start>
+__device__ __forceinline__ void queue_refill(const RenderLaunch& L, int lane, bool alive, bool& exhausted,
+                                             int& shard, int& tried, Start&& start) {
+    const bool want = !alive && !exhausted;
+    const uint64_t need = __ballot(want);
+    if (need && (__popcll(need) >= RT_QUEUE_REFILL || __ballot(alive) == 0)) {
+        const uint32_t it = queue_take(L, shard, need, lane);
+        if (__ballot(want && it == ~0u)) {  // this shard ran dry: move on
+            ++tried;
+            shard = (shard + 1) % kQueueShards;
+            if (tried >= kQueueShards) exhausted = true;
+        }
+        if (want && it != ~0u) start(it);
+    }
+}
+
+// Queue mode's second pass: the S partial sums of each pixel in the fixed
+// order ((p0 + p1) + p2) + ... (the static layout's shuffle order), then the
+// pixel write (mean, accumulate, u8) of write_pixel.
+__global__ __launch_bounds__(256) void combine_kernel(RenderLaunch L, float* __restrict__ out) {
+    const uint32_t pl = blockIdx.x * 256u + threadIdx.x;
+    const int SP = L.lanes_per_pixel;
+    int c, px, lrow;
+    if (pl * (uint32_t)SP >= L.n_items || !queue_item(L, pl * (uint32_t)SP, c, px, lrow)) return;
+    const float* p = L.partial + (size_t)pl * (size_t)SP * 3;
+    v3 acc{p[0], p[1], p[2]};
+    for (int j = 1; j < SP; ++j) acc = add(acc, v3{p[3 * j], p[3 * j + 1], p[3 * j + 2]});
+    write_pixel(L, out, ((size_t)lrow * (size_t)L.width + (size_t)px) * 3, acc, (float)L.spp);
+}
+
+template <bool kBvh, bool kQueue>
 __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
     const MatRec* __restrict__ mats, const BvhNode* __restrict__ nodes,
@@ -626,16 +703,22 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     // its samples (sub-lane c takes samples c, c+SP, c+2SP, ...). A wave covers
     // 64/SP pixels as a tw x th tile; a 4-wave workgroup covers 2tw x 2th.
     const int SP = L.lanes_per_pixel;
-    const int c = lane & (SP - 1);
+    int c = lane & (SP - 1);
     const int pix = lane / SP;
     const int tw = L.tile_w, th = L.tile_h;
-    const int px = blockIdx.x * (2 * tw) + (wave & 1) * tw + (pix % tw);
-    const int lrow = blockIdx.y * (2 * th) + (wave >> 1) * th + (pix / tw);
+    int px = blockIdx.x * (2 * tw) + (wave & 1) * tw + (pix % tw);
+    int lrow = blockIdx.y * (2 * th) + (wave >> 1) * th + (pix / tw);
     // Row tiling: local row -> global row (y = 0 is the bottom row).
-    const int lb = lrow / L.row_block;
-    const int y = (lb * L.row_world + L.row_rank) * L.row_block + (lrow - lb * L.row_block);
-    const bool valid = (px < L.width) && (lrow < L.local_rows) && (y < L.height);
-    const uint32_t pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
+    auto global_row = [&](int lr) {
+        const int lb = lr / L.row_block;
+        return (lb * L.row_world + L.row_rank) * L.row_block + (lr - lb * L.row_block);
+    };
+    int y = global_row(lrow);
+    bool valid = !kQueue && (px < L.width) && (lrow < L.local_rows) && (y < L.height);
+    uint32_t pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
+    uint32_t item = 0;
+    bool exhausted = false;
+    int shard = (int)(blockIdx.x % kQueueShards), shards_tried = 0;  // wave-uniform
 
     v3 sum{0.0f, 0.0f, 0.0f};
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
@@ -652,7 +735,20 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     uint64_t tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
     for (;;) {
-        if (__ballot(alive) == 0) break;  // wave-uniform exit
+        if (kQueue) {
+            // lanes without work take the next items once enough lanes are idle
+            queue_refill(L, lane, alive, exhausted, shard, shards_tried, [&](uint32_t it) {
+                if (!queue_item(L, it, c, px, lrow)) return;  // past the frame edge: ask again
+                item = it;
+                y = global_row(lrow);
+                pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
+                s = c;
+                sum = v3{0.0f, 0.0f, 0.0f};
+                alive = s < L.spp;
+                need_cam = true;
+            });
+        }
+        if (__ballot(alive || (kQueue && !exhausted)) == 0) break;  // wave-uniform exit
         RT_STAMP(t_a);
         if (alive && need_cam) {
             ray = camera_sample(cam, L, rng, pixel, px, y, s, fw, fh);
@@ -662,7 +758,10 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
             if (L.max_depth <= 0) {  // rayColor with BOUNCES = 0 returns black
                 need_cam = true;
                 s += SP;
-                if (s >= L.spp) alive = false;
+                if (s >= L.spp) {
+                    alive = false;
+                    if (kQueue) store_partial(L, item, sum);
+                }
             }
         }
         const bool live = alive && !need_cam;
@@ -778,7 +877,10 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
             sum = add(sum, contrib);
             need_cam = true;
             s += SP;
-            if (s >= L.spp) alive = false;
+            if (s >= L.spp) {
+                alive = false;
+                if (kQueue) store_partial(L, item, sum);
+            }
         }
 #ifdef RT_STAMPS
         {
@@ -789,7 +891,8 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     }
 
     // Fixed-order combination of the SP partial sums: ((p0 + p1) + p2) + ...
-    if (SP > 1) {
+    // (queue mode: combine_kernel does it from the partial buffer)
+    if (!kQueue && SP > 1) {
         const int base = lane - c;
         v3 acc = sum;
         for (int j = 1; j < SP; ++j) {
@@ -799,7 +902,7 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
         sum = acc;
     }
 
-    if (valid && c == 0) {
+    if (!kQueue && valid && c == 0) {
         const float fs = (float)L.spp;
         write_pixel(L, out, ((size_t)lrow * (size_t)L.width + (size_t)px) * 3, sum, fs);
     }
@@ -1075,7 +1178,7 @@ __device__ __forceinline__ void pt_traverse(const KTri* __restrict__ ktris,
 
 }  // namespace
 
-template <bool kDummy>
+template <bool kQueue>
 __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
     const KTri* __restrict__ ktris, const CFNode* __restrict__ nodes,
     const int32_t* __restrict__ tri_list, CamRec cam, RenderLaunch L, float* __restrict__ out,
@@ -1086,15 +1189,21 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
     uint32_t* stack = &stacks[wave][lane];
 
     const int SP = L.lanes_per_pixel;
-    const int c = lane & (SP - 1);
+    int c = lane & (SP - 1);
     const int pix = lane / SP;
     const int tw = L.tile_w, th = L.tile_h;
-    const int px = blockIdx.x * (2 * tw) + (wave & 1) * tw + (pix % tw);
-    const int lrow = blockIdx.y * (2 * th) + (wave >> 1) * th + (pix / tw);
-    const int lb = lrow / L.row_block;
-    const int y = (lb * L.row_world + L.row_rank) * L.row_block + (lrow - lb * L.row_block);
-    const bool valid = (px < L.width) && (lrow < L.local_rows) && (y < L.height);
-    const uint32_t pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
+    int px = blockIdx.x * (2 * tw) + (wave & 1) * tw + (pix % tw);
+    int lrow = blockIdx.y * (2 * th) + (wave >> 1) * th + (pix / tw);
+    auto global_row = [&](int lr) {
+        const int lb = lr / L.row_block;
+        return (lb * L.row_world + L.row_rank) * L.row_block + (lr - lb * L.row_block);
+    };
+    int y = global_row(lrow);
+    const bool valid = !kQueue && (px < L.width) && (lrow < L.local_rows) && (y < L.height);
+    uint32_t pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
+    uint32_t item = 0;
+    bool exhausted = false;
+    int shard = (int)(blockIdx.x % kQueueShards), shards_tried = 0;  // wave-uniform
 
     v3 sum{0.0f, 0.0f, 0.0f};
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
@@ -1110,7 +1219,19 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
     const bool has_mesh = L.pt_has_mesh != 0;
 
     for (;;) {
-        if (__ballot(alive) == 0) break;
+        if (kQueue) {
+            queue_refill(L, lane, alive, exhausted, shard, shards_tried, [&](uint32_t it) {
+                if (!queue_item(L, it, c, px, lrow)) return;  // past the frame edge: ask again
+                item = it;
+                y = global_row(lrow);
+                pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
+                s = c;
+                sum = v3{0.0f, 0.0f, 0.0f};
+                alive = s < L.spp;
+                need_cam = true;
+            });
+        }
+        if (__ballot(alive || (kQueue && !exhausted)) == 0) break;
         if (alive && need_cam) {
             const Ray r = camera_sample(cam, L, rng, pixel, px, y, s, fw, fh);
             o = r.o;
@@ -1282,11 +1403,14 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
             sum = add(sum, contrib);
             need_cam = true;
             s += SP;
-            if (s >= L.spp) alive = false;
+            if (s >= L.spp) {
+                alive = false;
+                if (kQueue) store_partial(L, item, sum);
+            }
         }
     }
 
-    if (SP > 1) {
+    if (!kQueue && SP > 1) {
         const int base = lane - c;
         v3 acc = sum;
         for (int j = 1; j < SP; ++j) {
@@ -1295,7 +1419,7 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
         }
         sum = acc;
     }
-    if (valid && c == 0) {
+    if (!kQueue && valid && c == 0) {
         const float fs = (float)L.spp;
         write_pixel(L, out, ((size_t)lrow * (size_t)L.width + (size_t)px) * 3, sum, fs);
     }
@@ -1314,25 +1438,54 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
 hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec& cam, const RenderLaunch& L,
                             float* out, unsigned long long* counters, hipStream_t stream) {
     dim3 block(64 * kWavesPerBlock);
+    if (L.queue) {
+        if (L.n_items == 0) return hipSuccess;
+        const uint32_t waves = (L.n_items + 63u) / 64u;
+        const uint32_t blocks = std::min<uint32_t>((waves + kWavesPerBlock - 1) / kWavesPerBlock,
+                                                   (uint32_t)L.queue);
+        hipLaunchKernelGGL(pathtrace_kernel<true>, dim3(blocks), block, 0, stream, sc.ktris, sc.nodes,
+                           sc.tri_list, cam, L, out, counters);
+        const uint32_t pixels = L.n_items / (uint32_t)L.lanes_per_pixel;
+        hipLaunchKernelGGL(combine_kernel, dim3((pixels + 255u) / 256u), dim3(256), 0, stream, L, out);
+        return hipGetLastError();
+    }
     dim3 grid((L.width + 2 * L.tile_w - 1) / (2 * L.tile_w),
               (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-    hipLaunchKernelGGL(pathtrace_kernel<true>, grid, block, 0, stream, sc.ktris, sc.nodes,
+    hipLaunchKernelGGL(pathtrace_kernel<false>, grid, block, 0, stream, sc.ktris, sc.nodes,
                        sc.tri_list, cam, L, out, counters);
     return hipGetLastError();
 }
 
+int queue_blocks(int n_cu) { return n_cu * 4; }  // 4 waves/SIMD x 4 SIMDs / 4-wave blocks
+
 hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLaunch& L, float* out,
                          unsigned long long* counters, hipStream_t stream) {
     dim3 block(64 * kWavesPerBlock);
+    if (L.queue) {
+        if (L.n_items == 0) return hipSuccess;
+        const uint32_t lanes_needed = (L.n_items + 63u) / 64u;  // waves
+        const uint32_t blocks = std::min<uint32_t>((lanes_needed + kWavesPerBlock - 1) / kWavesPerBlock,
+                                                   (uint32_t)L.queue);
+        dim3 grid(blocks, 1);
+        if (sc.has_bvh)
+            hipLaunchKernelGGL((render_kernel<true, true>), grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
+                               sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
+        else
+            hipLaunchKernelGGL((render_kernel<false, true>), grid, block, 0, stream, sc.objs, sc.tris,
+                               sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
+        const uint32_t pixels = L.n_items / (uint32_t)L.lanes_per_pixel;
+        hipLaunchKernelGGL(combine_kernel, dim3((pixels + 255u) / 256u), dim3(256), 0, stream, L, out);
+        return hipGetLastError();
+    }
     dim3 grid((L.width + 2 * L.tile_w - 1) / (2 * L.tile_w),
               (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
     if (sc.has_bvh)
-        hipLaunchKernelGGL(render_kernel<true>, grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
+        hipLaunchKernelGGL((render_kernel<true, false>), grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
                            sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
     else
-        hipLaunchKernelGGL(render_kernel<false>, grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
+        hipLaunchKernelGGL((render_kernel<false, false>), grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
                            sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
     return hipGetLastError();
 }

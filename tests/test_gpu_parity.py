@@ -171,7 +171,8 @@ def test_lanes_per_pixel_parity(rtmi, lanes):
 
 
 def test_auto_lane_layout(rtmi):
-    # largest power of two S <= min(32, spp) with pixels * S <= 2^24 (rt_kernel.h choose_layout)
+    # work-queue launches: largest power of two S <= min(32, spp) with pixels * S <= 2^25
+    # (rt_kernel.h choose_layout)
     with rtmi.Renderer(0) as r:
         rtmi.cornell_box1(r, 64, 64)
         r.render(64, 64, 32, 4, lanes_per_pixel=0)
@@ -179,7 +180,7 @@ def test_auto_lane_layout(rtmi):
         r.render(64, 64, 8, 4, lanes_per_pixel=0)
         assert r.stats()["lanes_per_pixel"] == 8
         r.render(2048, 2048, 64, 1, lanes_per_pixel=0)
-        assert r.stats()["lanes_per_pixel"] == 4
+        assert r.stats()["lanes_per_pixel"] == 8  # 4M pixels x 8 = 2^25 work items
 
 
 def test_auto_layout_within_north_star_tolerance_of_sequential_sum(rtmi):
@@ -292,3 +293,25 @@ def test_realtime_accumulation_matches_per_frame_sums():
     assert np.array_equal(acc.cpu().numpy(), want)
     scale = np.float32(1.0) / np.float32(frames)
     assert np.array_equal(pix.cpu().numpy(), orc.gamma_u8(want * scale))
+
+
+@pytest.mark.parametrize("scene", ["cornellbox1", "random_spheres", "materialball"])
+def test_work_queue_and_static_grid_agree(rtmi, scene):
+    # the persistent work-queue launch (default) and the static grid
+    # (RTMI_QUEUE=0) compute the same partial sums per (pixel, sub-stream)
+    w, h, spp, lanes = 40, 24, 8, 4
+    imgs = []
+    for mode in ("1", "0"):
+        os.environ["RTMI_QUEUE"] = mode
+        try:
+            with rtmi.Renderer(0) as r:
+                if scene == "materialball":
+                    rtmi.materialball(r, w, h)
+                    imgs.append(r.render(w, h, spp, 5, lanes_per_pixel=lanes, integrator="pathTrace"))
+                else:
+                    getattr(rtmi, scene if scene != "cornellbox1" else "cornell_box1")(r, w, h)
+                    imgs.append(r.render(w, h, spp, 6, lanes_per_pixel=lanes, row_block=4, row_rank=1,
+                                         row_world=3))
+        finally:
+            del os.environ["RTMI_QUEUE"]
+    assert np.array_equal(imgs[0], imgs[1])
