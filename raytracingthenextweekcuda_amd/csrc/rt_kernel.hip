@@ -609,8 +609,11 @@ __device__ __forceinline__ void write_pixel(const RenderLaunch& L, float* __rest
     }
 }
 
+// Partial sums are stored sub-stream major, [c][pixel][3], so the combine pass
+// reads them coalesced.
 __device__ __forceinline__ void store_partial(const RenderLaunch& L, uint32_t item, v3 sum) {
-    float* p = L.partial + (size_t)item * 3;
+    const uint32_t S = (uint32_t)L.lanes_per_pixel, npix = L.n_items / S;
+    float* p = L.partial + ((size_t)(item & (S - 1)) * npix + item / S) * 3;
     p[0] = sum.x;
     p[1] = sum.y;
     p[2] = sum.z;
@@ -678,9 +681,13 @@ __global__ __launch_bounds__(256) void combine_kernel(RenderLaunch L, float* __r
     const int SP = L.lanes_per_pixel;
     int c, px, lrow;
     if (pl * (uint32_t)SP >= L.n_items || !queue_item(L, pl * (uint32_t)SP, c, px, lrow)) return;
-    const float* p = L.partial + (size_t)pl * (size_t)SP * 3;
+    const size_t stride = (size_t)(L.n_items / (uint32_t)SP) * 3;  // one sub-stream plane
+    const float* p = L.partial + (size_t)pl * 3;
     v3 acc{p[0], p[1], p[2]};
-    for (int j = 1; j < SP; ++j) acc = add(acc, v3{p[3 * j], p[3 * j + 1], p[3 * j + 2]});
+    for (int j = 1; j < SP; ++j) {
+        p += stride;
+        acc = add(acc, v3{p[0], p[1], p[2]});
+    }
     write_pixel(L, out, ((size_t)lrow * (size_t)L.width + (size_t)px) * 3, acc, (float)L.spp);
 }
 
