@@ -13,7 +13,9 @@ r = rtmi.Renderer(0)
 rtmi.cornell_box1(r, W, H)
 out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
 stream = torch.cuda.current_stream().cuda_stream
-for world, lanes in [(1, 0), (2, 0), (4, 0), (8, 0), (8, 16), (8, 32)]:
+import sys as _s
+combos = [tuple(int(v) for v in a.split(",")) for a in _s.argv[1:]] or [(1, 0), (2, 0), (4, 0), (8, 0)]
+for world, lanes in combos:
     p = r.params(W, H, 128, 8, 1984, 0, 8, 0, world, lanes)
     best = 1e9
     for _ in range(3):
