@@ -12,6 +12,8 @@
  * failure on a context is rt_last_error(ctx). The library never calls exit()
  * (replaces gpuErrorCheck -> cudaDeviceReset -> exit, Utils.h:125-133).
  * Threading: one rt_ctx per HIP device; calls on one ctx are not thread-safe.
+ * Launches on one ctx run in issue order even across streams (each waits for
+ * the previous one: they share the context's work queue and counters).
  */
 #ifndef RTMI_H_
 #define RTMI_H_

@@ -45,6 +45,7 @@ struct rt_ctx {
     bool have_events = false;
     rt_render_stats last{};
     bool stats_pending = false;
+    bool launched = false;
 
     // pathTrace scene (prepareCUDAscene): raw loaded PLY data + device tables
     rt::PlyMesh pt_raw;
@@ -592,6 +593,10 @@ static rt_status validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch
 static rt_status launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaunch& L0, float* out,
                         hipStream_t st) {
     RT_HIP(c, hipSetDevice(c->device));
+    // The context's work queue, partial sums and counters are reused by every
+    // launch: a launch on another stream waits for the previous one.
+    if (c->launched) RT_HIP(c, hipStreamWaitEvent(st, c->ev1, 0));
+    c->launched = true;
     rt::RenderLaunch L = L0;
     // Work-queue mode (rt_kernel.h): persistent grid + partial sums, bit-identical
     // to the static layout with the same lanes_per_pixel. RTMI_QUEUE=0 selects the
