@@ -315,3 +315,23 @@ def test_work_queue_and_static_grid_agree(rtmi, scene):
         finally:
             del os.environ["RTMI_QUEUE"]
     assert np.array_equal(imgs[0], imgs[1])
+
+
+def test_launches_on_two_streams_do_not_race(rtmi):
+    # one context, two streams: the second launch waits for the first (they share
+    # the context's work queue and partial-sum buffer)
+    import torch
+
+    w, h = 64, 48
+    with rtmi.Renderer(0) as r:
+        rtmi.cornell_box1(r, w, h)
+        want_a = r.render(w, h, 16, 6, seed=1)
+        want_b = r.render(w, h, 16, 6, seed=2)
+        a = torch.empty((h, w, 3), dtype=torch.float32, device="cuda")
+        b = torch.empty_like(a)
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        r.render_device(r.params(w, h, 16, 6, 1), a.data_ptr(), s1.cuda_stream)
+        r.render_device(r.params(w, h, 16, 6, 2), b.data_ptr(), s2.cuda_stream)
+        torch.cuda.synchronize()
+    assert np.array_equal(a.cpu().numpy(), want_a)
+    assert np.array_equal(b.cpu().numpy(), want_b)
