@@ -9,6 +9,7 @@ import torch  # noqa: E402,F401
 import raytracingthenextweekcuda_amd as rtmi  # noqa: E402
 
 W = H = 512
+SPP = int(os.environ.get("SPP", "128"))
 r = rtmi.Renderer(0)
 rtmi.cornell_box1(r, W, H)
 out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
@@ -16,9 +17,9 @@ stream = torch.cuda.current_stream().cuda_stream
 import sys as _s
 combos = [tuple(int(v) for v in a.split(",")) for a in _s.argv[1:]] or [(1, 0), (2, 0), (4, 0), (8, 0)]
 for world, lanes in combos:
-    p = r.params(W, H, 128, 8, 1984, 0, 8, 0, world, lanes)
+    p = r.params(W, H, SPP, 8, 1984, 0, 8, 0, world, lanes)
     best = 1e9
     for _ in range(3):
         r.render_device(p, out.data_ptr(), stream)
         best = min(best, r.stats()["kernel_ms"])
-    print(f"world {world} S {lanes}->{r.stats()['lanes_per_pixel']} kernel_ms {best:.3f}", flush=True)
+    print(f"spp {SPP} world {world} S {lanes}->{r.stats()['lanes_per_pixel']} kernel_ms {best:.3f}", flush=True)
