@@ -201,6 +201,15 @@ rt_status rt_render(rt_ctx* ctx, const rt_render_params* params, float* out_rgb_
 rt_status rt_render_device(rt_ctx* ctx, const rt_render_params* params, float* out_rgb_device,
                            void* hip_stream);
 rt_status rt_sync_stats(rt_ctx* ctx, rt_render_stats* out);
+/* Single-process multi-device frame: ctxs[k] renders the row tiles of
+ * rank k of n (params->row_block; row_rank / row_world are set per context) on its
+ * own device, every launch is issued before any is awaited, and the tiles are
+ * copied back and de-interleaved into out_rgb_host (height x width x 3 floats).
+ * Each context needs the same committed scene and camera. The scaling path is one
+ * process per GPU with an RCCL gather (raytracingthenextweekcuda_amd/distributed.py);
+ * this is the C-only convenience for one host process. */
+rt_status rt_render_multi(rt_ctx* const* ctxs, int32_t n, const rt_render_params* params,
+                          float* out_rgb_host);
 /* renderKernel's offline output (Canvas::writePixel(index, color / spp), Canvas.h:58-71):
  * gamma-corrected uint8 RGB of the owned rows, computed on the device. */
 rt_status rt_render_u8(rt_ctx* ctx, const rt_render_params* params, uint8_t* out_rgb8_host);

@@ -10,6 +10,7 @@ from .renderer import (  # noqa: F401
     Camera, MaterialHandle, Renderer, createCube, createDieletricMaterial,
     createEmissionMaterial, createLambertianMaterial, createMesh, createMetalMaterial,
     createMovingSphere, createPlane, createSphere, gamma_u8, owned_row_ids, owned_rows,
+    render_multi,
 )
 from .scene import (  # noqa: F401
     bunny_cornell_box, cornell_box1, cornell_box_media, load_json_scene, load_yaml_scene, materialball, random_spheres,

@@ -34,7 +34,7 @@ EXPORTS = [
     "rt_mesh_ply", "rt_ply_bvh_image", "rt_load_object", "rt_process_triangle_data",
     "rt_pathtrace_bvh_image",
     "rt_camera", "rt_commit", "rt_scene_info", "rt_render", "rt_render_device", "rt_sync_stats",
-    "rt_render_u8", "rt_accumulate", "rt_gamma_u8",
+    "rt_render_u8", "rt_accumulate", "rt_render_multi", "rt_gamma_u8",
 ]
 
 
@@ -123,6 +123,7 @@ def lib():
     L.rt_render.argtypes = [vp, C.POINTER(RenderParams), fp]
     L.rt_render_device.argtypes = [vp, C.POINTER(RenderParams), vp, vp]
     L.rt_sync_stats.argtypes = [vp, C.POINTER(RenderStats)]
+    L.rt_render_multi.argtypes = [C.POINTER(vp), i32, C.POINTER(RenderParams), fp]
     L.rt_render_u8.argtypes = [vp, C.POINTER(RenderParams), C.POINTER(C.c_uint8)]
     L.rt_accumulate.argtypes = [vp, C.POINTER(RenderParams), vp, C.c_uint32, vp, vp]
     L.rt_gamma_u8.argtypes = [fp, C.c_int64, C.POINTER(C.c_uint8)]

@@ -713,6 +713,52 @@ rt_status rt_render(rt_ctx* c, const rt_render_params* p, float* out_host) {
     return RT_OK;
 }
 
+rt_status rt_render_multi(rt_ctx* const* ctxs, int32_t n, const rt_render_params* p, float* out_host) {
+    if (!ctxs || n < 1 || !p || !out_host) return RT_ERR_INVALID;
+    for (int32_t k = 0; k < n; ++k)
+        if (!ctxs[k]) return RT_ERR_INVALID;
+    // launch every device's row tiles first (asynchronous), then collect
+    std::vector<rt_render_params> pk((size_t)n, *p);
+    for (int32_t k = 0; k < n; ++k) {
+        rt_ctx* c = ctxs[k];
+        pk[k].row_rank = k;
+        pk[k].row_world = n;
+        rt::RenderLaunch L;
+        rt_status s = validate(c, &pk[k], L);
+        if (s != RT_OK) return s;
+        const size_t bytes = (size_t)L.local_rows * L.width * 3 * sizeof(float);
+        RT_HIP(c, hipSetDevice(c->device));
+        if (bytes > c->d_out_bytes) {
+            (void)hipFree(c->d_out);
+            c->d_out = nullptr;
+            c->d_out_bytes = 0;
+            RT_HIP(c, hipMalloc(&c->d_out, bytes));
+            c->d_out_bytes = bytes;
+        }
+        s = launch(c, &pk[k], L, c->d_out, nullptr);
+        if (s != RT_OK) return s;
+    }
+    std::vector<float> tile;
+    const int32_t W = p->width, rb = p->row_block;
+    for (int32_t k = 0; k < n; ++k) {
+        rt_ctx* c = ctxs[k];
+        const int32_t rows = rt::owned_rows(p->height, rb, k, n);
+        RT_HIP(c, hipSetDevice(c->device));
+        RT_HIP(c, hipStreamSynchronize(nullptr));
+        tile.resize((size_t)rows * W * 3);
+        if (rows) RT_HIP(c, hipMemcpy(tile.data(), c->d_out, tile.size() * sizeof(float), hipMemcpyDeviceToHost));
+        for (int32_t j = 0; j < rows; ++j) {  // local row j of rank k -> global row y
+            const int32_t lb = j / rb;
+            const int32_t y = (lb * n + k) * rb + (j - lb * rb);
+            memcpy(out_host + (size_t)y * W * 3, tile.data() + (size_t)j * W * 3, (size_t)W * 3 * sizeof(float));
+        }
+        rt_status s = rt_sync_stats(c, nullptr);
+        if (s != RT_OK) return s;
+        if (c->last.overflow) return fail(c, RT_ERR_OVERFLOW, "BVH traversal stack overflow");
+    }
+    return RT_OK;
+}
+
 rt_status rt_render_u8(rt_ctx* c, const rt_render_params* p, uint8_t* out_host) {
     if (!c) return RT_ERR_INVALID;
     rt::RenderLaunch L;

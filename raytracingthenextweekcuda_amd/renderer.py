@@ -291,6 +291,21 @@ def _integrator(i) -> int:
     return int(i)
 
 
+def render_multi(renderers, width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=8,
+                 lanes_per_pixel=0, integrator="rayColor") -> np.ndarray:
+    """rt_render_multi: one host process renders a frame over several contexts
+    (devices), renderer k taking the row tiles of rank k; returns (H, W, 3)."""
+    L = lib()
+    p = Renderer.params(width, height, spp, max_depth, seed, sample_offset, row_block, 0, 1,
+                        lanes_per_pixel, integrator)
+    arr = (C.c_void_p * len(renderers))(*[r.ctx for r in renderers])
+    out = np.zeros((height, width, 3), np.float32)
+    st = L.rt_render_multi(arr, len(renderers), C.byref(p), out.ctypes.data_as(C.POINTER(C.c_float)))
+    if st != 0:
+        raise RTError(st, L.rt_last_error(renderers[0].ctx).decode())
+    return out
+
+
 def owned_rows(height, block, rank, world) -> int:
     n, b = 0, rank
     while b * block < height:

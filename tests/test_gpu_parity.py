@@ -335,3 +335,19 @@ def test_launches_on_two_streams_do_not_race(rtmi):
         torch.cuda.synchronize()
     assert np.array_equal(a.cpu().numpy(), want_a)
     assert np.array_equal(b.cpu().numpy(), want_b)
+
+
+def test_render_multi_assembles_the_frame(rtmi):
+    # rt_render_multi over 3 contexts (all on device 0 here): row tiles rendered per
+    # context, copied back and de-interleaved == the one-context frame
+    w, h = 40, 37
+    rs = [rtmi.Renderer(0) for _ in range(3)]
+    for r in rs:
+        rtmi.cornell_box1(r, w, h)
+    try:
+        multi = rtmi.render_multi(rs, w, h, 8, 5, row_block=4, lanes_per_pixel=4)
+        one = rs[0].render(w, h, 8, 5, lanes_per_pixel=4)
+    finally:
+        for r in rs:
+            r.close()
+    assert np.array_equal(multi, one)
