@@ -89,46 +89,59 @@ def object_bytes_per_segment(r) -> int:
 
 def cpu_baseline(args, threads: int):
     """The CPU restatement (oracle/, a port of the reference's integrator) on a
-    bounded sample of the same workload: full frame at --cpu-spp spp."""
+    bounded sample of the same workload: the median of 3 runs on `threads`
+    threads, plus one single-thread run on 1/8 of the sample's samples."""
     from oracle import oracle as orc
 
     scenes = os.path.join(REPO, "assets", "scenes")
+    models = os.path.join(REPO, "assets", "models")
     w, h = args.width // args.cpu_div, args.height // args.cpu_div
     if args.scene == "materialball":
         # pathTrace: the restatement traverses the reference's own `.bvh` cache
         # (tests/golden) as BVH_IntersectTriangles does (full DFS, no pruning).
-        cam = orc.yaml_scene(os.path.join(scenes, "cornellbox2.yaml"), os.path.join(REPO, "assets", "models"), w, h)
+        cam = orc.yaml_scene(os.path.join(scenes, "cornellbox2.yaml"), models, w, h)
         pt = orc.OraclePathTrace()
-        pt.load_object(os.path.join(REPO, "assets", "models", "materialball", "materialball.ply"), "COAT")
+        pt.load_object(os.path.join(models, "materialball", "materialball.ply"), "COAT")
         pt.process((0.1, 0.0, -1.0))
         with open(os.path.join(REPO, "tests", "golden", "bvh", "materialball.ply.bvh"), "rb") as fh:
             pt.set_bvh(fh.read())
-        pt.render(cam, 16, 16, 1, args.depth, threads=threads)  # warm-up
-        t0 = time.perf_counter()
-        _, st = pt.render(cam, w, h, args.cpu_spp, args.depth, threads=threads)
-        dt = time.perf_counter() - t0
-        sc = None
-    elif args.scene == "spheres":
-        sc = orc.json_scene(os.path.join(scenes, "random_spheres.json"), w, h)
+
+        def run(spp, nthreads):
+            return pt.render(cam, w, h, spp, args.depth, threads=nthreads)[1]
     else:
-        name = {"cornellbox1": "cornellbox1.yaml", "bunny": "bunny_cornellbox.yaml",
-                "media": "cornellbox_media.yaml"}[args.scene]
-        sc = orc.yaml_scene(os.path.join(scenes, name), os.path.join(REPO, "assets", "models"), w, h)
-    if sc is not None:
-        sc.render(16, 16, 1, args.depth, threads=threads)  # warm-up
+        if args.scene == "spheres":
+            sc = orc.json_scene(os.path.join(scenes, "random_spheres.json"), w, h)
+        else:
+            name = {"cornellbox1": "cornellbox1.yaml", "bunny": "bunny_cornellbox.yaml",
+                    "media": "cornellbox_media.yaml"}[args.scene]
+            sc = orc.yaml_scene(os.path.join(scenes, name), models, w, h)
+
+        def run(spp, nthreads):
+            return sc.render(w, h, spp, args.depth, threads=nthreads)[1]
+
+    run(1, threads)  # warm-up (OpenMP pool, page-in)
+    times = []
+    for _ in range(3):
         t0 = time.perf_counter()
-        _, st = sc.render(w, h, args.cpu_spp, args.depth, threads=threads)
-        dt = time.perf_counter() - t0
+        st = run(args.cpu_spp, threads)
+        times.append(time.perf_counter() - t0)
+    dt = sorted(times)[1]
+    spp1 = max(1, args.cpu_spp // 8)
+    t0 = time.perf_counter()
+    st1 = run(spp1, 1)
+    dt1 = time.perf_counter() - t0
     frame_ms = dt * 1e3 * (args.width * args.height * args.spp) / (w * h * args.cpu_spp)
     return {
         "value": st["segments"] / dt / 1e6,
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
+        "value_1thread": st1["segments"] / dt1 / 1e6,
         "sample": (f"{args.scene} {w}x{h} spp={args.cpu_spp} depth={args.depth} (same camera; "
                    f"{w * h * args.cpu_spp} of the frame's {args.width * args.height * args.spp} samples), "
-                   f"{dt:.2f} s wall, {st['segments']} segments; ms/frame extrapolated by samples: "
-                   f"{frame_ms:.0f}"),
+                   f"median of 3 on {threads} threads: {dt:.2f} s wall, {st['segments']} segments; "
+                   f"ms/frame extrapolated by samples: {frame_ms:.0f}; value_1thread: spp={spp1} on 1 thread, "
+                   f"{dt1:.2f} s"),
     }
 
 
