@@ -47,6 +47,7 @@ struct Builder {
     }
 
     bool reference_search = false;  // true: the reference's O(N x bins) split search
+    size_t leaf_min_split = 4;      // Recurse makes a leaf below 4 entries (BVH.cpp:106)
 
     // Split search of Recurse (BVH.cpp:136-260) in O(N log N + bins log N) per
     // axis, same result bit for bit: the left set of a candidate split is
@@ -132,7 +133,7 @@ struct Builder {
 
     // Recurse (BVH.cpp:94-333).
     int recurse(std::vector<Entry>& work, int depth) {
-        if (work.size() < 4) return make_leaf(work);
+        if (work.size() < leaf_min_split) return make_leaf(work);
 
         v3 bottom{FLT_MAX, FLT_MAX, FLT_MAX}, top{-FLT_MAX, -FLT_MAX, -FLT_MAX};
         for (const Entry& v : work) {
@@ -308,7 +309,8 @@ void process_ply_vertices(PlyMesh& m, v3 offset, float max_coord) {
     }
 }
 
-void build_cf_bvh_boxes(const std::vector<v3>& bottoms, const std::vector<v3>& tops, CFBvh& out) {
+void build_cf_bvh_boxes(const std::vector<v3>& bottoms, const std::vector<v3>& tops, CFBvh& out,
+                        int leaf_min_split) {
     // CreateBVH (BVH.cpp:335-392) over precomputed primitive boxes.
     const size_t nt = bottoms.size();
     std::vector<Entry> work;
@@ -325,6 +327,7 @@ void build_cf_bvh_boxes(const std::vector<v3>& bottoms, const std::vector<v3>& t
         work.push_back(b);
     }
     Builder B;
+    B.leaf_min_split = (size_t)leaf_min_split;
     // test knob: the reference's own O(N x bins) search (tests/test_bvh.py compares both)
     B.reference_search = getenv("RTMI_BVH_REFERENCE_SEARCH") != nullptr;
     B.pool.reserve(nt);
@@ -341,7 +344,7 @@ void build_cf_bvh_boxes(const std::vector<v3>& bottoms, const std::vector<v3>& t
 }
 
 void build_cf_bvh(const std::vector<v3>& vertices, const std::vector<uint32_t>& indices,
-                  CFBvh& out) {
+                  CFBvh& out, int leaf_min_split) {
     // Per-triangle boxes: min3/max3 over the three vertices from FLT_MAX seeds.
     const size_t nt = indices.size() / 3;
     std::vector<v3> lo(nt), hi(nt);
@@ -352,7 +355,7 @@ void build_cf_bvh(const std::vector<v3>& vertices, const std::vector<uint32_t>& 
         lo[j] = b;
         hi[j] = t;
     }
-    build_cf_bvh_boxes(lo, hi, out);
+    build_cf_bvh_boxes(lo, hi, out, leaf_min_split);
 }
 
 namespace {

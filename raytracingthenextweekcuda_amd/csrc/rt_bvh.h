@@ -47,11 +47,14 @@ struct CFBvh {
 };
 
 // CreateBVH + CreateCFBVH over triangles given by vertex index triples.
+// leaf_min_split = 4 is the reference's tree (byte-identical `.bvh` caches);
+// rayColor meshes, which the reference brute-forces, may use larger leaves.
 void build_cf_bvh(const std::vector<v3>& vertices, const std::vector<uint32_t>& indices,
-                  CFBvh& out);
+                  CFBvh& out, int leaf_min_split = 4);
 
 // Same builder over arbitrary primitive boxes (object-level BVH).
-void build_cf_bvh_boxes(const std::vector<v3>& bottoms, const std::vector<v3>& tops, CFBvh& out);
+void build_cf_bvh_boxes(const std::vector<v3>& bottoms, const std::vector<v3>& tops, CFBvh& out,
+                        int leaf_min_split = 4);
 
 // Kuchkuda triangle record of the pathTrace integrator, as uploaded by
 // prepareCUDAscene (main.cu:457-494) minus the unused centre: plane normal + d,

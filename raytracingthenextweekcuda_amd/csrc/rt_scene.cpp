@@ -7,6 +7,7 @@
 
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -313,7 +314,8 @@ std::string HostScene::flatten() {
                     ix[k] = (uint32_t)k;
                 }
                 CFBvh b;
-                build_cf_bvh(vs, ix, b);
+                const char* lenv = getenv("RTMI_MESH_LEAF");  // A/B only
+                build_cf_bvh(vs, ix, b, lenv ? atoi(lenv) : 4);
                 if (b.max_depth >= kBvhStackDepth)
                     return "mesh " + std::to_string(i) + ": BVH depth " + std::to_string(b.max_depth) +
                            " exceeds the traversal stack (" + std::to_string(kBvhStackDepth) + ")";
@@ -395,7 +397,8 @@ std::string HostScene::group_spheres() {
         hi[k] = h;
     }
     CFBvh b;
-    build_cf_bvh_boxes(lo, hi, b);
+    const char* lenv = getenv("RTMI_SPHERE_LEAF");  // A/B only
+    build_cf_bvh_boxes(lo, hi, b, lenv ? atoi(lenv) : 4);
     if (b.max_depth >= kBvhStackDepth)
         return "sphere BVH depth " + std::to_string(b.max_depth) + " exceeds the traversal stack";
     bvh_max_depth = std::max(bvh_max_depth, b.max_depth);
