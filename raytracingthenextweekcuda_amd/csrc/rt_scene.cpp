@@ -314,8 +314,7 @@ std::string HostScene::flatten() {
                     ix[k] = (uint32_t)k;
                 }
                 CFBvh b;
-                const char* lenv = getenv("RTMI_MESH_LEAF");  // A/B only
-                build_cf_bvh(vs, ix, b, lenv ? atoi(lenv) : 4);
+                build_cf_bvh(vs, ix, b);  // reference leaves (larger: measured slower)
                 if (b.max_depth >= kBvhStackDepth)
                     return "mesh " + std::to_string(i) + ": BVH depth " + std::to_string(b.max_depth) +
                            " exceeds the traversal stack (" + std::to_string(kBvhStackDepth) + ")";
@@ -397,8 +396,7 @@ std::string HostScene::group_spheres() {
         hi[k] = h;
     }
     CFBvh b;
-    const char* lenv = getenv("RTMI_SPHERE_LEAF");  // A/B only
-    build_cf_bvh_boxes(lo, hi, b, lenv ? atoi(lenv) : 4);
+    build_cf_bvh_boxes(lo, hi, b);
     if (b.max_depth >= kBvhStackDepth)
         return "sphere BVH depth " + std::to_string(b.max_depth) + " exceeds the traversal stack";
     bvh_max_depth = std::max(bvh_max_depth, b.max_depth);
