@@ -183,3 +183,25 @@ def test_gpu_materialball_committed_configuration():
     r.close()
     _assert_parity(got, want)
     assert np.array_equal(got, want)  # bit-identical in practice (same IEEE op order)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(8))
+def test_gpu_pathtrace_random_views(seed):
+    # random camera, bounce count, seed and sub-stream layout per case
+    rng = np.random.RandomState(100 + seed)
+    name = sorted(S.PT_SCENES)[seed % 3]
+    eye = (float(rng.uniform(-2.5, 2.5)), float(rng.uniform(-0.5, 2.0)), float(rng.uniform(1.5, 3.5)))
+    cam = (eye, (0.1, 0.0, -0.5), (0.0, 1.0, 0.0), 1.25, float(rng.uniform(25, 70)),
+           float(rng.uniform(0.0, 0.05)), 3.0, 0.0, 1.0)
+    bounces, lanes = int(rng.randint(1, 9)), [1, 2, 8][seed % 3]
+    pt, oc = S.build_pathtrace_oracle(name, cam)
+    want, ost = pt.render(oc, 30, 24, 4, bounces, seed=seed, threads=8, lanes_per_pixel=lanes)
+    r = _product(0)
+    S.build_pathtrace_product(r, name, cam)
+    got = r.render(30, 24, 4, bounces, seed=seed, lanes_per_pixel=lanes, integrator="pathTrace")
+    st = r.stats()
+    r.close()
+    _assert_parity(got, want)
+    assert np.array_equal(got, want)
+    assert st["segments"] == ost["segments"]
