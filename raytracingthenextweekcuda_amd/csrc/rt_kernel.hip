@@ -221,10 +221,13 @@ __device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, ui
     __builtin_amdgcn_wave_barrier();
     const uint32_t total = (uint32_t)__popcll(mask) * m;
     const float t0 = h.t;
+    // p / m as a multiply-high: magic = ceil(2^32 / m) is exact for p < 2^26 (p < 64 * 64
+    // here); m = 1 (2^32 does not fit) divides by itself
+    const uint32_t magic = m > 1u ? 0xFFFFFFFFu / m + 1u : 0u;
     for (uint32_t p0 = 0; p0 < total; p0 += 64) {
         const uint32_t p = p0 + (uint32_t)lane;
         const bool act = p < total;
-        const uint32_t r = act ? p / m : 0u;
+        const uint32_t r = act ? (m > 1u ? __umulhi(p, magic) : p) : 0u;
         const uint32_t k = act ? p - r * m : 0u;
         const int src = W.src[r];
         const v3 ro{__shfl(o.x, src, 64), __shfl(o.y, src, 64), __shfl(o.z, src, 64)};
