@@ -56,7 +56,8 @@ def parse():
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--depth", type=int, default=None)
-    ap.add_argument("--row-block", type=int, default=8)
+    ap.add_argument("--row-block", type=int, default=2,
+                    help="rows per round-robin block (2: per-rank shard times within 1.1%% at N=8, tools/shard_balance.py)")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per pixel (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-spp", type=int, default=None)
