@@ -37,6 +37,9 @@ SCENES = {
     "spheres": ("random_spheres", 1280, 720, 256, 10, "RTNW final scene (488 spheres, 388 moving; object BVH)"),
     "bunny": ("bunny_cornell_box", 1024, 1024, 512, 8, "bun_zipper.ply (69,451 triangles, SAH BVH) in CornellBox1 walls"),
     "media": ("cornell_box_media", 2048, 2048, 1024, 16, "CornellBox1 walls + 2 constant-medium boxes + glass sphere (media: build extension)"),
+    # the scene of the reference's only published timings (images.MD:44-53, 3,857 ms/frame on
+    # an unstated sm_61 GPU; scene inferred from the image); not a BASELINE config
+    "suzanne": ("suzanne_cornell_box", 512, 512, 32, 10, "cornellbox3.yaml (suzanne_small.obj, 968 triangles) + metal and glass spheres (images.MD published-timing scene)"),
     # the reference's committed renderKernel configuration (pathTrace, main.cu:187;
     # samplesPerPixel 32, 5 bounces); not a BASELINE config, reported separately
     "materialball": ("materialball", 512, 512, 32, 5, "materialball.ply (46,816 triangles, COAT) + 6 spheres, pathTrace integrator"),
@@ -72,7 +75,7 @@ def parse():
     # restatement scans meshes brute force like the reference's TriangleMesh::hit,
     # so the bunny sample is a 1/8-scale frame at 1 spp.
     a.cpu_div, cpu_spp = {"cornellbox1": (1, 128), "spheres": (2, 16), "bunny": (8, 1),
-                          "materialball": (1, 32), "media": (4, 64)}[a.scene]
+                          "materialball": (1, 32), "media": (4, 64), "suzanne": (2, 8)}[a.scene]
     a.cpu_spp = a.cpu_spp or cpu_spp
     return a
 
@@ -114,7 +117,7 @@ def cpu_baseline(args, threads: int):
             sc = orc.json_scene(os.path.join(scenes, "random_spheres.json"), w, h)
         else:
             name = {"cornellbox1": "cornellbox1.yaml", "bunny": "bunny_cornellbox.yaml",
-                    "media": "cornellbox_media.yaml"}[args.scene]
+                    "media": "cornellbox_media.yaml", "suzanne": "suzanne_cornellbox.yaml"}[args.scene]
             sc = orc.yaml_scene(os.path.join(scenes, name), models, w, h)
 
         def run(spp, nthreads):

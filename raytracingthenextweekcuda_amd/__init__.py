@@ -14,4 +14,5 @@ from .renderer import (  # noqa: F401
 )
 from .scene import (  # noqa: F401
     bunny_cornell_box, cornell_box1, cornell_box_media, load_json_scene, load_yaml_scene, materialball, random_spheres,
+    suzanne_cornell_box,
 )

@@ -129,6 +129,23 @@ __device__ __forceinline__ float tri_t(const TriRec& tr, v3 o, v3 d) {
     return kNo;
 }
 
+// tri_t for a pair already known to pass the backface cull.
+[[maybe_unused]] __device__ __forceinline__ float tri_t_culled(const TriRec& tr, v3 o, v3 d) {
+    const float kNo = __builtin_nanf("");
+    v3 e1{tr.e1x, tr.e1y, tr.e1z}, e2{tr.e2x, tr.e2y, tr.e2z};
+    v3 s = sub(o, v3{tr.v0x, tr.v0y, tr.v0z});
+    v3 s1 = cross(d, e2);
+    v3 s2 = cross(s, e1);
+    float coef = fdiv(1.0f, dot(s1, e1));
+    float t = coef * dot(s2, e2);
+    float b1 = coef * dot(s1, s);
+    float b2 = coef * dot(s2, d);
+    if (((t >= kFltEpsilon) && (t >= kTMin)) && (b1 >= kFltEpsilon) && (b2 >= kFltEpsilon) &&
+        ((1.0f - b1 - b2) >= kFltEpsilon))
+        return t;
+    return kNo;
+}
+
 // Closest-hit state with the reference's sequential tie rule (hit(),
 // main.cu:43-57, each object called with tMax = closestSoFar): planes and
 // triangles accept t < closestSoFar, spheres t <= closestSoFar (Sphere.cu:25).
@@ -172,9 +189,16 @@ struct Hit {
     }
 };
 
+#ifndef RT_MESH_TWO_PHASE
+#define RT_MESH_TWO_PHASE 1  // cull-filtered compaction (mesh_compact); 0 = one pass (A/B only)
+#endif
+
 struct WaveLds {
     unsigned long long key[64];  // per-ray (t bits << 32 | triangle) minima
     int32_t src[64];             // rank -> lane of the rays wanting a mesh
+#if RT_MESH_TWO_PHASE
+    uint16_t ring[128];          // pair ids that passed the backface cull, awaiting the full test
+#endif
 };
 
 struct Counters {
@@ -224,6 +248,52 @@ __device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, ui
     // p / m as a multiply-high: magic = ceil(2^32 / m) is exact for p < 2^26 (p < 64 * 64
     // here); m = 1 (2^32 does not fit) divides by itself
     const uint32_t magic = m > 1u ? 0xFFFFFFFFu / m + 1u : 0u;
+#if RT_MESH_TWO_PHASE
+    // Phase 1 runs only TriangleMesh.cu:72's backface cull over the packed pairs and
+    // queues the survivors (about half of a closed mesh's pairs) in a 128-entry LDS
+    // ring; phase 2 runs the rest of the test on full batches of 64 survivors. The
+    // accepted set, and so the atomic-min result, is that of the one-pass scan.
+    uint32_t queued = 0, tested = 0;  // wave-uniform ring positions
+    auto full_test = [&](uint32_t count) {
+        const uint32_t i = tested + (uint32_t)lane;
+        const bool act = (uint32_t)lane < count;
+        const uint32_t p = act ? (uint32_t)W.ring[i & 127u] : 0u;
+        const uint32_t r = m > 1u ? __umulhi(p, magic) : p;
+        const uint32_t k = p - r * m;
+        const int src = W.src[r];
+        const v3 ro{__shfl(o.x, src, 64), __shfl(o.y, src, 64), __shfl(o.z, src, 64)};
+        const v3 rd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
+        const float rt0 = __shfl(t0, src, 64);
+        if (act) {
+            const float t = tri_t_culled(tris[base + k], ro, rd);
+            if (t <= rt0) {
+                const unsigned long long key =
+                    ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)k;
+                atomicMin(&W.key[r], key);
+            }
+        }
+        tested += count;
+    };
+    for (uint32_t p0 = 0; p0 < total; p0 += 64) {
+        const uint32_t p = p0 + (uint32_t)lane;
+        const bool act = p < total;
+        const uint32_t r = act ? (m > 1u ? __umulhi(p, magic) : p) : 0u;
+        const uint32_t k = act ? p - r * m : 0u;
+        const int src = W.src[r];
+        const v3 rd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
+        bool keep = false;
+        if (act) {
+            const TriRec& tr = tris[base + k];
+            keep = !(dot(rd, v3{tr.nx, tr.ny, tr.nz}) > kFltEpsilon);
+        }
+        const uint64_t km = __ballot(keep);
+        if (keep) W.ring[(queued + (uint32_t)lane_rank(km)) & 127u] = (uint16_t)p;
+        queued += (uint32_t)__popcll(km);
+        __builtin_amdgcn_wave_barrier();
+        if (queued - tested >= 64u) full_test(64u);
+    }
+    if (queued > tested) full_test(queued - tested);
+#else
     for (uint32_t p0 = 0; p0 < total; p0 += 64) {
         const uint32_t p = p0 + (uint32_t)lane;
         const bool act = p < total;
@@ -242,6 +312,7 @@ __device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, ui
             }
         }
     }
+#endif
     __builtin_amdgcn_wave_barrier();
     if (want) {
         const unsigned long long key = W.key[rank];

@@ -110,6 +110,15 @@ def cornell_box_media(r: Renderer, width: int, height: int, commit: bool = True)
                            commit=commit)
 
 
+def suzanne_cornell_box(r: Renderer, width: int, height: int, commit: bool = True) -> Camera:
+    """The scene of the reference's only published timings (R/images/images.MD:44-53:
+    512x512, 32 spp, 10 bounces, 3,857 ms on an unstated sm_61 GPU), as inferred from its
+    image: cornellbox3.yaml (suzanne_small.obj, 968 triangles) + the metal and glass
+    spheres of cornellbox0.yaml (assets/scenes/suzanne_cornellbox.yaml)."""
+    return load_yaml_scene(r, os.path.join(SCENES_DIR, "suzanne_cornellbox.yaml"), width, height,
+                           commit=commit)
+
+
 def materialball(r: Renderer, width: int, height: int, commit: bool = True) -> Camera:
     """The reference's committed renderKernel configuration: pathTrace
     (main.cu:187) over materialball.ply as COAT at offset (0.1, 0, -1)

@@ -53,7 +53,8 @@ def test_cornellbox1_parity(rtmi, w, h, spp, depth):
     assert st["samples"] == w * h * spp
 
 
-@pytest.mark.parametrize("name", ["cornellbox0.yaml", "cornellbox2.yaml", "cornellbox_empty.yaml"])
+@pytest.mark.parametrize("name", ["cornellbox0.yaml", "cornellbox2.yaml", "cornellbox3.yaml", "cornellbox_empty.yaml",
+                                  "suzanne_cornellbox.yaml"])
 def test_yaml_scenes_parity(rtmi, name):
     w, h, spp, depth = 48, 48, 4, 10
     with rtmi.Renderer(0) as r:
