@@ -575,14 +575,20 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             const float den = dot(nrm, d);
             const bool proceed = ob.u1 ? (fabsf(den) > kTMin) : (den > kTMin);
             const float t = fdiv(dot(sub(v3{f[0], f[1], f[2]}, o), nrm), den);
-            const v3 p = add(o, scale(d, t));
-            bool in;
-            if (ob.u0 == 0u)
-                in = (p.x > f[0] - f[6]) & (p.x < f[0] + f[6]) & (p.y > f[1] - f[7]) & (p.y < f[1] + f[7]);
-            else if (ob.u0 == 1u)
-                in = (p.y > f[1] - f[7]) & (p.y < f[1] + f[7]) & (p.z > f[2] - f[8]) & (p.z < f[2] + f[8]);
-            else
-                in = (p.x > f[0] - f[6]) & (p.x < f[0] + f[6]) & (p.z > f[2] - f[8]) & (p.z < f[2] + f[8]);
+            // the hit point's two in-plane coordinates (ray.at(t) per component), tested
+            // against the bounds rt_scene.cpp precomputed with Plane::hit's float ops
+            float pa, pb;
+            if (ob.u0 == 0u) {
+                pa = o.x + d.x * t;
+                pb = o.y + d.y * t;
+            } else if (ob.u0 == 1u) {
+                pa = o.y + d.y * t;
+                pb = o.z + d.z * t;
+            } else {
+                pa = o.x + d.x * t;
+                pb = o.z + d.z * t;
+            }
+            const bool in = (pa > f[6]) & (pa < f[7]) & (pb > f[8]) & (pb < f[9]);
             const bool ok = proceed & (t >= kTMin) & in;
             h.merge(ok ? t : __builtin_nanf(""), ob.order, false, i, -1);
         } else if (ob.type == kObjSphere || ob.type == kObjMovingSphere) {

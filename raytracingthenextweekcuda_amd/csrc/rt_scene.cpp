@@ -352,6 +352,18 @@ std::string HostScene::flatten() {
         objs.push_back(r);
     }
     for (size_t k = 0; k < objs.size(); ++k) objs[k].order = (uint32_t)k;  // sequential scan position
+    // Plane::hit's rectangle bounds (Plane.cu:25-45: position -/+ extend on the two axes
+    // of the orientation), evaluated once here with the same float ops; the kernel
+    // compares the hit point against f[6..9] = (lo_a, hi_a, lo_b, hi_b).
+    for (ObjRec& r : objs) {
+        if (r.type != kObjPlane) continue;
+        const int a = r.u0 == 1u ? 1 : 0, b = r.u0 == 0u ? 1 : 2;
+        const float pa = r.f[a], ea = r.f[6 + a], pb = r.f[b], eb = r.f[6 + b];
+        r.f[6] = pa - ea;
+        r.f[7] = pa + ea;
+        r.f[8] = pb - eb;
+        r.f[9] = pb + eb;
+    }
     n_scan = (int)objs.size();
     return group_spheres();
 }

@@ -39,7 +39,8 @@ struct alignas(16) ObjRec {
     uint32_t order;  // position in the reference's sequential hit() scan (tie rule)
     // sphere: center xyz, radius
     // moving sphere: center0 xyz, center1 xyz, time0, time1, radius
-    // plane: position xyz, normal xyz, extend xyz
+    // plane: position xyz, normal xyz, rectangle bounds (lo_a, hi_a, lo_b, hi_b) on the
+    //        orientation's axes a, b (XY: x, y; YZ: y, z; XZ: x, z)
     // mesh: boundsMin xyz, boundsMax xyz (computeMeshAABB, main.cu:261-281)
     float f[10];
 };
