@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RTMI_ABI_VERSION 5
+#define RTMI_ABI_VERSION 6
 
 typedef int32_t rt_status;
 enum {
@@ -161,6 +161,25 @@ rt_status rt_mesh_ply(rt_ctx* ctx, int32_t index, const char* path, const float 
  * `capacity` bytes to `out` (may be NULL) and the full size to *size. */
 rt_status rt_ply_bvh_image(const char* path, const float offset[3], float max_coord,
                            uint8_t* out, int64_t capacity, int64_t* size);
+
+/* ---- BVH builder ----
+ * RT_BVH_HOST (default): the reference's Recurse + PopulateCacheFriendlyBVH on the
+ * host (BVH.cpp:94-497; rt_bvh.cpp, exact O(N log N) split search).
+ * RT_BVH_GPU: the same builder restated level by level on the context's device
+ * (rt_bvh_gpu.hip), byte-identical trees; used by rt_commit (mesh and sphere
+ * BVHs) and rt_process_triangle_data. It declines inputs with -0.0 coordinates
+ * (the reference's min3/max3 tie rule is order-dependent there); those are built
+ * on the host. */
+#define RT_BVH_HOST 0
+#define RT_BVH_GPU 1
+rt_status rt_set_bvh_builder(rt_ctx* ctx, int32_t builder);
+/* Wall time (ms) of the BVH builds of the last rt_commit + rt_process_triangle_data,
+ * and how many of them the GPU builder ran. */
+rt_status rt_bvh_build_stats(const rt_ctx* ctx, double* build_ms, int32_t* gpu_builds);
+/* rt_ply_bvh_image with the GPU builder on `device`; *build_ms (may be NULL) = the
+ * build's wall time (upload, levels, numbering, download). */
+rt_status rt_ply_bvh_image_gpu(int32_t device, const char* path, const float offset[3], float max_coord,
+                               uint8_t* out, int64_t capacity, int64_t* size, double* build_ms);
 
 /* ---- pathTrace scene (prepareCUDAscene, main.cu:404-553) ----
  * loadObject (Loader.cpp:207-319): appends a PLY mesh whose triangles carry

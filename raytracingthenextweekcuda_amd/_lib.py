@@ -23,7 +23,7 @@ STATUS_NAMES = {
 }
 
 # Every symbol include/rtmi.h declares (checked by tests/test_abi.py).
-ABI_VERSION = 5  # include/rtmi.h RTMI_ABI_VERSION
+ABI_VERSION = 6  # include/rtmi.h RTMI_ABI_VERSION
 
 EXPORTS = [
     "rt_abi_version", "rt_create", "rt_destroy", "rt_last_error", "rt_clear_scene",
@@ -32,7 +32,7 @@ EXPORTS = [
     "rt_sphere", "rt_moving_sphere", "rt_plane",
     "rt_cube", "rt_mesh", "rt_mesh_obj", "rt_mesh_triangle_count", "rt_mesh_vertices",
     "rt_mesh_ply", "rt_ply_bvh_image", "rt_load_object", "rt_process_triangle_data",
-    "rt_pathtrace_bvh_image",
+    "rt_pathtrace_bvh_image", "rt_set_bvh_builder", "rt_bvh_build_stats", "rt_ply_bvh_image_gpu",
     "rt_camera", "rt_commit", "rt_scene_info", "rt_render", "rt_render_device", "rt_sync_stats",
     "rt_render_u8", "rt_accumulate", "rt_render_multi", "rt_gamma_u8",
 ]
@@ -114,6 +114,10 @@ def lib():
     L.rt_mesh_ply.argtypes = [vp, i32, C.c_char_p, fp, C.c_float, i32]
     L.rt_ply_bvh_image.argtypes = [C.c_char_p, fp, C.c_float, C.POINTER(C.c_uint8), C.c_int64,
                                    C.POINTER(C.c_int64)]
+    L.rt_ply_bvh_image_gpu.argtypes = [i32, C.c_char_p, fp, C.c_float, C.POINTER(C.c_uint8), C.c_int64,
+                                       C.POINTER(C.c_int64), C.POINTER(C.c_double)]
+    L.rt_set_bvh_builder.argtypes = [vp, i32]
+    L.rt_bvh_build_stats.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int32)]
     L.rt_load_object.argtypes = [vp, C.c_char_p, i32]
     L.rt_process_triangle_data.argtypes = [vp, fp, C.c_float, C.POINTER(C.c_int32)]
     L.rt_pathtrace_bvh_image.argtypes = [vp, C.POINTER(C.c_uint8), C.c_int64, C.POINTER(C.c_int64)]

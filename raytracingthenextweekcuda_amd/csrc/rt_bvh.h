@@ -56,6 +56,15 @@ void build_cf_bvh(const std::vector<v3>& vertices, const std::vector<uint32_t>& 
 void build_cf_bvh_boxes(const std::vector<v3>& bottoms, const std::vector<v3>& tops, CFBvh& out,
                         int leaf_min_split = 4);
 
+// The same builder on the GPU (rt_bvh_gpu.hip): level-synchronous, one
+// workgroup per node, byte-identical output. Returns "" on success, else why it
+// declined (-0.0 coordinates, allocation failure, ...): callers then use the
+// host builder. *ms = wall time of the build (upload, levels, download).
+std::string gpu_build_cf_bvh(int device, const std::vector<v3>& vertices, const std::vector<uint32_t>& indices,
+                             CFBvh& out, int leaf_min_split, double* ms);
+std::string gpu_build_cf_bvh_boxes(int device, const std::vector<v3>& lo, const std::vector<v3>& hi, CFBvh& out,
+                                   int leaf_min_split, double* ms);
+
 // Kuchkuda triangle record of the pathTrace integrator, as uploaded by
 // prepareCUDAscene (main.cu:457-494) minus the unused centre: plane normal + d,
 // three edge planes + d1..d3 (processTriangleData, Loader.cpp:166-202) and the

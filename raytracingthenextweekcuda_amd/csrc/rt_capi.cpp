@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -57,6 +58,8 @@ struct rt_ctx {
     rt::KTri* d_pt_tris = nullptr;
     rt::CFNode* d_pt_nodes = nullptr;
     int32_t* d_pt_list = nullptr;
+    double pt_build_ms = 0.0;
+    int pt_gpu_builds = 0;
 };
 
 namespace {
@@ -402,6 +405,38 @@ rt_status rt_ply_bvh_image(const char* path, const float offset[3], float max_co
     return RT_OK;
 }
 
+rt_status rt_ply_bvh_image_gpu(int32_t device, const char* path, const float offset[3], float max_coord,
+                               uint8_t* out, int64_t capacity, int64_t* size, double* build_ms) {
+    if (device < 0 || !path || !finite3(offset) || !size || !(max_coord > 0.0f)) return RT_ERR_INVALID;
+    rt::PlyMesh m;
+    if (!rt::load_ply(path, m).empty()) return RT_ERR_IO;
+    rt::process_ply_vertices(m, rt::v3{offset[0], offset[1], offset[2]}, max_coord);
+    rt::CFBvh b;
+    double ms = 0.0;
+    if (!rt::gpu_build_cf_bvh(device, m.vertices, m.indices, b, 4, &ms).empty()) return RT_ERR_HIP;
+    if (build_ms) *build_ms = ms;
+    std::vector<uint8_t> img = rt::bvh_image(b);
+    *size = (int64_t)img.size();
+    if (out && capacity > 0) memcpy(out, img.data(), (size_t)std::min<int64_t>(capacity, *size));
+    return RT_OK;
+}
+
+rt_status rt_set_bvh_builder(rt_ctx* c, int32_t builder) {
+    if (!c) return RT_ERR_INVALID;
+    if (builder != RT_BVH_HOST && builder != RT_BVH_GPU) return fail(c, RT_ERR_INVALID, "unknown BVH builder");
+    if (builder == RT_BVH_GPU && c->device < 0) return fail(c, RT_ERR_NODEV, "the GPU builder needs a device context");
+    c->scene.bvh_gpu = builder == RT_BVH_GPU;
+    c->scene.bvh_device = c->device;
+    return RT_OK;
+}
+
+rt_status rt_bvh_build_stats(const rt_ctx* c, double* build_ms, int32_t* gpu_builds) {
+    if (!c) return RT_ERR_INVALID;
+    if (build_ms) *build_ms = c->scene.bvh_build_ms + c->pt_build_ms;
+    if (gpu_builds) *gpu_builds = c->scene.bvh_gpu_builds + c->pt_gpu_builds;
+    return RT_OK;
+}
+
 int32_t rt_mesh_triangle_count(const rt_ctx* c, int32_t index) {
     if (!c || index < 0 || (size_t)index >= c->scene.objects.size()) return 0;
     const rt::HostObject& o = c->scene.objects[index];
@@ -436,6 +471,8 @@ rt_status rt_process_triangle_data(rt_ctx* c, const float offset[3], float max_c
         return fail(c, RT_ERR_INVALID, "process_triangle_data: bad arguments");
     if (c->device >= 0) RT_HIP(c, hipSetDevice(c->device));
     free_pathtrace(c);
+    c->pt_build_ms = 0.0;
+    c->pt_gpu_builds = 0;
     rt::PlyMesh m = c->pt_raw;
     float scale_max = 0.0f;
     std::vector<rt::KTri> kt;
@@ -447,7 +484,12 @@ rt_status rt_process_triangle_data(rt_ctx* c, const float offset[3], float max_c
             const rt::v3 v = m.vertices[i];
             scale_max = std::max(scale_max, std::max(fabsf(v.x), std::max(fabsf(v.y), fabsf(v.z))));
         }
-        rt::build_cf_bvh(m.vertices, m.indices, b);
+        const auto t0 = std::chrono::steady_clock::now();
+        if (c->scene.bvh_gpu && rt::gpu_build_cf_bvh(c->device, m.vertices, m.indices, b, 4, nullptr).empty())
+            c->pt_gpu_builds = 1;
+        else
+            rt::build_cf_bvh(m.vertices, m.indices, b);
+        c->pt_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     if (out_info) {
         out_info[0] = (int32_t)kt.size();

@@ -150,7 +150,9 @@ RT_HD v3 random_in_unit_sphere(Rng& r) {
         float y = r.next();
         float z = r.next();
         v3 p = adds(scale(v3{x, y, z}, 2.0f), -1.0f);
+#ifndef RT_ABL_NOREJECT  // timing ablation builds only (results differ)
         if (lengthsq(p) >= 1.0f) continue;
+#endif
         return p;
     }
 }

@@ -3,6 +3,8 @@
 // tables of rt_scene.h. Compiled with -ffp-contract=off (see Makefile).
 #include "rt_scene.h"
 
+#include <chrono>
+
 #include "rt_bvh.h"
 
 #include <math.h>
@@ -228,7 +230,23 @@ std::string load_obj_transformed(const std::string& path, v3 scl, v3 rot, v3 off
     return "";
 }
 
+void HostScene::build_bvh(const std::vector<v3>& vs, const std::vector<uint32_t>& ix, CFBvh& b) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (bvh_gpu && gpu_build_cf_bvh(bvh_device, vs, ix, b, 4, nullptr).empty()) ++bvh_gpu_builds;
+    else build_cf_bvh(vs, ix, b);
+    bvh_build_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+void HostScene::build_bvh_boxes(const std::vector<v3>& lo, const std::vector<v3>& hi, CFBvh& b) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (bvh_gpu && gpu_build_cf_bvh_boxes(bvh_device, lo, hi, b, 4, nullptr).empty()) ++bvh_gpu_builds;
+    else build_cf_bvh_boxes(lo, hi, b);
+    bvh_build_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 std::string HostScene::flatten() {
+    bvh_build_ms = 0.0;
+    bvh_gpu_builds = 0;
     objs.clear();
     n_scan = 0;
     tris.clear();
@@ -314,7 +332,7 @@ std::string HostScene::flatten() {
                     ix[k] = (uint32_t)k;
                 }
                 CFBvh b;
-                build_cf_bvh(vs, ix, b);  // reference leaves (larger: measured slower)
+                build_bvh(vs, ix, b);  // reference leaves (larger: measured slower)
                 if (b.max_depth >= kBvhStackDepth)
                     return "mesh " + std::to_string(i) + ": BVH depth " + std::to_string(b.max_depth) +
                            " exceeds the traversal stack (" + std::to_string(kBvhStackDepth) + ")";
@@ -408,7 +426,7 @@ std::string HostScene::group_spheres() {
         hi[k] = h;
     }
     CFBvh b;
-    build_cf_bvh_boxes(lo, hi, b);
+    build_bvh_boxes(lo, hi, b);
     if (b.max_depth >= kBvhStackDepth)
         return "sphere BVH depth " + std::to_string(b.max_depth) + " exceeds the traversal stack";
     bvh_max_depth = std::max(bvh_max_depth, b.max_depth);

@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 
+#include "rt_bvh.h"
 #include "rt_math.h"
 
 namespace rt {
@@ -136,9 +137,18 @@ struct HostScene {
     std::vector<uint32_t> tri_orig;
     int bvh_max_depth = 0;
 
+    // BVH builder (rt_set_bvh_builder): host Recurse, or its GPU restatement on
+    // `bvh_device` (byte-identical; falls back to the host when it declines).
+    bool bvh_gpu = false;
+    int bvh_device = -1;
+    double bvh_build_ms = 0.0;  // summed wall time of the last flatten()'s builds
+    int bvh_gpu_builds = 0;     // builds the GPU ran in the last flatten()
+
     // Returns "" on success or an error message.
     std::string flatten();
     std::string group_spheres();
+    void build_bvh(const std::vector<v3>& vs, const std::vector<uint32_t>& ix, CFBvh& b);
+    void build_bvh_boxes(const std::vector<v3>& lo, const std::vector<v3>& hi, CFBvh& b);
 };
 
 // Camera::initialize + updateViewMatrix (Camera.h:19-34, 86-103) on the host.

@@ -184,6 +184,19 @@ class Renderer:
         self._check(self.L.rt_process_triangle_data(self.ctx, _v(offset), max_coord, out))
         return {"triangles": out[0], "bvh_nodes": out[1], "tri_list": out[2], "depth": out[3]}
 
+    def set_bvh_builder(self, builder: str = "host"):
+        """BVH builder for rt_commit / process_triangle_data: "host" (Recurse on the
+        host) or "gpu" (the byte-identical level-synchronous GPU restatement)."""
+        code = {"host": 0, "gpu": 1}[builder]
+        self._check(self.L.rt_set_bvh_builder(self.ctx, code))
+
+    def bvh_build_stats(self) -> dict:
+        """Wall time of the last commit's + process_triangle_data's BVH builds, and
+        how many the GPU builder ran."""
+        ms, n = C.c_double(), C.c_int32()
+        self._check(self.L.rt_bvh_build_stats(self.ctx, C.byref(ms), C.byref(n)))
+        return {"build_ms": ms.value, "gpu_builds": n.value}
+
     def pathtrace_bvh_image(self) -> bytes:
         """The `.bvh` cache image of the processed pathTrace scene (BVH.cpp:537-540)."""
         size = C.c_int64()

@@ -8,6 +8,6 @@ for r in $(seq 1 ${ROUNDS:-3}); do
     lib=raytracingthenextweekcuda_amd/librtmi.so
     [ "$v" != "default" ] && lib=raytracingthenextweekcuda_amd/librtmi_$v.so
     RTMI_LIB=$lib timeout -k 10 300 python bench.py --scene ${SCENE:-cornellbox1} --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/ab_${v}_$r.log 2>&1 || exit $?
-    echo "round $r $v $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_${v}_$r.log)"
+    echo "round $r $v $(grep -o "\"value\": [0-9.]*\|\"ms_per_step\": [0-9.]*" gpurun_out/ab_${v}_$r.log | tr "\n" " ")"
   done
 done
