@@ -68,10 +68,11 @@ typedef struct rt_render_params {
     int32_t row_block;      /* rows per tile block (>= 1) */
     int32_t row_rank;       /* this shard's rank */
     int32_t row_world;      /* number of shards (>= 1) */
-    int32_t lanes_per_pixel;/* lanes that split one pixel's samples: 0 = auto, or a
-                               power of two <= 64. Partial sums are combined in a
-                               fixed order, so results are deterministic for a
-                               given value; 1 = the reference's sequential sum. */
+    int32_t lanes_per_pixel;/* sub-streams that split one pixel's samples: 0 = auto,
+                               or a power of two <= 128 (<= 64 with RTMI_QUEUE=0).
+                               Partial sums are combined in a fixed order, so
+                               results are deterministic for a given value; 1 (and
+                               spp) = the reference's sequential sum. */
     int32_t integrator;     /* RT_INTEGRATOR_RAYCOLOR (0) or RT_INTEGRATOR_PATHTRACE (1).
                                pathTrace bounces max_depth times (reference: 5). */
     uint32_t flags;         /* RT_RENDER_KEEP_COUNTERS: add this launch's counters to the

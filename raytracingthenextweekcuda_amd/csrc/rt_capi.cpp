@@ -614,10 +614,12 @@ static rt_status validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch
     L.row_world = p->row_world;
     L.local_rows = rt::owned_rows(p->height, p->row_block, p->row_rank, p->row_world);
     const int32_t s = p->lanes_per_pixel;
-    if (s < 0 || s > 64 || (s & (s - 1)) != 0)
-        return fail(c, RT_ERR_INVALID, "lanes_per_pixel must be 0 (auto) or a power of two <= 64");
     const char* qenv = getenv("RTMI_QUEUE");
     const bool queue = !(qenv && qenv[0] == '0');  // RTMI_QUEUE=0: static grid (A/B only)
+    // work-queue launches split a pixel into up to 128 sub-streams (items); the
+    // static grid maps one pixel's sub-streams onto lanes of one wave (<= 64)
+    if (s < 0 || s > (queue ? 128 : 64) || (s & (s - 1)) != 0)
+        return fail(c, RT_ERR_INVALID, "lanes_per_pixel must be 0 (auto) or a power of two <= 128 (64 static)");
     rt::choose_layout(L, s, queue);
     L.accumulate = 0;
     L.accum_scale = 0.0f;

@@ -55,7 +55,7 @@ inline void choose_layout(RenderLaunch& L, int32_t requested, bool queue) {
         while (2 * s <= 32 && 2 * s <= L.spp && px * 2 * s <= cap) s *= 2;
     }
     L.lanes_per_pixel = s;
-    const int32_t p = 64 / s;
+    const int32_t p = s <= 64 ? 64 / s : 1;  // S > 64 (work queue only): no static tile
     L.tile_w = p >= 8 ? 8 : p;
     L.tile_h = p / L.tile_w;
 }

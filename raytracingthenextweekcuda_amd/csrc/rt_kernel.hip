@@ -832,6 +832,8 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
                 s = c;
                 sum = v3{0.0f, 0.0f, 0.0f};
                 alive = s < L.spp;
+                // a sub-stream with no samples (S > spp) still owns its partial-sum slot
+                if (!alive) store_partial(L, item, sum);
                 need_cam = true;
             });
         }
@@ -1315,6 +1317,8 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
                 s = c;
                 sum = v3{0.0f, 0.0f, 0.0f};
                 alive = s < L.spp;
+                // a sub-stream with no samples (S > spp) still owns its partial-sum slot
+                if (!alive) store_partial(L, item, sum);
                 need_cam = true;
             });
         }

@@ -171,6 +171,39 @@ def test_lanes_per_pixel_parity(rtmi, lanes):
     assert np.max(np.abs(img - seq)) <= 1e-5
 
 
+@pytest.mark.parametrize("spp", [64, 128])
+def test_one_sample_per_substream_is_the_sequential_sum(rtmi, spp):
+    # S = spp (work queue, up to 128 sub-streams): every item is one sample and the
+    # fixed-order combine ((p0 + p1) + p2) + ... is the reference's sequential sum, so
+    # the image equals S = 1 bit for bit (and the oracle's sequential order)
+    w, h, depth = 24, 16, 5
+    with rtmi.Renderer(0) as r:
+        rtmi.cornell_box1(r, w, h)
+        one = r.render(w, h, spp, depth, lanes_per_pixel=spp)
+        assert r.stats()["lanes_per_pixel"] == spp
+        seq = r.render(w, h, spp, depth, lanes_per_pixel=1)
+    ref, _ = _oracle_yaml("cornellbox1.yaml", w, h).render(w, h, spp, depth)
+    assert np.array_equal(one, seq)
+    assert np.array_equal(one, ref)
+
+
+@pytest.mark.parametrize("integrator", ["rayColor", "pathTrace"])
+def test_more_substreams_than_samples(rtmi, integrator):
+    # S > spp: sub-streams without samples must still clear their partial-sum slots.
+    # The first render fills the context's partial buffer with nonzero sums; the
+    # second (spp 4 < S 8) reuses it and must not pick them up.
+    w, h, depth = 24, 16, 5
+    with rtmi.Renderer(0) as r:
+        if integrator == "pathTrace":
+            rtmi.materialball(r, w, h)
+        else:
+            rtmi.cornell_box1(r, w, h)
+        r.render(w, h, 8, depth, lanes_per_pixel=8, integrator=integrator)
+        img = r.render(w, h, 4, depth, lanes_per_pixel=8, integrator=integrator)
+        ref = r.render(w, h, 4, depth, lanes_per_pixel=1, integrator=integrator)
+    assert np.array_equal(img, ref)  # empty sub-streams add +0.0: the sequential sum
+
+
 def test_auto_lane_layout(rtmi):
     # work-queue launches: largest power of two S <= min(32, spp) with pixels * S <= 2^25
     # (rt_kernel.h choose_layout)
