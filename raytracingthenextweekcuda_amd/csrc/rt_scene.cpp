@@ -7,6 +7,7 @@
 
 #include "rt_bvh.h"
 
+#include <float.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -424,6 +425,40 @@ std::string HostScene::group_spheres() {
             return "sphere with non-finite bounds (degenerate moving-sphere time range?)";
         lo[k] = l;
         hi[k] = h;
+    }
+    // Spheres far larger than the rest (RTNW's r = 1000 ground) stay in the linear scan:
+    // inside the tree their box would enlarge every node on their root path, and every
+    // ray would descend it. Any split of the objects between the scan and the group
+    // gives the same hit (Hit::merge restates the sequential tie rule).
+    {
+        std::vector<float> ext(members.size());
+        for (size_t k = 0; k < members.size(); ++k)
+            ext[k] = std::max(hi[k].x - lo[k].x, std::max(hi[k].y - lo[k].y, hi[k].z - lo[k].z));
+        std::vector<float> sorted = ext;
+        std::nth_element(sorted.begin(), sorted.begin() + sorted.size() / 2, sorted.end());
+        const float core_cap = 8.0f * sorted[sorted.size() / 2];
+        v3 cl{FLT_MAX, FLT_MAX, FLT_MAX}, ch{-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (size_t k = 0; k < members.size(); ++k) {
+            if (ext[k] > core_cap) continue;
+            cl = v3{std::min(cl.x, lo[k].x), std::min(cl.y, lo[k].y), std::min(cl.z, lo[k].z)};
+            ch = v3{std::max(ch.x, hi[k].x), std::max(ch.y, hi[k].y), std::max(ch.z, hi[k].z)};
+        }
+        const float core_ext = std::max(ch.x - cl.x, std::max(ch.y - cl.y, ch.z - cl.z));
+        std::vector<ObjRec> keep;
+        std::vector<v3> klo, khi;
+        for (size_t k = 0; k < members.size(); ++k) {
+            if (ext[k] > 0.5f * core_ext) {
+                scan.push_back(members[k]);
+                continue;
+            }
+            keep.push_back(members[k]);
+            klo.push_back(lo[k]);
+            khi.push_back(hi[k]);
+        }
+        if (keep.size() < kSphereBvhMin) return "";  // not worth a tree: scan everything
+        members.swap(keep);
+        lo.swap(klo);
+        hi.swap(khi);
     }
     CFBvh b;
     build_bvh_boxes(lo, hi, b);
