@@ -142,14 +142,25 @@ struct Rng {
 // Utils::random(min,max) = min + (max - min) * u (Utils.h:49-51).
 RT_HD float random_range(Rng& r, float lo, float hi) { return lo + (hi - lo) * r.next(); }
 
+// 2u - 1 for the next draw u = RN(RN(x) 2^-32 + 2^-33) (u01). Scaling by 2 is exact,
+// so 2u = RN(RN(x) 2^-31 + 2^-32), and since RN(x) 2^-31 is exact that is one FMA:
+// the same bits as (u * 2) + (-1) and as -1 + (1 - -1) * u, in fewer instructions.
+RT_HD float two_u_minus_one(Rng& r) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_fmaf((float)r.next_u32(), 4.6566129e-10f /* 2^-31 */, 2.3283064e-10f /* 2^-32 */) + -1.0f;
+#else
+    return r.next() * 2.0f + -1.0f;
+#endif
+}
+
 // randomInUnitSphere (Utils.h:69-78): x, y, z drawn in order, each 2u + (-1)
 // (randomVector(min,max) = min + (max-min)*v, Utils.h:64-66 -> v*(2) + (-1)).
 RT_HD v3 random_in_unit_sphere(Rng& r) {
     for (;;) {
-        float x = r.next();
-        float y = r.next();
-        float z = r.next();
-        v3 p = adds(scale(v3{x, y, z}, 2.0f), -1.0f);
+        const float px = two_u_minus_one(r);
+        const float py = two_u_minus_one(r);
+        const float pz = two_u_minus_one(r);
+        v3 p{px, py, pz};
 #ifndef RT_ABL_NOREJECT  // timing ablation builds only (results differ)
         if (lengthsq(p) >= 1.0f) continue;
 #endif
@@ -161,8 +172,9 @@ RT_HD v3 random_in_unit_sphere(Rng& r) {
 // is unspecified; this build pins x before y.
 RT_HD v3 random_in_unit_disk(Rng& r) {
     for (;;) {
-        float x = random_range(r, -1.0f, 1.0f);
-        float y = random_range(r, -1.0f, 1.0f);
+        // random_range(r, -1, 1) = -1 + 2u: the same bits as 2u + (-1)
+        float x = two_u_minus_one(r);
+        float y = two_u_minus_one(r);
         v3 p = v3{x, y, 0.0f};
         if (lengthsq(p) >= 1.0f) continue;
         return p;
