@@ -153,7 +153,7 @@ rt_status rt_create(int32_t device, rt_ctx** out) {
         }
         c->have_events = true;
         if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
-            hipMalloc(&c->d_queue, 8 * 32 * sizeof(uint32_t)) != hipSuccess) {
+            hipMalloc(&c->d_queue, rt::kQueueHeadWords * sizeof(uint32_t)) != hipSuccess) {
             rt_destroy(c);
             return RT_ERR_HIP;
         }
@@ -661,7 +661,7 @@ static rt_status launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLa
             L.queue = rt::queue_blocks(c->n_cu);
             L.n_items = (uint32_t)items;
             L.partial = c->d_partial;
-            RT_HIP(c, hipMemsetAsync(c->d_queue, 0, 8 * 32 * sizeof(uint32_t), st));
+            RT_HIP(c, hipMemsetAsync(c->d_queue, 0, rt::kQueueHeadWords * sizeof(uint32_t), st));
         }
     }
     const bool keep = (p->flags & RT_RENDER_KEEP_COUNTERS) != 0;

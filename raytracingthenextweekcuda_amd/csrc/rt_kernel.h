@@ -60,6 +60,9 @@ inline void choose_layout(RenderLaunch& L, int32_t requested, bool queue) {
     L.tile_h = p / L.tile_w;
 }
 
+// Work-queue heads: up to 64 shards, one 128 B line (32 words) each.
+constexpr int kQueueHeadWords = 64 * 32;
+
 // counters[0] = segments, [1] = triangle tests, [2] = mesh-box tests,
 // [3] = BVH node visits, [4] = traversal overflow flag, [5] / [6] = spheres /
 // moving spheres tested in object-BVH leaves.

@@ -715,7 +715,11 @@ __device__ __forceinline__ bool queue_item(const RenderLaunch& L, uint32_t item,
 // chunks, each with its own head on its own 128 B line (one device word
 // saturates near 90 dequeues/us, MI355X_MICROARCH.md). A wave starts on
 // shard blockIdx % kQueueShards and moves on when its shard runs dry.
-constexpr int kQueueShards = 8;
+#ifndef RT_QUEUE_SHARDS
+#define RT_QUEUE_SHARDS 8
+#endif
+constexpr int kQueueShards = RT_QUEUE_SHARDS;
+static_assert(kQueueShards * 32 <= kQueueHeadWords, "queue heads");
 constexpr int kQueueStride = 32;  // u32 words between heads
 #ifndef RT_QUEUE_REFILL
 #define RT_QUEUE_REFILL 4  // idle lanes that trigger a refill (or all lanes idle); measured 1/2/4/8/16/32
