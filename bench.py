@@ -3,8 +3,10 @@
 
 One step = one full frame: every rank renders its interleaved pixel-row tiles
 with the HIP megakernel (librtmi.so) straight into an HBM buffer, then the
-tiles are gathered to rank 0 with one RCCL gather over xGMI (N > 1). The frame
-work is fixed as N grows (strong scaling).
+tiles are gathered to rank 0 with one RCCL gather over xGMI (N > 1), which
+overlaps the next frame's render (double-buffered tiles); the timed region ends
+after the last frame is assembled on rank 0. The frame work is fixed as N grows
+(strong scaling).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 N > 1 is launched by torch.distributed.run (one process per GPU).
@@ -192,8 +194,11 @@ def main():
 
     block = args.row_block
     rows = rtmi.owned_rows(H, block, rank, world)
+    # N > 1: frames are pipelined - frame k's RCCL gather runs on the NCCL stream under
+    # frame k+1's render (double-buffered tiles); every frame is complete by the end
     frame = RowShardedFrame(W, H, block,
-                            device=torch.device("cpu") if rehearsal else torch.device("cuda", local))
+                            device=torch.device("cpu") if rehearsal else torch.device("cuda", local),
+                            pipeline=world > 1)
     integrator = INTEGRATOR.get(args.scene, "rayColor")
     params = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, world, args.lanes, integrator)
     # timed launches add to the device counters (one read after the loop, no
@@ -211,7 +216,8 @@ def main():
             r.render_device(p, tile.data_ptr(), stream.cuda_stream)
 
     for _ in range(args.warmup):
-        frame.render(lambda tile: render_into(tile, params))
+        frame.submit(lambda tile: render_into(tile, params))
+        frame.drain()
         r.stats()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
@@ -227,7 +233,8 @@ def main():
             render_into(tile, p)
             e[1].record(stream)
 
-        frame.render(timed_render)  # this rank's row tiles, then the RCCL gather to rank 0
+        frame.submit(timed_render)  # this rank's row tiles; the RCCL gather to rank 0 overlaps the next frame
+    frame.drain()  # the last frame's gather and row assembly
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -40,7 +40,8 @@ class RowShardedFrame:
     rank 0 and None elsewhere.
     """
 
-    def __init__(self, width: int, height: int, row_block: int, group=None, device=None):
+    def __init__(self, width: int, height: int, row_block: int, group=None, device=None,
+                 pipeline: bool = False):
         import torch
         import torch.distributed as dist
 
@@ -56,12 +57,18 @@ class RowShardedFrame:
         self.frame = None
         self.gather_list = None
         self.src_rows = None
+        self.pending = None  # (async gather work, landing block index) of the last submitted frame
+        self.n_submitted = 0
         if self.world == 1:
             # one rank owns every row in order: render straight into the frame
             self.frame = torch.zeros((height, width, 3), dtype=torch.float32, device=self.device)
             self.tile = self.frame
             return
         self.tile = torch.zeros((self.max_rows, width, 3), dtype=torch.float32, device=self.device)
+        # pipelined frames (submit/drain): two tile buffers (and two landing blocks on rank 0),
+        # so frame k's gather overlaps frame k+1's render
+        self.pipeline = pipeline
+        self.tiles = [self.tile] + ([torch.zeros_like(self.tile)] if pipeline else [])
         if self.rank == 0:
             self.frame = torch.zeros((height, width, 3), dtype=torch.float32, device=self.device)
             # the gather lands in one (world * max_rows) block; frame row y is
@@ -69,6 +76,10 @@ class RowShardedFrame:
             self.gathered = torch.empty((self.world * self.max_rows, width, 3), dtype=torch.float32,
                                         device=self.device)
             self.gather_list = list(self.gathered.view(self.world, self.max_rows, width, 3).unbind(0))
+            self.landing = [(self.gathered, self.gather_list)]
+            if pipeline:
+                g2 = torch.empty_like(self.gathered)
+                self.landing.append((g2, list(g2.view(self.world, self.max_rows, width, 3).unbind(0))))
             src = [0] * height
             for k, ids in enumerate(tile_rows(height, row_block, self.world)):
                 for j, y in enumerate(ids):
@@ -89,6 +100,39 @@ class RowShardedFrame:
     def render(self, render_into: Callable[["object"], None]):
         render_into(self.tile)
         return self.gather()
+
+    # ---- pipelined frames ----
+    def _finish_pending(self):
+        work, b = self.pending
+        self.pending = None
+        work.wait()  # the current stream waits for the gather (the host does not, on NCCL)
+        if self.rank == 0:
+            self.torch.index_select(self.landing[b][0], 0, self.src_rows, out=self.frame)
+
+    def submit(self, render_into: Callable[["object"], None]):
+        """Render the next frame into the free tile buffer and start its gather without
+        waiting for it; the previous frame's gather (which ran under this render) is
+        completed and assembled on rank 0 after this frame's render is enqueued."""
+        if self.world == 1:
+            render_into(self.frame)
+            return
+        if not self.pipeline:
+            raise RuntimeError("RowShardedFrame(pipeline=True) is required for submit()")
+        b = self.n_submitted % 2
+        self.n_submitted += 1
+        tile = self.tiles[b]
+        render_into(tile)  # enqueued before waiting on the previous gather
+        if self.pending is not None:
+            self._finish_pending()
+        work = self.dist.gather(tile, self.landing[b][1] if self.rank == 0 else None, dst=0,
+                                group=self.group, async_op=True)
+        self.pending = (work, b)
+
+    def drain(self) -> Optional["object"]:
+        """Complete the last submitted frame; returns it on rank 0 (None elsewhere)."""
+        if self.pending is not None:
+            self._finish_pending()
+        return self.frame if self.rank == 0 else None
 
 
 def render_params_for_rank(renderer, width, height, spp, depth, row_block, rank, world, seed=1984,
