@@ -330,7 +330,7 @@ __device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, ui
 // is descended first (kept in registers), the farther one waits on the LDS
 // stack and is re-tested against the best t when popped. The candidate set and
 // the (t, original index) merge make the result independent of the order.
-__device__ __forceinline__ void mesh_bvh(const TriRec* __restrict__ tris,
+[[maybe_unused]] __device__ __forceinline__ void mesh_bvh(const TriRec* __restrict__ tris,
                                          const uint32_t* __restrict__ tri_orig,
                                          const BvhNode* __restrict__ nodes, uint32_t root, bool want,
                                          v3 o, v3 d, v3 inv, Hit& h, int32_t obj, uint32_t order,
@@ -358,7 +358,7 @@ __device__ __forceinline__ void mesh_bvh(const TriRec* __restrict__ tris,
             for (uint32_t k = cur.a; k < cur.a + nt; ++k) {
                 const float t = tri_t(tris[k], o, d);
                 if (t <= t0) {
-                    const uint32_t orig = tri_orig[k];
+                    const uint32_t orig = tri_orig[2 * k];
                     if (t < best || (t == best && orig < best_orig)) {
                         best = t;
                         best_orig = orig;
@@ -392,6 +392,145 @@ __device__ __forceinline__ void mesh_bvh(const TriRec* __restrict__ tris,
         }
     }
     if (best_orig != 0xFFFFFFFFu) h.merge(best, order, false, obj, (int32_t)best_k);
+}
+
+#ifndef RT_BVH_STEAL
+#define RT_BVH_STEAL 1  // cooperative (work-stealing) mesh traversal; 0 = per-lane mesh_bvh (A/B)
+#endif
+
+// Cooperative BVH mesh traversal (called by all 64 lanes). Per-lane traversal
+// leaves most of a wave idle while its deepest rays finish (VALU lane use was
+// 18% on the bunny). Here a lane whose work ran out takes the bottom (oldest,
+// shallowest) pending subtree of a lane that still has one, together with that
+// ray (origin, direction, inverse, closestSoFar) and its current best distance
+// as the pruning bound. Each lane's stack is a deque in the LDS: owners push and
+// pop at the top, thieves take from the bottom, all in the wave's one
+// instruction stream. A lane reports the best (t, mesh-local index) it found
+// for a ray with a 64-bit LDS atomic-min on that ray's slot before it switches
+// rays. Every subtree is still traversed exactly once, against a bound no
+// tighter than the one the owner would have used, so the candidate set and the
+// (t, lowest index) winner are those of the sequential scan.
+__device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
+                                              const uint32_t* __restrict__ tri_orig,
+                                              const BvhNode* __restrict__ nodes, uint32_t root, uint32_t base,
+                                              bool want, v3 o, v3 d, v3 inv, Hit& h, int32_t obj,
+                                              uint32_t order, uint32_t* wstack, WaveLds& W, int lane,
+                                              Counters& cnt) {
+    const uint64_t wm = __ballot(want);
+    if (wm == 0) return;
+    W.key[lane] = ~0ull;
+    int owner = lane;
+    v3 ro = o, rd = d, ri = inv;
+    float t0 = h.t;    // the ray's closestSoFar: accept t <= t0
+    float best = t0;   // this lane's pruning bound for the ray
+    uint32_t best_orig = 0xFFFFFFFFu;
+    BvhNode cur = nodes[root];
+    bool has = want;
+    if (want) ++cnt.node_visits;
+    int sp = 0, bot = 0;  // pending subtrees: wstack[k * 64 + lane], bot <= k < sp
+    auto flush = [&]() {
+        if (best_orig != 0xFFFFFFFFu)
+            atomicMin(&W.key[owner], ((unsigned long long)__float_as_uint(best) << 32) | best_orig);
+        best_orig = 0xFFFFFFFFu;
+    };
+    __builtin_amdgcn_wave_barrier();
+    for (;;) {
+        if (__ballot(has || sp > bot) == 0) break;
+        // steal: pair the r-th idle lane with the r-th lane that has a spare subtree
+        const bool idle = !has && sp == bot;
+        const bool spare = sp - bot >= (has ? 1 : 2);
+        const uint64_t im = __ballot(idle), vm = __ballot(spare);
+        if (im != 0 && vm != 0) {
+            const int nv = __popcll(vm), ni = __popcll(im);
+            if (spare) W.src[lane_rank(vm)] = lane;
+            __builtin_amdgcn_wave_barrier();
+            int vic = lane;
+            const bool thief = idle && lane_rank(im) < nv;
+            if (thief) vic = W.src[lane_rank(im)];
+            const int vb = __shfl(bot, vic, 64);
+            const int v_owner = __shfl(owner, vic, 64);
+            const v3 v_o{__shfl(ro.x, vic, 64), __shfl(ro.y, vic, 64), __shfl(ro.z, vic, 64)};
+            const v3 v_d{__shfl(rd.x, vic, 64), __shfl(rd.y, vic, 64), __shfl(rd.z, vic, 64)};
+            const v3 v_i{__shfl(ri.x, vic, 64), __shfl(ri.y, vic, 64), __shfl(ri.z, vic, 64)};
+            const float v_t0 = __shfl(t0, vic, 64), v_best = __shfl(best, vic, 64);
+            if (thief) {
+                const uint32_t entry = wstack[vb * 64 + vic];
+                flush();
+                owner = v_owner;
+                ro = v_o;
+                rd = v_d;
+                ri = v_i;
+                t0 = v_t0;
+                best = v_best;
+                sp = bot = 0;
+                cur = nodes[entry];
+                ++cnt.node_visits;
+                float tn;
+                has = node_hit(cur, ro, ri, best, tn);
+            }
+            if (spare && lane_rank(vm) < ni) ++bot;  // robbed
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (!has) {
+            if (sp > bot) {
+                cur = nodes[wstack[(--sp) * 64 + lane]];
+                ++cnt.node_visits;
+                float tn;
+                has = node_hit(cur, ro, ri, best, tn);  // best improved since the push?
+            }
+            if (sp == bot) sp = bot = 0;
+            if (!has) continue;
+        }
+        if (cur.b & 0x80000000u) {
+            const uint32_t nt = cur.b & 0x7FFFFFFFu;
+            cnt.tri_tests += nt;
+            for (uint32_t k = cur.a; k < cur.a + nt; ++k) {
+                const float t = tri_t(tris[k], ro, rd);
+                if (t <= t0) {
+                    const uint32_t orig = tri_orig[2 * k];
+                    if (t < best || (t == best && orig < best_orig)) {
+                        best = t;
+                        best_orig = orig;
+                    }
+                }
+            }
+            has = false;
+            continue;
+        }
+        const uint32_t il = cur.a, ir = cur.b;
+        const BvhNode nl = nodes[il], nr = nodes[ir];
+        cnt.node_visits += 2;
+        float tl, tr;
+        const bool hl = node_hit(nl, ro, ri, best, tl);
+        const bool hr = node_hit(nr, ro, ri, best, tr);
+        if (hl && hr) {
+            if (sp + 1 > kStackDepth) {
+                cnt.overflow = 1;
+                has = false;
+                sp = bot = 0;
+                continue;
+            }
+            const bool left_first = tl <= tr;
+            wstack[(sp++) * 64 + lane] = left_first ? ir : il;
+            cur = left_first ? nl : nr;
+        } else if (hl) {
+            cur = nl;
+        } else if (hr) {
+            cur = nr;
+        } else {
+            has = false;
+        }
+    }
+    flush();
+    __builtin_amdgcn_wave_barrier();
+    if (want) {
+        const unsigned long long key = W.key[lane];
+        if (key != ~0ull) {
+            const uint32_t k = tri_orig[2 * (base + (uint32_t)(key & 0xFFFFFFFFu)) + 1];
+            h.merge(__uint_as_float((uint32_t)(key >> 32)), order, false, obj, (int32_t)k);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
 }
 
 // One object record (64 B) as a single wave-uniform scalar load; the same
@@ -608,7 +747,12 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 RT_STAMP(t_m1);
                 RT_ACC(3, t_m0, t_m1);
             } else {
+#if RT_BVH_STEAL
+                mesh_bvh_coop(S.tris, S.tri_orig, S.nodes, root, ob.u0, want, o, d, inv, h, i, ob.order,
+                              stack - lane, W, lane, cnt);
+#else
                 mesh_bvh(S.tris, S.tri_orig, S.nodes, root, want, o, d, inv, h, i, ob.order, stack, cnt);
+#endif
             }
         } else if (ob.type == kObjMedium) {
             h.merge(live ? medium_candidate(ob, o, d, mk) : __builtin_nanf(""), ob.order, false, i, -1);

@@ -361,11 +361,16 @@ std::string HostScene::flatten() {
                     nodes.push_back(n);
                 }
             }
+            // tri_orig pairs per leaf-order position j = base + t: (mesh-local index of the
+            // triangle at j, position of the triangle whose mesh-local index is t)
+            const size_t pair0 = tri_orig.size();
+            tri_orig.resize(pair0 + 2 * nt);
             for (size_t t = 0; t < nt; ++t) {
                 const float* p = &o.tri_vertices[9 * (size_t)order[t]];
                 tris.push_back(make_triangle(v3{p[0], p[1], p[2]}, v3{p[3], p[4], p[5]},
                                              v3{p[6], p[7], p[8]}));
-                tri_orig.push_back((uint32_t)order[t]);
+                tri_orig[pair0 + 2 * t] = (uint32_t)order[t];
+                tri_orig[pair0 + 2 * (size_t)order[t] + 1] = r.u0 + (uint32_t)t;
             }
         }
         objs.push_back(r);

@@ -97,7 +97,7 @@ struct SceneArgs {
     const TriRec* tris;
     const MatRec* mats;
     const BvhNode* nodes;
-    const uint32_t* tri_orig;  // mesh-local triangle index of each TriRec
+    const uint32_t* tri_orig;  // per TriRec j: [2j] mesh-local index, [2j+1] position of mesh-local index j - base
     int32_t n_objs;            // records scanned by hit(); sphere-group members follow them
     int32_t n_mats;
     bool has_bvh;  // any mesh carries a BVH (selects the kernel variant)
@@ -134,7 +134,7 @@ struct HostScene {
     std::vector<TriRec> tris;
     std::vector<MatRec> mats;
     std::vector<BvhNode> nodes;
-    std::vector<uint32_t> tri_orig;
+    std::vector<uint32_t> tri_orig;  // 2 per triangle: (mesh-local index, inverse map), see flatten()
     int bvh_max_depth = 0;
 
     // BVH builder (rt_set_bvh_builder): host Recurse, or its GPU restatement on
