@@ -461,7 +461,7 @@ __device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
                 rd = v_d;
                 ri = v_i;
                 t0 = v_t0;
-                best = v_best;
+                best = fminf(v_best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
                 sp = bot = 0;
                 cur = nodes[entry];
                 ++cnt.node_visits;
@@ -475,6 +475,8 @@ __device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
             if (sp > bot) {
                 cur = nodes[wstack[(--sp) * 64 + lane]];
                 ++cnt.node_visits;
+                // the ray's best so far over all lanes (NaN while none: fminf keeps ours)
+                best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
                 float tn;
                 has = node_hit(cur, ro, ri, best, tn);  // best improved since the push?
             }
@@ -494,6 +496,8 @@ __device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
                     }
                 }
             }
+            // publish at once: the ray's owner and the other lanes working on it prune with it
+            flush();
             has = false;
             continue;
         }
