@@ -453,8 +453,9 @@ __device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
             const v3 v_d{__shfl(rd.x, vic, 64), __shfl(rd.y, vic, 64), __shfl(rd.z, vic, 64)};
             const v3 v_i{__shfl(ri.x, vic, 64), __shfl(ri.y, vic, 64), __shfl(ri.z, vic, 64)};
             const float v_t0 = __shfl(t0, vic, 64), v_best = __shfl(best, vic, 64);
+            const int vt = vb;  // the victim's oldest pending subtree (newest: same speed, measured)
             if (thief) {
-                const uint32_t entry = wstack[vb * 64 + vic];
+                const uint32_t entry = wstack[vt * 64 + vic];
                 flush();
                 owner = v_owner;
                 ro = v_o;
@@ -1350,7 +1351,7 @@ __device__ __forceinline__ void pt_leaf(const KTri* __restrict__ ktris,
 // is skipped only when every point of its eps-widened box lies beyond the
 // best hit. Children are tested at their parent and the nearer is descended
 // first, which changes the order but not the set of candidates that can win.
-__device__ __forceinline__ void pt_traverse(const KTri* __restrict__ ktris,
+[[maybe_unused]] __device__ __forceinline__ void pt_traverse(const KTri* __restrict__ ktris,
                                             const CFNode* __restrict__ nodes,
                                             const int32_t* __restrict__ tri_list,
                                             uint32_t* stack, const PtRay& r, int avoid,
@@ -1417,6 +1418,173 @@ __device__ __forceinline__ void pt_traverse(const KTri* __restrict__ ktris,
     }
 }
 
+// Cooperative BVH_IntersectTriangles (all lanes of the wave that reach it; the
+// same work stealing as mesh_bvh_coop). Lanes without a subtree take the oldest
+// pending subtree of a lane that has a spare one, with its ray and pruning bound;
+// per-ray minima of (distance^2, DFS list position), the reference's tie rule,
+// merge through 64-bit LDS atomic-min. Every subtree is traversed once with the
+// reference's exact box decisions and a bound no tighter than the owner's, so
+// the winner is the one BVH_IntersectTriangles finds. The owner recomputes the
+// winner's hit point with pt_leaf's operations.
+__device__ __forceinline__ void pt_traverse_coop(const KTri* __restrict__ ktris,
+                                                 const CFNode* __restrict__ nodes,
+                                                 const int32_t* __restrict__ tri_list, uint32_t* wstack,
+                                                 unsigned long long* keys, int32_t* vlist, int lane, bool want,
+                                                 const PtRay& ray, int avoid_in, float len_in, float eps_in,
+                                                 PtBest& out, Counters& cnt) {
+    const uint64_t wm = __ballot(want);
+    if (wm == 0) return;
+    keys[lane] = ~0ull;
+    int owner = lane;
+    PtRay r = ray;
+    int avoid = avoid_in;
+    float len_d = len_in, eps = eps_in;
+    PtBest b{3.40282347e+38f, 3.40282347e+38f, 0x7FFFFFFF, -1, v3{0.0f, 0.0f, 0.0f}};
+    auto pruned = [&](float tw) { return tw > 0.0f && tw * len_d > b.dist * 1.0001f + eps; };
+    auto flush = [&]() {
+        if (b.i != 0x7FFFFFFF)
+            atomicMin(&keys[owner], ((unsigned long long)__float_as_uint(b.hz) << 32) | (uint32_t)b.i);
+        b.i = 0x7FFFFFFF;
+    };
+    auto refresh = [&]() {  // the ray's best over all lanes (NaN while none)
+        const float g = __uint_as_float((uint32_t)(keys[owner] >> 32));
+        if (g < b.hz) {
+            b.hz = g;
+            b.dist = fsqrt(g);
+        }
+    };
+    CFNode cur = nodes[0];
+    bool has = want;
+    if (want) {
+        ++cnt.node_visits;
+        if (!(cur.u0 & 0x80000000u)) {
+            float tw, od;
+            has = pt_box_decide(cur, r, tw, od);
+        }
+    }
+    int sp = 0, bot = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (;;) {
+        if (__ballot(has || sp > bot) == 0) break;
+        const bool idle = !has && sp == bot;
+        const bool spare = sp - bot >= (has ? 1 : 2);
+        const uint64_t im = __ballot(idle), vm = __ballot(spare);
+        if (im != 0 && vm != 0) {
+            const int nv = __popcll(vm), ni = __popcll(im);
+            if (spare) vlist[lane_rank(vm)] = lane;
+            __builtin_amdgcn_wave_barrier();
+            int vic = lane;
+            const bool thief = idle && lane_rank(im) < nv;
+            if (thief) vic = vlist[lane_rank(im)];
+            const int vb = __shfl(bot, vic, 64);
+            const int v_owner = __shfl(owner, vic, 64), v_avoid = __shfl(avoid, vic, 64);
+            PtRay vr;
+            vr.o = v3{__shfl(r.o.x, vic, 64), __shfl(r.o.y, vic, 64), __shfl(r.o.z, vic, 64)};
+            vr.d = v3{__shfl(r.d.x, vic, 64), __shfl(r.d.y, vic, 64), __shfl(r.d.z, vic, 64)};
+            vr.inv = v3{__shfl(r.inv.x, vic, 64), __shfl(r.inv.y, vic, 64), __shfl(r.inv.z, vic, 64)};
+            vr.pad_t = v3{__shfl(r.pad_t.x, vic, 64), __shfl(r.pad_t.y, vic, 64), __shfl(r.pad_t.z, vic, 64)};
+            vr.exact = __shfl((int)r.exact, vic, 64) != 0;
+            const float v_len = __shfl(len_d, vic, 64), v_eps = __shfl(eps, vic, 64);
+            const float v_hz = __shfl(b.hz, vic, 64), v_dist = __shfl(b.dist, vic, 64);
+            if (thief) {
+                const uint32_t entry = wstack[vb * 64 + vic];
+                flush();
+                owner = v_owner;
+                r = vr;
+                avoid = v_avoid;
+                len_d = v_len;
+                eps = v_eps;
+                b.hz = v_hz;
+                b.dist = v_dist;
+                refresh();
+                sp = bot = 0;
+                cur = nodes[entry];
+                ++cnt.node_visits;
+                float tw, od;
+                pt_box_bounds(cur, r, tw, od);
+                has = !pruned(tw);
+            }
+            if (spare && lane_rank(vm) < ni) ++bot;  // robbed
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (!has) {
+            if (sp > bot) {
+                cur = nodes[wstack[(--sp) * 64 + lane]];
+                ++cnt.node_visits;
+                refresh();
+                float tw, od;
+                pt_box_bounds(cur, r, tw, od);
+                has = !pruned(tw);  // the best hit improved since the push
+            }
+            if (sp == bot) sp = bot = 0;
+            if (!has) continue;
+        }
+        if (cur.u0 & 0x80000000u) {
+            pt_leaf(ktris, tri_list, cur.u0, cur.u1, r, avoid, b, cnt);
+            flush();
+            has = false;
+            continue;
+        }
+        const uint32_t i0 = cur.u0, i1 = cur.u1;
+        const CFNode c0 = nodes[i0], c1 = nodes[i1];
+        cnt.node_visits += 2;
+        float w0, o0, w1, o1;
+        bool h0, h1;
+        if (c0.u0 & 0x80000000u) {
+            pt_box_bounds(c0, r, w0, o0);
+            h0 = true;
+        } else {
+            h0 = pt_box_decide(c0, r, w0, o0);
+        }
+        if (c1.u0 & 0x80000000u) {
+            pt_box_bounds(c1, r, w1, o1);
+            h1 = true;
+        } else {
+            h1 = pt_box_decide(c1, r, w1, o1);
+        }
+        h0 = h0 && !pruned(w0);
+        h1 = h1 && !pruned(w1);
+        if (h0 && h1) {
+            if (sp + 1 > kStackDepth) {
+                cnt.overflow = 1;
+                has = false;
+                sp = bot = 0;
+                continue;
+            }
+            const bool first0 = o0 <= o1;
+            wstack[(sp++) * 64 + lane] = first0 ? i1 : i0;
+            cur = first0 ? c0 : c1;
+        } else if (h0) {
+            cur = c0;
+        } else if (h1) {
+            cur = c1;
+        } else {
+            has = false;
+        }
+    }
+    flush();
+    __builtin_amdgcn_wave_barrier();
+    if (want) {
+        const unsigned long long key = keys[lane];
+        if (key != ~0ull) {
+            // the winner's hit point with pt_leaf's operations on the owner's ray
+            const int i = (int)(uint32_t)(key & 0xFFFFFFFFu);
+            const int idx = tri_list[i];
+            const float4 q0 = reinterpret_cast<const float4*>(ktris + idx)[0];
+            const v3 nn{q0.x, q0.y, q0.z};
+            const float k = dot(nn, ray.d);
+            const float sd = fdiv(q0.w - dot(nn, ray.o), k);
+            const float hz = __uint_as_float((uint32_t)(key >> 32));
+            out.hz = hz;
+            out.dist = fsqrt(hz);
+            out.i = i;
+            out.idx = idx;
+            out.hit = add(scale(ray.d, sd), ray.o);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 }  // namespace
 
 template <bool kQueue>
@@ -1425,6 +1593,8 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
     const int32_t* __restrict__ tri_list, CamRec cam, RenderLaunch L, float* __restrict__ out,
     unsigned long long* __restrict__ counters) {
     __shared__ uint32_t stacks[kWavesPerBlock][kStackDepth * 64];
+    __shared__ unsigned long long pt_keys[kWavesPerBlock][64];  // per-ray minima (cooperative traversal)
+    __shared__ int32_t pt_vlist[kWavesPerBlock][64];            // victims of a steal round
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     uint32_t* stack = &stacks[wave][lane];
@@ -1485,13 +1655,11 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
             bounce = 0;
             need_cam = false;
         }
-        if (!alive) continue;
-        ++cnt.segs;
-
         // BVH_IntersectTriangles (CUDAPathTracer.cu:192-352). Candidates merge on
         // (distance^2, position in the DFS triangle list): the reference's
         // first-in-DFS-order tie rule, so subtrees can be pruned once their
         // entry distance exceeds the best hit without changing the result.
+        // Every lane enters: lanes without a path help the others (pt_traverse_coop).
         PtBest best{3.40282347e+38f, 3.40282347e+38f, 0x7FFFFFFF, -1, v3{0.0f, 0.0f, 0.0f}};
         if (has_mesh) {
             PtRay r;
@@ -1505,8 +1673,15 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
             // coordinates involved), with a 10x margin.
             const float eps = 1e-5f * (1.0f + fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) + L.pt_scale);
             r.pad_t = v3{eps * fabsf(r.inv.x), eps * fabsf(r.inv.y), eps * fabsf(r.inv.z)};
-            pt_traverse(ktris, nodes, tri_list, stack, r, avoid, fsqrt(dot(d, d)), eps, best, cnt);
+#if RT_BVH_STEAL
+            pt_traverse_coop(ktris, nodes, tri_list, stack - lane, pt_keys[wave], pt_vlist[wave], lane, alive, r,
+                             avoid, fsqrt(dot(d, d)), eps, best, cnt);
+#else
+            if (alive) pt_traverse(ktris, nodes, tri_list, stack, r, avoid, fsqrt(dot(d, d)), eps, best, cnt);
+#endif
         }
+        if (!alive) continue;
+        ++cnt.segs;
         const int best_idx = best.idx;
         const v3 best_hit = best.hit;
         const uint32_t best_mat = best_idx >= 0 ? (uint32_t)ktris[best_idx].material : kDiffuse;
