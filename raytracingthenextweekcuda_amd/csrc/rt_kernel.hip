@@ -924,6 +924,111 @@ __global__ __launch_bounds__(256) void combine_kernel(RenderLaunch L, float* __r
     write_pixel(L, out, ((size_t)lrow * (size_t)L.width + (size_t)px) * 3, acc, (float)L.spp);
 }
 
+#ifndef RT_TAIL_STEAL
+#define RT_TAIL_STEAL 1  // lanes idle at the end of the queue take other lanes' last samples
+#endif
+
+// End (exclusive) of sub-stream c's sample sequence c, c + SP, ... < spp.
+__device__ __forceinline__ int sub_end(int spp, int c, int SP) {
+    return spp > c ? c + ((spp - c + SP - 1) / SP) * SP : c;
+}
+
+// A sample's path finished with radiance `contrib`. Owners fold it into the
+// item's sum in sample order (((p0 + p1) + p2) + ...); a thief holds it in `thr`
+// until its owner folds it in (tail_steal).
+__device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, int SP, uint32_t item, int own_end,
+                                            int& s, v3& sum, v3& thr, bool& alive, bool& need_cam, int towner,
+                                            bool& held, bool& waiting, uint32_t tl_pack) {
+    need_cam = true;
+    if (towner >= 0) {
+        thr = contrib;
+        held = true;
+        alive = false;
+        return;
+    }
+    sum = add(sum, contrib);
+    s += SP;
+    if (s >= own_end) {
+        alive = false;
+        if (L.queue) {
+            if (tl_pack) waiting = true;  // its last samples were taken by other lanes
+            else store_partial(L, item, sum);
+        }
+    }
+}
+
+// Tail stealing (work-queue launches, once the queue is dry; wave-uniform). The
+// sample sum of a sub-stream is a sequential fold, but the samples themselves are
+// independent (random-access RNG keyed by pixel and sample). An idle lane takes
+// the LAST unstarted sample of a lane that still has two or more to go, traces it
+// and holds its radiance; the owner, once its own samples are done, folds the
+// held values in sample order and writes the partial sum. The partial sums are
+// therefore bit-identical; only the tail of the launch gets shorter.
+[[maybe_unused]] __device__ __forceinline__ void tail_steal(const RenderLaunch& L, WaveLds& W, int lane, int SP, bool& alive,
+                                           bool& waiting, bool& held, int& towner, uint32_t& tl_pack,
+                                           int& own_end, int& c, int& s, int& px, int& y, uint32_t& pixel,
+                                           uint32_t item, v3& sum, v3& thr, bool& need_cam) {
+    // 1. owners whose stolen samples are all held fold them in and write the partial
+    if (__ballot(waiting || held) != 0) {
+        bool ready = true;
+        v3 vals[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int src = (int)((tl_pack >> (8 * k)) & 0xFFu) - 1;
+            const int sl = waiting && src >= 0 ? src : lane;
+            vals[k] = v3{__shfl(thr.x, sl, 64), __shfl(thr.y, sl, 64), __shfl(thr.z, sl, 64)};
+            const bool hd = __shfl((int)held, sl, 64) != 0;
+            if (waiting && src >= 0) ready = ready && hd;
+        }
+        if (waiting && ready) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if ((tl_pack >> (8 * k)) & 0xFFu) sum = add(sum, vals[k]);  // positions ascend with samples
+            store_partial(L, item, sum);
+            waiting = false;
+            tl_pack = 0;
+        }
+        // thieves whose owner has folded their value are free again
+        const uint32_t otp = (uint32_t)__shfl((int)tl_pack, towner >= 0 ? towner : lane, 64);
+        if (held && otp == 0u) {
+            held = false;
+            towner = -1;
+        }
+    }
+    // 2. pair the r-th idle lane with the r-th lane that has a spare (unstarted, not
+    //    current) sample; items of at most 4 samples (one byte per position in tl_pack)
+    const bool idle = !alive && !waiting && !held;
+    const bool spare = alive && towner < 0 && s + SP < own_end && sub_end(L.spp, c, SP) - c <= 4 * SP;
+    const uint64_t im = __ballot(idle), vm = __ballot(spare);
+    if (im == 0 || vm == 0) return;
+    const int nv = __popcll(vm), ni = __popcll(im);
+    const int ri = lane_rank(im), rv = lane_rank(vm);
+    if (spare) W.src[rv] = lane;
+    if (idle) W.key[ri] = (unsigned long long)lane;
+    __builtin_amdgcn_wave_barrier();
+    const bool thief = idle && ri < nv;
+    const int vic = thief ? W.src[ri] : lane;
+    const int v_end = __shfl(own_end, vic, 64), v_c = __shfl(c, vic, 64), v_px = __shfl(px, vic, 64);
+    const int v_y = __shfl(y, vic, 64);
+    const uint32_t v_pixel = (uint32_t)__shfl((int)pixel, vic, 64);
+    if (spare && rv < ni) {  // robbed: its last unstarted sample goes to the thief of the same rank
+        own_end -= SP;
+        const int pos = (own_end - c) / SP;
+        tl_pack |= ((uint32_t)W.key[rv] + 1u) << (8 * pos);
+    }
+    if (thief) {
+        towner = vic;
+        c = v_c;
+        s = v_end - SP;
+        px = v_px;
+        y = v_y;
+        pixel = v_pixel;
+        alive = true;
+        need_cam = true;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 template <bool kBvh, bool kQueue>
 __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
@@ -964,6 +1069,13 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     Counters cnt{0, 0, 0, 0, 0, 0, 0};
     int s = c;
     bool alive = valid && s < L.spp;
+    // the sub-stream's samples are c, c + SP, ... < own_end; at the end of the queue
+    // other lanes of the wave may take the last unstarted ones (tail stealing)
+    int own_end = sub_end(L.spp, c, SP);
+    uint32_t tl_pack = 0;  // owner: thief lane + 1 per stolen item position (8 bits each)
+    int towner = -1;       // thief: the lane whose sample it traces
+    bool held = false;     // thief: finished, its sample's radiance waits in `thr`
+    bool waiting = false;  // owner: own samples done, stolen ones not yet folded in
     bool need_cam = true;
     int depth = 0;
     Ray ray{{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 1.0f}, 0.0f};
@@ -985,26 +1097,27 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
                 s = c;
                 sum = v3{0.0f, 0.0f, 0.0f};
                 alive = s < L.spp;
+                own_end = sub_end(L.spp, c, SP);
                 // a sub-stream with no samples (S > spp) still owns its partial-sum slot
                 if (!alive) store_partial(L, item, sum);
                 need_cam = true;
             });
         }
-        if (__ballot(alive || (kQueue && !exhausted)) == 0) break;  // wave-uniform exit
+#if RT_TAIL_STEAL
+        if (kQueue && exhausted)
+            tail_steal(L, W, lane, SP, alive, waiting, held, towner, tl_pack, own_end, c, s, px, y, pixel, item,
+                       sum, thr, need_cam);
+#endif
+        if (__ballot(alive || waiting || held || (kQueue && !exhausted)) == 0) break;  // wave-uniform exit
         RT_STAMP(t_a);
         if (alive && need_cam) {
             ray = camera_sample(cam, L, rng, pixel, px, y, s, fw, fh);
             thr = v3{1.0f, 1.0f, 1.0f};
             depth = 0;
             need_cam = false;
-            if (L.max_depth <= 0) {  // rayColor with BOUNCES = 0 returns black
-                need_cam = true;
-                s += SP;
-                if (s >= L.spp) {
-                    alive = false;
-                    if (kQueue) store_partial(L, item, sum);
-                }
-            }
+            if (L.max_depth <= 0)  // rayColor with BOUNCES = 0 returns black
+                sample_done(L, v3{0.0f, 0.0f, 0.0f}, SP, item, own_end, s, sum, thr, alive, need_cam, towner,
+                            held, waiting, tl_pack);
         }
         const bool live = alive && !need_cam;
         RT_STAMP(t_b);
@@ -1115,15 +1228,9 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
             contrib = mul(thr, bg);
             done = true;
         }
-        if (done) {
-            sum = add(sum, contrib);
-            need_cam = true;
-            s += SP;
-            if (s >= L.spp) {
-                alive = false;
-                if (kQueue) store_partial(L, item, sum);
-            }
-        }
+        if (done)
+            sample_done(L, contrib, SP, item, own_end, s, sum, thr, alive, need_cam, towner, held, waiting,
+                        tl_pack);
 #ifdef RT_STAMPS
         {
             RT_STAMP(t_d);
