@@ -5,6 +5,7 @@
 // written against the C++ facade include/rtmi.hpp. Renders to materialball.ppm.
 //   ./materialball [device=0] [width=512] [height=512] [spp=32]
 //   device -1: load and process the mesh only (no GPU), print the census and exit.
+//   With a device the BVH is built by the GPU builder (rt_set_bvh_builder).
 #include <cstdio>
 #include <cstdlib>
 
@@ -22,11 +23,14 @@ int main(int argc, char** argv) {
         rtmi::Camera camera(eye, center, up, float(width) / height, 60.0f, 0.0f, 2.0f, 0.0f, 1.0f);
         ctx.setCamera(camera);
 
+        // on a GPU context the BVH is built on the device (byte-identical to the host build)
+        if (device >= 0) ctx.setBVHBuilder(RT_BVH_GPU);
         ctx.loadObject(RTMI_ASSETS "/models/materialball/materialball.ply", RT_PT_COAT);
         int32_t info[4];
         const Vector3Df offset(0.1f, 0.0f, -1.0f);
         ctx.check(rt_process_triangle_data(ctx.raw(), offset.data(), 1.0f, info));
-        std::printf("pathTrace scene: %d triangles, %d BVH nodes, depth %d\n", info[0], info[1], info[3]);
+        std::printf("pathTrace scene: %d triangles, %d BVH nodes, depth %d; BVH build %.2f ms (%s)\n", info[0],
+                    info[1], info[3], ctx.lastBVHBuildMs(), device >= 0 ? "GPU" : "host");
         if (device < 0) return 0;
 
         rtmi::Canvas canvas(width, height);

@@ -143,6 +143,14 @@ public:
                         c.aperture, c.focusDistance, c.time0, c.time1));
     }
     void commit() { check(rt_commit(ctx_)); }
+    // BVH builds of commit() / processTriangleData(): RT_BVH_HOST (Recurse on the host,
+    // BVH.cpp:94-497) or RT_BVH_GPU (its byte-identical GPU restatement).
+    void setBVHBuilder(int32_t builder) { check(rt_set_bvh_builder(ctx_, builder)); }
+    double lastBVHBuildMs() const {
+        double ms = 0.0;
+        check(rt_bvh_build_stats(ctx_, &ms, nullptr));
+        return ms;
+    }
 
     // pathTracing (main.cu:875-898): one frame of `spp` samples into the canvas,
     // with rayColor over the create* scene.
