@@ -98,3 +98,21 @@ def test_gpu_builder_declines_negative_zero():
         r.mesh(20, tris, 20)
         r.commit()
         assert r.bvh_build_stats()["gpu_builds"] == 0
+
+
+def test_gpu_builder_random_ply_byte_identical(tmp_path):
+    # 30k seeded random small triangles (deep, unbalanced splits): GPU == host builder
+    L = _lib.lib()
+    n = 30000
+    rng = np.random.RandomState(11)
+    c = rng.uniform(-1.0, 1.0, size=(n, 1, 3)) * np.array([1.0, 0.2, 0.6])
+    v = (c + rng.uniform(-0.02, 0.02, size=(n, 3, 3))).reshape(-1, 3)
+    path = tmp_path / "random.ply"
+    with open(path, "w") as fh:
+        fh.write(f"ply\nformat ascii 1.0\nelement vertex {3 * n}\nproperty float x\nproperty float y\n"
+                 f"property float z\nelement face {n}\nproperty list uchar int vertex_indices\nend_header\n")
+        fh.write("\n".join(f"{a:.6f} {b:.6f} {d:.6f}" for a, b, d in v) + "\n")
+        fh.write("\n".join(f"3 {3 * i} {3 * i + 1} {3 * i + 2}" for i in range(n)) + "\n")
+    img, _ = gpu_bvh_image(str(path), (0.2, -0.1, 0.0), 0.8)
+    assert img == bvh_image(str(path), (0.2, -0.1, 0.0), 0.8)
+    assert struct.unpack("<II", img[:8])[1] == n
