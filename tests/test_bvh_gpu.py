@@ -102,7 +102,6 @@ def test_gpu_builder_declines_negative_zero():
 
 def test_gpu_builder_random_ply_byte_identical(tmp_path):
     # 30k seeded random small triangles (deep, unbalanced splits): GPU == host builder
-    L = _lib.lib()
     n = 30000
     rng = np.random.RandomState(11)
     c = rng.uniform(-1.0, 1.0, size=(n, 1, 3)) * np.array([1.0, 0.2, 0.6])
