@@ -137,11 +137,22 @@ def cpu_baseline(args, threads: int):
     st1 = run(spp1, 1)
     dt1 = time.perf_counter() - t0
     frame_ms = dt * 1e3 * (args.width * args.height * args.spp) / (w * h * args.cpu_spp)
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
     return {
         "value": st["segments"] / dt / 1e6,
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
+        "cpu_model": model,
+        "host_cpus": os.cpu_count(),
         "value_1thread": st1["segments"] / dt1 / 1e6,
         "sample": (f"{args.scene} {w}x{h} spp={args.cpu_spp} depth={args.depth} (same camera; "
                    f"{w * h * args.cpu_spp} of the frame's {args.width * args.height * args.spp} samples), "
