@@ -132,9 +132,10 @@ rt_status rt_cube(rt_ctx* ctx, int32_t index, const float center[3], const float
 /* Constant-density medium bounded by an axis-aligned cube (build extension for
  * BASELINE config 5; the reference has no media). Boundary = the six two-sided
  * faces of rt_cube. Per segment: entry t1 (any t) and exit t2 (> t1 + 1e-4) of
- * the boundary; t1 clamps to 0.001; free flight hd = -ln(u) / density with u
- * from the medium's own counter-based draw (seed, pixel, sample, bounce, slot);
- * hit at t1 + hd/|d| when hd <= (t2 - t1)|d|; closest rule strict like planes. */
+ * the boundary; t1 clamps to 0.001; free flight hd = -ln(u) / density with u the
+ * sample's next uniform, drawn when the ray crosses the boundary (ConstantMedium's
+ * random_double(); media are tested in slot order, hit()'s order); hit at
+ * t1 + hd/|d| when hd <= (t2 - t1)|d|; closest rule strict like planes. */
 rt_status rt_constant_medium(rt_ctx* ctx, int32_t index, const float center[3],
                              const float extend[3], float density, int32_t material);
 /* Triangle mesh from world-space vertices, 9 floats per triangle

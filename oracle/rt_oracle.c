@@ -242,8 +242,6 @@ typedef struct Object {
     float neg_inv_density;
 } Object;
 
-/* Key of a segment's medium free-flight draws. */
-typedef struct { uint32_t seed, pixel, sample, bounce; } MediumKey;
 
 typedef struct {
     Material* mats;
@@ -389,15 +387,6 @@ static double ln_pos_d(float xf) {
     return (de * ln2_hi + ln_m) + de * ln2_lo;
 }
 
-/* One uniform per (pixel, sample, bounce, medium slot) from its own Philox
- * counter: independent of the order in which hit() meets the media. */
-static float medium_u01(const MediumKey* mk, uint32_t slot) {
-    uint32_t ctr[4] = {mk->sample, mk->bounce + 1u, slot, 0x6D656469u}, key[2] = {mk->seed, mk->pixel}, out[4];
-    philox(ctr, key, out);
-    const float inv = 2.3283064e-10f;
-    return (float)out[0] * inv + (inv / 2.0f);
-}
-
 /* Cube::hit over the six faces (Cube.cu:10-23). */
 static int cube_hit(const Object* o, const Ray* ray, float tmin, float tmax, HitResult* hr) {
     HitResult tmp;
@@ -413,10 +402,11 @@ static int cube_hit(const Object* o, const Ray* ray, float tmin, float tmax, Hit
     return any;
 }
 
-/* ConstantMedium::hit ("Ray Tracing: The Next Week") with the cube boundary and
- * the build's order-independent draw (rtmi.h rt_constant_medium). */
+/* ConstantMedium::hit ("Ray Tracing: The Next Week") with the cube boundary; a
+ * ray that crosses it draws the free-flight uniform from the sample's stream
+ * (random_double() there), in hit()'s slot order (rtmi.h rt_constant_medium). */
 static int medium_hit(const Object* o, const Ray* ray, float tmin, float tmax, HitResult* hr,
-                      const MediumKey* mk, int slot) {
+                      RandState* rs) {
     HitResult r1, r2;
     if (!cube_hit(o, ray, -INFINITY, INFINITY, &r1)) return 0;
     if (!cube_hit(o, ray, r1.t + 0.0001f, INFINITY, &r2)) return 0;
@@ -426,7 +416,7 @@ static int medium_hit(const Object* o, const Ray* ray, float tmin, float tmax, H
     if (t1 < 0) t1 = 0;
     float len = vlen(ray->direction);
     float inside = (t2 - t1) * len;
-    float hd = o->neg_inv_density * (float)ln_pos_d(medium_u01(mk, (uint32_t)slot));
+    float hd = o->neg_inv_density * (float)ln_pos_d(curand_uniform_(rs));
     if (hd > inside) return 0;
     float t = t1 + hd / len;
     if (!(t < tmax)) return 0;  /* closest rule: strict, like Plane::hit */
@@ -438,28 +428,28 @@ static int medium_hit(const Object* o, const Ray* ray, float tmin, float tmax, H
 }
 
 static int object_hit(const Object* o, const Ray* ray, float tmin, float tmax, HitResult* hr,
-                      uint64_t* tri_tests, const MediumKey* mk, int slot) {
+                      uint64_t* tri_tests, RandState* rs) {
     switch (o->type) {
     case O_SPHERE: return sphere_hit(o, o->center, ray, tmin, tmax, hr);
     case O_MOVING: return sphere_hit(o, moving_center(o, ray->time), ray, tmin, tmax, hr);
     case O_PLANE: return plane_hit(&o->plane, ray, tmin, tmax, hr);
     case O_MESH: return mesh_hit(o, ray, tmin, tmax, hr, tri_tests);
     case O_CUBE: return cube_hit(o, ray, tmin, tmax, hr);
-    case O_MEDIUM: return medium_hit(o, ray, tmin, tmax, hr, mk, slot);
+    case O_MEDIUM: return medium_hit(o, ray, tmin, tmax, hr, rs);
     }
     return 0;
 }
 
 /* hit (main.cu:43-57) */
 static int scene_hit(const Scene* s, const Ray* ray, float tmin, float tmax, HitResult* out,
-                     uint64_t* tri_tests, const MediumKey* mk) {
+                     uint64_t* tri_tests, RandState* rs) {
     HitResult tmp;
     memset(&tmp, 0, sizeof(tmp));
     int any = 0;
     float closest = tmax;
     for (int i = 0; i < s->n_objs; ++i) {
         const Object* o = &s->objs[i];
-        if (o->defined && object_hit(o, ray, tmin, closest, &tmp, tri_tests, mk, i)) {
+        if (o->defined && object_hit(o, ray, tmin, closest, &tmp, tri_tests, rs)) {
             any = 1;
             closest = tmp.t;
             *out = tmp;
@@ -528,8 +518,7 @@ static V3 ray_color(const Scene* s, Ray ray, int bounces, RandState* rs, uint64_
         h.t = -INFINITY;
         h.front_face = 1;
         ++*segs;
-        MediumKey mk = {seed, pixel, sample, (uint32_t)i};
-        if (scene_hit(s, &ray, ORC_EPS, INFINITY, &h, tri_tests, &mk)) {
+        if (scene_hit(s, &ray, ORC_EPS, INFINITY, &h, tri_tests, rs)) {
             V3 att;
             Ray sc;
             if (scatter(&s->mats[h.material], &ray, &h, &att, &sc, rs)) {
@@ -1024,8 +1013,9 @@ int orc_trace(const Scene* s, const float o[3], const float d[3], float time, fl
     HitResult h;
     memset(&h, 0, sizeof h);
     uint64_t tt = 0;
-    MediumKey mk = {0u, 0u, 0u, 0u};
-    int hit = scene_hit(s, &r, ORC_EPS, INFINITY, &h, &tt, &mk);
+    RandState rs;
+    rand_init(&rs, 0u, 0u, 0u);  /* a fixed stream for the media's free-flight draw */
+    int hit = scene_hit(s, &r, ORC_EPS, INFINITY, &h, &tt, &rs);
     if (hit) {
         *t = h.t; normal[0] = h.normal.x; normal[1] = h.normal.y; normal[2] = h.normal.z;
         *front = h.front_face; *material = h.material;

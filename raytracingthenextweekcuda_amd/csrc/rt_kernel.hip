@@ -631,16 +631,14 @@ __device__ __forceinline__ void sphere_group(const ObjRec* __restrict__ objs,
     }
 }
 
-// Key of a segment's medium free-flight draws (medium_u01).
-struct MediumKey {
-    uint32_t seed, pixel, sample, bounce;
-};
-
 // Constant medium bounded by a cube (rt_constant_medium, rtmi.h; "Ray Tracing:
 // The Next Week" ConstantMedium::hit with the boundary = the six two-sided faces
-// of createCube, kernels.h:139-154, each tested like Plane::hit). Returns the
-// scattering distance t, or NaN.
-__device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, const MediumKey& mk) {
+// of createCube, kernels.h:139-154, each tested like Plane::hit). A ray that
+// crosses the boundary draws its free-flight uniform from the sample's stream, as
+// ConstantMedium::hit calls random_double(); the scan visits media in slot order,
+// so the draw order is the sequential hit()'s. Returns the scattering distance t,
+// or NaN.
+__device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, Rng& rng) {
     const float* f = ob.f;
     const v3 c{f[0], f[1], f[2]}, e{f[3], f[4], f[5]};
     const v3 pos[6] = {{c.x - e.x, c.y, c.z}, {c.x + e.x, c.y, c.z}, {c.x, c.y + e.y, c.z},
@@ -687,7 +685,7 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
     if (t1c >= t2) return __builtin_nanf("");
     const float len = fsqrt(dot(d, d));
     const float inside = (t2 - t1c) * len;
-    const float u = medium_u01(mk.seed, mk.pixel, mk.sample, mk.bounce, ob.u0);
+    const float u = rng.next();
     const float hd = f[6] * (float)ln_pos_d(u);
     if (hd > inside) return __builtin_nanf("");
     return t1c + fdiv(hd, len);
@@ -699,7 +697,7 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
 // per-object tests are branch-free candidates merged with Hit's tie rule.
 template <bool kBvh>
 __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v3 inv, bool live,
-                                           const MediumKey& mk, WaveLds& W, uint32_t* stack, int lane,
+                                           Rng& rng, WaveLds& W, uint32_t* stack, int lane,
                                            Counters& cnt
 #ifdef RT_STAMPS
                                            , uint64_t* tm
@@ -760,7 +758,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
 #endif
             }
         } else if (ob.type == kObjMedium) {
-            h.merge(live ? medium_candidate(ob, o, d, mk) : __builtin_nanf(""), ob.order, false, i, -1);
+            h.merge(live ? medium_candidate(ob, o, d, rng) : __builtin_nanf(""), ob.order, false, i, -1);
         } else if (kBvh) {  // kObjSphereGroup
             sphere_group(S.objs, S.nodes, ob.u2, live, ray, inv, h, stack, cnt);
         }
@@ -1129,8 +1127,7 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
 #endif
 
         const v3 inv = rcp(ray.d);
-        const MediumKey mk{L.seed, pixel, L.sample_offset + (uint32_t)s, (uint32_t)depth};
-        const Hit h = closest_hit<kBvh>(S, ray, inv, live, mk, W, stack, lane, cnt
+        const Hit h = closest_hit<kBvh>(S, ray, inv, live, rng, W, stack, lane, cnt
 #ifdef RT_STAMPS
                                         , tm
 #endif

@@ -319,12 +319,4 @@ RT_HD float pt_powf(float xf, float yf) {
     return (float)ldexp(q, (int)n);
 }
 
-// Free-flight draw of a constant medium: one uniform per (pixel, sample,
-// bounce, medium slot) from its own Philox counter, so the draw does not
-// depend on the order in which the closest-hit scan meets the media.
-RT_HD float medium_u01(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce,
-                       uint32_t slot) {
-    return u01(philox4x32_10(u4{sample, bounce + 1u, slot, 0x6D656469u}, seed, pixel).x);
-}
-
 }  // namespace rt

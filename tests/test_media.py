@@ -1,7 +1,7 @@
 """Participating media (BASELINE config 5; a build extension: the reference has
 no media). Semantics are those of "Ray Tracing: The Next Week" ConstantMedium +
-isotropic with a cube boundary and an order-independent free-flight draw
-(include/rtmi.h rt_constant_medium). Parity is against the CPU restatement
+isotropic with a cube boundary and the free-flight draw taken from the
+sample's stream in slot order (include/rtmi.h rt_constant_medium). Parity is against the CPU restatement
 only: unpinned against the reference, which has no such code."""
 import math
 import os
