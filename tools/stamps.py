@@ -16,7 +16,7 @@ lanes = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 W = H = 512
 (rtmi.cornell_box1 if scene == "cb1" else rtmi.bunny_cornell_box)(r, W, H)
 spp = 128 if scene == "cb1" else 16
-r.render(W, H, spp, 8, row_block=8, row_rank=0, row_world=world, lanes_per_pixel=lanes)
+r.render(W, H, spp, 8, row_block=2, row_rank=0, row_world=world, lanes_per_pixel=lanes)
 st = r.stats()
 d = st["debug"]
 tot = d[0] + d[1] + d[2]
