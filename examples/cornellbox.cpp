@@ -58,6 +58,7 @@ int main(int argc, char** argv) {
         rt_render_stats st;
         ctx.check(rt_sync_stats(ctx.raw(), &st));
         canvas.writeToPPM("cornellbox.ppm");
+        canvas.writeToPNG("cornellbox.png");
         std::printf("rendered %dx%d spp=%d: %.3f ms, %.1f Mrays/s\n", width, height, spp, st.kernel_ms,
                     st.segments / (st.kernel_ms * 1e3));
     } catch (const rtmi::Error& e) {

@@ -24,6 +24,8 @@
 #include <cstdio>
 #include <memory>
 #include <stdexcept>
+#include <algorithm>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -102,6 +104,67 @@ public:
         if (!f) throw Error(RT_ERR_IO, "cannot write " + path);
         std::fprintf(f, "P6\n%d %d\n255\n", width, height);
         for (int32_t y = height - 1; y >= 0; --y) std::fwrite(&px[(size_t)y * width * 3], 1, (size_t)width * 3, f);
+        std::fclose(f);
+    }
+    // writeToPNG (Canvas.h:141-154, stbi_write_png with the rows flipped): RGB8, top row
+    // first, zlib stream of stored (uncompressed) deflate blocks - no codec dependency.
+    void writeToPNG(const std::string& path) const {
+        std::vector<uint8_t> px = pixels();
+        std::vector<uint8_t> raw;  // filter byte 0 + one top-down row
+        raw.reserve((size_t)height * ((size_t)width * 3 + 1));
+        for (int32_t y = height - 1; y >= 0; --y) {
+            raw.push_back(0);
+            raw.insert(raw.end(), px.begin() + (size_t)y * width * 3, px.begin() + (size_t)(y + 1) * width * 3);
+        }
+        std::vector<uint8_t> z{0x78, 0x01};
+        for (size_t off = 0; off < raw.size() || off == 0; off += 65535) {
+            const size_t n = std::min<size_t>(65535, raw.size() - off);
+            z.push_back(off + n >= raw.size() ? 1 : 0);  // BFINAL, BTYPE = 00 (stored)
+            z.push_back((uint8_t)(n & 0xFF));
+            z.push_back((uint8_t)(n >> 8));
+            z.push_back((uint8_t)(~n & 0xFF));
+            z.push_back((uint8_t)((~n >> 8) & 0xFF));
+            z.insert(z.end(), raw.begin() + off, raw.begin() + off + n);
+            if (n == 0) break;
+        }
+        uint32_t a = 1, b = 0;  // Adler-32 of the uncompressed data
+        for (uint8_t v : raw) {
+            a = (a + v) % 65521u;
+            b = (b + a) % 65521u;
+        }
+        for (int k = 3; k >= 0; --k) z.push_back((uint8_t)(((b << 16) | a) >> (8 * k)));
+        FILE* f = std::fopen(path.c_str(), "wb");
+        if (!f) throw Error(RT_ERR_IO, "cannot write " + path);
+        static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
+        std::fwrite(sig, 1, 8, f);
+        auto be32 = [](uint8_t* o, uint32_t v) {
+            for (int k = 0; k < 4; ++k) o[k] = (uint8_t)(v >> (24 - 8 * k));
+        };
+        auto chunk = [&](const char* tag, const std::vector<uint8_t>& data) {
+            uint8_t hdr[8];
+            be32(hdr, (uint32_t)data.size());
+            std::memcpy(hdr + 4, tag, 4);
+            std::fwrite(hdr, 1, 8, f);
+            if (!data.empty()) std::fwrite(data.data(), 1, data.size(), f);
+            uint32_t crc = 0xFFFFFFFFu;  // CRC-32 over tag + data
+            auto upd = [&](uint8_t v) {
+                crc ^= v;
+                for (int k = 0; k < 8; ++k) crc = (crc >> 1) ^ (0xEDB88320u & (0u - (crc & 1u)));
+            };
+            for (int k = 0; k < 4; ++k) upd((uint8_t)tag[k]);
+            for (uint8_t v : data) upd(v);
+            uint8_t c[4];
+            be32(c, crc ^ 0xFFFFFFFFu);
+            std::fwrite(c, 1, 4, f);
+        };
+        std::vector<uint8_t> ihdr(13, 0);
+        be32(ihdr.data(), (uint32_t)width);
+        be32(ihdr.data() + 4, (uint32_t)height);
+        ihdr[8] = 8;  // bit depth
+        ihdr[9] = 2;  // colour type RGB
+        chunk("IHDR", ihdr);
+        chunk("IDAT", z);
+        chunk("IEND", {});
         std::fclose(f);
     }
 

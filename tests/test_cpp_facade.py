@@ -49,3 +49,44 @@ def test_facade_pathtrace_renders_on_gpu(pt_binary, tmp_path):
     assert "Mrays/s" in out
     data = (tmp_path / "materialball.ppm").read_bytes()
     assert data.startswith(b"P6\n48 32\n255\n") and len(data) == len(b"P6\n48 32\n255\n") + 48 * 32 * 3
+
+
+def test_facade_png_writer_matches_ppm(tmp_path):
+    # Canvas::writeToPNG (stored-deflate PNG, no codec dependency) carries the same
+    # gamma'd top-down rows as writeToPPM; decoded here with zlib
+    import struct
+    import zlib
+
+    src = tmp_path / "png_check.cpp"
+    src.write_text(r'''
+#include "rtmi.hpp"
+int main() {
+    rtmi::Canvas c(37, 300);  // > 65535 raw bytes: several stored blocks
+    for (int i = 0; i < 37 * 300 * 3; ++i) c.data()[i] = (float)((i * 7919) % 1000) / 999.0f;
+    c.writeToPPM("out.ppm");
+    c.writeToPNG("out.png");
+    return 0;
+}
+''')
+    exe = tmp_path / "png_check"
+    lib = os.path.join(S.REPO, "raytracingthenextweekcuda_amd")
+    subprocess.run(["g++", "-O1", "-std=c++17", f"-I{os.path.join(S.REPO, 'include')}", str(src), "-o", str(exe),
+                    f"-L{lib}", "-lrtmi", f"-Wl,-rpath,{lib}"], check=True)
+    subprocess.run([str(exe)], check=True, cwd=tmp_path)
+    png = (tmp_path / "out.png").read_bytes()
+    assert png[:8] == b"\x89PNG\r\n\x1a\n"
+    chunks, off = {}, 8
+    while off < len(png):
+        n, tag = struct.unpack(">I4s", png[off:off + 8])
+        data = png[off + 8:off + 8 + n]
+        assert struct.unpack(">I", png[off + 8 + n:off + 12 + n])[0] == zlib.crc32(tag + data)
+        chunks[tag] = data
+        off += 12 + n
+    w, h, depth, ctype = struct.unpack(">IIBB", chunks[b"IHDR"][:10])
+    assert (w, h, depth, ctype) == (37, 300, 8, 2)
+    raw = zlib.decompress(chunks[b"IDAT"])
+    rows = [raw[y * (w * 3 + 1):(y + 1) * (w * 3 + 1)] for y in range(h)]
+    assert all(r[0] == 0 for r in rows)
+    ppm = (tmp_path / "out.ppm").read_bytes()
+    header = b"P6\n37 300\n255\n"
+    assert ppm.startswith(header) and b"".join(r[1:] for r in rows) == ppm[len(header):]
