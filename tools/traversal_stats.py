@@ -25,3 +25,16 @@ for name, make, w, h, depth in [("bunny", rtmi.bunny_cornell_box, 1024, 1024, 8)
               f"per segment: nodes {best['node_visits'] / seg:.2f} tris {best['tri_tests'] / seg:.2f} "
               f"mesh boxes {best['box_tests'] / seg:.2f} grp spheres "
               f"{(best['group_sphere_tests'] + best['group_moving_sphere_tests']) / seg:.2f}", flush=True)
+
+# pathTrace (the reference's committed integrator): materialball through its exact BVH decisions
+with rtmi.Renderer(0) as r:
+    rtmi.materialball(r, 512, 512)
+    best = None
+    for _ in range(2):
+        r.render(512, 512, spp, 5, lanes_per_pixel=0, integrator="pathTrace")
+        st = r.stats()
+        best = st if best is None or st["kernel_ms"] < best["kernel_ms"] else best
+    seg = best["segments"]
+    print(f"materialball pathTrace 512x512 spp {spp}: {best['kernel_ms']:.2f} ms, "
+          f"{seg / best['kernel_ms'] / 1e6:.2f} Gseg/s, per segment: nodes {best['node_visits'] / seg:.2f} "
+          f"tris {best['tri_tests'] / seg:.2f}", flush=True)
