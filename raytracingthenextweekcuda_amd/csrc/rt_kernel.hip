@@ -869,7 +869,7 @@ constexpr int kQueueShards = RT_QUEUE_SHARDS;
 static_assert(kQueueShards * 32 <= kQueueHeadWords, "queue heads");
 constexpr int kQueueStride = 32;  // u32 words between heads
 #ifndef RT_QUEUE_REFILL
-#define RT_QUEUE_REFILL 4  // idle lanes that trigger a refill (or all lanes idle); measured 1/2/4/8/16/32
+#define RT_QUEUE_REFILL 8  // idle lanes that trigger a refill (or all lanes idle); measured 1-32: 4 best before tail stealing, 8 after
 #endif
 
 // Wave-wide dequeue from shard `sh`: every lane in `need` gets an item index,
