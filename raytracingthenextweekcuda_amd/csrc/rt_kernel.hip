@@ -6,19 +6,25 @@
 // (Camera.h:151-168) + cuRAND (main.cu:120-129) with one hand-written kernel.
 //
 // Execution model:
-//  * lanes own pixels (or 1/S of a pixel's samples, lanes_per_pixel = S); a
-//    256-thread workgroup covers a 2x2 block of per-wave pixel tiles;
+//  * a persistent grid takes work items (pixel, sub-stream of S = lanes_per_pixel)
+//    from 8 sharded queue heads (one per XCD band); each lane folds its
+//    sub-stream's samples in order and stores a partial sum, and combine_kernel
+//    sums a pixel's S partials in a fixed order (the static grid, RTMI_QUEUE=0,
+//    computes the same sums for A/B);
 //  * path regeneration: a lane whose path terminates starts its next sample in
-//    the same loop trip, so lanes stay busy until their last sample;
+//    the same loop trip, so lanes stay busy until their last sample; once the
+//    queue is dry, idle lanes trace other lanes' last samples (tail stealing);
 //  * the main loop is wave-uniform (exits on an empty __ballot of live lanes),
 //    so the whole wave is available for cooperative work inside a trip;
 //  * small meshes (the reference's brute-force TriangleMesh) are tested with
-//    ballot compaction: the (ray, triangle) pairs of the lanes whose rays hit
-//    the mesh box are packed densely over all 64 lanes, and per-ray results are
-//    merged with a 64-bit LDS atomic-min on (t, triangle index);
-//  * large meshes use the reference's binned-SAH BVH (BVH.cpp) with a per-lane
-//    traversal stack resident in LDS (32 entries x 64 lanes per wave, laid out
-//    so lane i always hits bank i);
+//    two-phase ballot compaction: the (ray, triangle) pairs of the lanes whose
+//    rays hit the mesh box are packed densely over all 64 lanes, backface-culled,
+//    then fully tested in batches; per-ray results merge with a 64-bit LDS
+//    atomic-min on (t, triangle index);
+//  * large meshes and the pathTrace triangles use the reference's binned-SAH BVH
+//    (BVH.cpp) with per-lane traversal stacks in LDS (32 entries x 64 lanes per
+//    wave, lane i always on bank i) and cooperative traversal: idle lanes steal
+//    pending subtrees, per-ray minima merge by LDS atomic-min;
 //  * scene records of the closest-hit scan are read at wave-uniform addresses
 //    (scalar loads broadcast to 64 lanes); materials/nodes per lane;
 //  * counter-based RNG (rt_math.h): no init kernel and no RNG state in HBM.
