@@ -78,3 +78,16 @@ def test_gamma_u8_matches_canvas_gamma():
     a = rtmi.gamma_u8(x)
     assert np.array_equal(a, orc.gamma_u8(x))
     assert a[1] == 255 and a[0] == 0 and a[4] == 127  # 255.99*0.5
+
+
+def test_missing_library_fails_loudly():
+    # the product path has no fallback: without librtmi.so the renderer refuses to start
+    import subprocess
+    import sys
+
+    code = ("import raytracingthenextweekcuda_amd as r\n"
+            "try:\n    r.Renderer(0)\nexcept ImportError as e:\n    print('IMPORT_ERROR', e)\n")
+    env = dict(os.environ, RTMI_LIB="/nonexistent/librtmi.so")
+    out = subprocess.run([sys.executable, "-c", code], cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert "IMPORT_ERROR" in out.stdout and "no fallback" in out.stdout, out.stdout + out.stderr
