@@ -692,7 +692,11 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
     const float len = fsqrt(dot(d, d));
     const float inside = (t2 - t1c) * len;
     const float u = rng.next();
+#ifdef RT_ABL_FLOATLOG  // ablation only: float log (results differ)
+    const float hd = f[6] * __logf(u);
+#else
     const float hd = f[6] * (float)ln_pos_d(u);
+#endif
     if (hd > inside) return __builtin_nanf("");
     return t1c + fdiv(hd, len);
 }
