@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RTMI_ABI_VERSION 6
+#define RTMI_ABI_VERSION 7
 
 typedef int32_t rt_status;
 enum {
@@ -212,6 +212,27 @@ rt_status rt_commit(rt_ctx* ctx);
  * [6] BVH nodes, [7] spheres placed behind the object BVH (the counts
  * [1]/[2] include them). */
 rt_status rt_scene_info(const rt_ctx* ctx, int32_t out[8]);
+/* FNV-1a 64 digest of the committed host tables (objects, triangles, materials,
+ * BVH nodes, triangle maps, camera): two scene builds that agree on it upload
+ * identical device data. Works on device -1 contexts. */
+rt_status rt_scene_digest(const rt_ctx* ctx, uint64_t* out);
+
+/* ---- scene files ----
+ * initialize() for SCENE == 1 (main.cu:623-786): reads a scene YAML of the
+ * reference's schema (the .yaml files under resources/scenes) with a built-in block-style
+ * reader (the reference links yaml-cpp 0.7.0) and creates its camera,
+ * materials and objects without committing:
+ *   camera: eye, center, up, fov, aperture; focus = |center - eye|, aspect =
+ *     float(width) / height, shutter [0, 1] (main.cu:632-638);
+ *   materials 0-8 pre-created first (main.cu:643-651), so a YAML material whose
+ *     id is taken is ignored (the nullptr guards, main.cu:714-744);
+ *   object slot i = list position; the primitive type is the first field of
+ *     the object's map (main.cu:706, 749): 0 sphere, 1 plane, 2 mesh (OBJ with
+ *     scale/rotate/offset; meshes use materials[3], main.cu:781), and the build
+ *     extensions 3 cube, 4 constant medium, `.ply` meshes (offset, maxCoord).
+ * Model paths are relative to `models_dir`. Parse errors name the line. */
+rt_status rt_load_yaml_scene(rt_ctx* ctx, const char* path, const char* models_dir, int32_t width,
+                             int32_t height);
 
 /* ---- render (renderKernel, main.cu:160-206, launched by pathTracing 875-898) ----
  * Output: float32 RGB mean radiance (color / spp, BEFORE Canvas::gamma). */

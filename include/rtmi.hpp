@@ -206,6 +206,17 @@ public:
                         c.aperture, c.focusDistance, c.time0, c.time1));
     }
     void commit() { check(rt_commit(ctx_)); }
+    // initialize() for SCENE == 1 (main.cu:623-786): camera, pre-seeded materials
+    // and objects of a scene YAML; model paths relative to modelsDir. The
+    // materials()/objects() tables are not updated: query rt_material_defined.
+    void loadYAMLScene(const std::string& path, const std::string& modelsDir, int32_t width, int32_t height) {
+        check(rt_load_yaml_scene(ctx_, path.c_str(), modelsDir.c_str(), width, height));
+    }
+    uint64_t sceneDigest() const {
+        uint64_t h = 0;
+        check(rt_scene_digest(ctx_, &h));
+        return h;
+    }
     // BVH builds of commit() / processTriangleData(): RT_BVH_HOST (Recurse on the host,
     // BVH.cpp:94-497) or RT_BVH_GPU (its byte-identical GPU restatement).
     void setBVHBuilder(int32_t builder) { check(rt_set_bvh_builder(ctx_, builder)); }

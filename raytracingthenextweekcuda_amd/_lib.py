@@ -23,7 +23,7 @@ STATUS_NAMES = {
 }
 
 # Every symbol include/rtmi.h declares (checked by tests/test_abi.py).
-ABI_VERSION = 6  # include/rtmi.h RTMI_ABI_VERSION
+ABI_VERSION = 7  # include/rtmi.h RTMI_ABI_VERSION
 
 EXPORTS = [
     "rt_abi_version", "rt_create", "rt_destroy", "rt_last_error", "rt_clear_scene",
@@ -33,7 +33,8 @@ EXPORTS = [
     "rt_cube", "rt_mesh", "rt_mesh_obj", "rt_mesh_triangle_count", "rt_mesh_vertices",
     "rt_mesh_ply", "rt_ply_bvh_image", "rt_load_object", "rt_process_triangle_data",
     "rt_pathtrace_bvh_image", "rt_set_bvh_builder", "rt_bvh_build_stats", "rt_ply_bvh_image_gpu",
-    "rt_camera", "rt_commit", "rt_scene_info", "rt_render", "rt_render_device", "rt_sync_stats",
+    "rt_camera", "rt_commit", "rt_scene_info", "rt_scene_digest", "rt_load_yaml_scene",
+    "rt_render", "rt_render_device", "rt_sync_stats",
     "rt_render_u8", "rt_accumulate", "rt_render_multi", "rt_gamma_u8",
 ]
 
@@ -124,6 +125,8 @@ def lib():
     L.rt_camera.argtypes = [vp, fp, fp, fp] + [C.c_float] * 6
     L.rt_commit.argtypes = [vp]
     L.rt_scene_info.argtypes = [vp, C.POINTER(C.c_int32)]
+    L.rt_scene_digest.argtypes = [vp, C.POINTER(C.c_uint64)]
+    L.rt_load_yaml_scene.argtypes = [vp, C.c_char_p, C.c_char_p, i32, i32]
     L.rt_render.argtypes = [vp, C.POINTER(RenderParams), fp]
     L.rt_render_device.argtypes = [vp, C.POINTER(RenderParams), vp, vp]
     L.rt_sync_stats.argtypes = [vp, C.POINTER(RenderStats)]

@@ -18,6 +18,7 @@
 #include "rt_bvh.h"
 #include "rt_kernel.h"
 #include "rt_scene.h"
+#include "rt_yaml.h"
 
 struct rt_ctx {
     int device = -1;
@@ -843,6 +844,215 @@ rt_status rt_gamma_u8(const float* rgb, int64_t n, uint8_t* out) {
         float v = fmaxf(0.0f, fminf(sqrtf(rgb[i]), 0.999f));
         out[i] = (uint8_t)(uint32_t)(255.99f * v);
     }
+    return RT_OK;
+}
+
+}  // extern "C"
+
+// ---- scene files (initialize(), main.cu:623-786, SCENE == 1) ----
+
+namespace {
+
+namespace Y = rt::yaml;
+
+bool vec3(const Y::Node* n, float out[3]) {
+    if (!n || n->kind != Y::Node::kSeq || n->seq.size() != 3) return false;
+    for (int k = 0; k < 3; ++k) {
+        double v;
+        if (!Y::as_double(n->seq[k], v)) return false;
+        out[k] = (float)v;
+    }
+    return true;
+}
+
+// Python-style int(x) of a YAML int or float scalar (the reference reads these
+// fields with as<int>()).
+bool int_of(const Y::Node* n, long& out) {
+    if (!n) return false;
+    if (Y::as_int(*n, out)) return true;
+    double v;
+    if (!Y::as_double(*n, v)) return false;
+    out = (long)v;
+    return true;
+}
+
+bool float_of(const Y::Node* n, float& out) {
+    double v;
+    if (!n || !Y::as_double(*n, v)) return false;
+    out = (float)v;
+    return true;
+}
+
+bool bool_of(const Y::Node* n, bool& out) {
+    if (!n) return false;
+    if (Y::as_bool(*n, out)) return true;
+    double v;
+    if (!Y::as_double(*n, v)) return false;
+    out = v != 0.0;
+    return true;
+}
+
+std::string where(const Y::Node* n, const std::string& what) {
+    return "line " + std::to_string(n ? n->line : 0) + ": " + what;
+}
+
+}  // namespace
+
+extern "C" {
+
+rt_status rt_load_yaml_scene(rt_ctx* c, const char* path, const char* models_dir, int32_t width,
+                             int32_t height) {
+    if (!c) return RT_ERR_INVALID;
+    if (!path || !models_dir) return fail(c, RT_ERR_INVALID, "null path");
+    if (width < 1 || height < 1) return fail(c, RT_ERR_INVALID, "width and height must be >= 1");
+    Y::Node root;
+    std::string e = Y::parse_file(path, root);
+    if (!e.empty()) return fail(c, e.rfind("cannot open", 0) == 0 ? RT_ERR_IO : RT_ERR_INVALID, e);
+    const Y::Node* cam = root.get("camera");
+    const Y::Node* objects = root.get("objects");
+    if (!cam || cam->kind != Y::Node::kMap) return fail(c, RT_ERR_INVALID, "scene has no camera map");
+
+    // camera (main.cu:632-638): focus = |center - eye| in float, aspect = float(w) / h
+    float eye[3], center[3], up[3], fov, aperture;
+    if (!vec3(cam->get("eye"), eye) || !vec3(cam->get("center"), center) || !vec3(cam->get("up"), up) ||
+        !float_of(cam->get("fov"), fov) || !float_of(cam->get("aperture"), aperture))
+        return fail(c, RT_ERR_INVALID, where(cam, "camera needs eye, center, up, fov and aperture"));
+    const float dx = center[0] - eye[0], dy = center[1] - eye[1], dz = center[2] - eye[2];
+    const float focus = sqrtf(dx * dx + dy * dy + dz * dz);
+    const float aspect = (float)width / (float)height;
+    if (!objects || objects->kind != Y::Node::kSeq) return fail(c, RT_ERR_INVALID, "scene has no objects list");
+    rt_status s = rt_camera(c, eye, center, up, aspect, fov, aperture, focus, 0.0f, 1.0f);
+    if (s != RT_OK) return s;
+
+    // materials 0-8 exist before any object (main.cu:643-651)
+    const float red[3] = {1, 0, 0}, green[3] = {0, 1, 0}, blue[3] = {0, 0, 1}, white[3] = {1, 1, 1};
+    const float wl[3] = {0.75f, 0.25f, 0.25f}, wr[3] = {0.25f, 0.25f, 0.75f};
+    if ((s = rt_material_lambertian(c, 0, red, 1.0f)) || (s = rt_material_lambertian(c, 1, green, 1.0f)) ||
+        (s = rt_material_lambertian(c, 2, blue, 1.0f)) || (s = rt_material_lambertian(c, 3, white, 1.0f)) ||
+        (s = rt_material_lambertian(c, 4, wl, 1.0f)) || (s = rt_material_lambertian(c, 5, wr, 1.0f)) ||
+        (s = rt_material_metal(c, 6, white, 0.0f)) || (s = rt_material_dielectric(c, 7, 1.5f)) ||
+        (s = rt_material_emission(c, 8, white, 5.0f)))
+        return s;
+
+    for (size_t i = 0; i < objects->seq.size(); ++i) {
+        const Y::Node& entry = objects->seq[i];
+        if (entry.kind != Y::Node::kMap || entry.map.empty() || entry.map[0].second.kind != Y::Node::kMap ||
+            entry.map[0].second.map.empty())
+            return fail(c, RT_ERR_INVALID, where(&entry, "object entry must be 'kind: {type: ...}'"));
+        const Y::Node& obj = entry.map[0].second;  // the first key names the object (main.cu:706)
+        const Y::Node* mat = obj.get("material");
+        long mid, mtype, ptype;
+        if (!mat || !int_of(obj.get("materialId"), mid) || !int_of(mat->get("type"), mtype))
+            return fail(c, RT_ERR_INVALID, where(&obj, "object needs materialId and material.type"));
+        if (mid < 0 || mid > INT32_MAX) return fail(c, RT_ERR_INVALID, where(&obj, "materialId out of range"));
+        if (!rt_material_defined(c, (int32_t)mid)) {  // the nullptr guards (main.cu:714-744)
+            float albedo[3], p;
+            if (mtype == 0 || mtype == 1 || mtype == 3 || mtype == 4) {
+                if (!vec3(mat->get("albedo"), albedo))
+                    return fail(c, RT_ERR_INVALID, where(mat, "material needs albedo"));
+            }
+            if (mtype == 0) {
+                s = rt_material_lambertian(c, (int32_t)mid, albedo, 1.0f);
+            } else if (mtype == 2) {
+                if (!float_of(mat->get("indexOfRefraction"), p))
+                    return fail(c, RT_ERR_INVALID, where(mat, "dielectric needs indexOfRefraction"));
+                s = rt_material_dielectric(c, (int32_t)mid, p);
+            } else if (mtype == 1) {
+                if (!float_of(mat->get("fuzz"), p)) return fail(c, RT_ERR_INVALID, where(mat, "metal needs fuzz"));
+                s = rt_material_metal(c, (int32_t)mid, albedo, p);
+            } else if (mtype == 3) {
+                if (!float_of(mat->get("intensity"), p))
+                    return fail(c, RT_ERR_INVALID, where(mat, "emission needs intensity"));
+                s = rt_material_emission(c, (int32_t)mid, albedo, p);
+            } else if (mtype == 4) {  // build extension: isotropic phase function
+                s = rt_material_isotropic(c, (int32_t)mid, albedo);
+            }
+            if (s != RT_OK) return s;
+        }
+        // the primitive type is the object map's first value (main.cu:749)
+        if (!int_of(&obj.map[0].second, ptype))
+            return fail(c, RT_ERR_INVALID, where(&obj, "the first field must be the primitive type"));
+        const int32_t idx = (int32_t)i, m = (int32_t)mid;
+        float a[3], b[3], d[3], f;
+        if (ptype == 0) {
+            if (!vec3(obj.get("center"), a) || !float_of(obj.get("radius"), f))
+                return fail(c, RT_ERR_INVALID, where(&obj, "sphere needs center and radius"));
+            s = rt_sphere(c, idx, a, f, m, 1);
+        } else if (ptype == 1) {
+            long orient;
+            bool two;
+            if (!vec3(obj.get("position"), a) || !vec3(obj.get("normal"), b) || !vec3(obj.get("extend"), d) ||
+                !int_of(obj.get("orientation"), orient) || !bool_of(obj.get("twoSide"), two))
+                return fail(c, RT_ERR_INVALID,
+                            where(&obj, "plane needs position, normal, extend, orientation and twoSide"));
+            s = rt_plane(c, idx, a, b, d, m, (int32_t)orient, two ? 1 : 0);
+        } else if (ptype == 2) {
+            const Y::Node* model = obj.get("model");
+            if (!model || model->kind != Y::Node::kScalar)
+                return fail(c, RT_ERR_INVALID, where(&obj, "mesh needs a model path"));
+            const std::string file = std::string(models_dir) + "/" + model->scalar;
+            std::string lower = file;
+            for (char& ch : lower) ch = (char)tolower((unsigned char)ch);
+            // meshes always take materials[3] (main.cu:781)
+            if (lower.size() >= 4 && lower.compare(lower.size() - 4, 4, ".ply") == 0) {
+                // build extension: PLY meshes with loadObject/processTriangleData placement
+                float off[3] = {0, 0, 0}, max_coord = 1.0f;
+                if (obj.get("offset") && !vec3(obj.get("offset"), off))
+                    return fail(c, RT_ERR_INVALID, where(&obj, "bad offset"));
+                if (obj.get("maxCoord") && !float_of(obj.get("maxCoord"), max_coord))
+                    return fail(c, RT_ERR_INVALID, where(&obj, "bad maxCoord"));
+                s = rt_mesh_ply(c, idx, file.c_str(), off, max_coord, 3);
+            } else {
+                if (!vec3(obj.get("scale"), a) || !vec3(obj.get("rotate"), b) || !vec3(obj.get("offset"), d))
+                    return fail(c, RT_ERR_INVALID, where(&obj, "OBJ mesh needs scale, rotate and offset"));
+                s = rt_mesh_obj(c, idx, file.c_str(), a, b, d, 3);
+            }
+        } else if (ptype == 3) {  // build extension: cube (createCube, kernels.h:139-154)
+            if (!vec3(obj.get("center"), a) || !vec3(obj.get("extend"), d))
+                return fail(c, RT_ERR_INVALID, where(&obj, "cube needs center and extend"));
+            s = rt_cube(c, idx, a, d, m);
+        } else if (ptype == 4) {  // build extension: constant medium in a cube
+            if (!vec3(obj.get("center"), a) || !vec3(obj.get("extend"), d) || !float_of(obj.get("density"), f))
+                return fail(c, RT_ERR_INVALID, where(&obj, "medium needs center, extend and density"));
+            s = rt_constant_medium(c, idx, a, d, f, m);
+        } else {
+            return fail(c, RT_ERR_INVALID, where(&obj, "unknown primitive type " + std::to_string(ptype)));
+        }
+        if (s != RT_OK) return s;
+    }
+    return RT_OK;
+}
+
+rt_status rt_scene_digest(const rt_ctx* c, uint64_t* out) {
+    if (!c || !out) return RT_ERR_INVALID;
+    if (!c->committed) return RT_ERR_STATE;
+    uint64_t h = 1469598103934665603ull;  // FNV-1a 64
+    auto mix = [&h](const void* p, size_t n) {
+        const unsigned char* b = (const unsigned char*)p;
+        for (size_t k = 0; k < n; ++k) {
+            h ^= b[k];
+            h *= 1099511628211ull;
+        }
+    };
+    const auto& S = c->scene;
+    const uint64_t sizes[5] = {S.objs.size(), S.tris.size(), S.mats.size(), S.nodes.size(), S.tri_orig.size()};
+    mix(sizes, sizeof(sizes));
+    mix(&S.n_scan, sizeof(S.n_scan));
+    if (!S.objs.empty()) mix(S.objs.data(), S.objs.size() * sizeof(S.objs[0]));
+    if (!S.tris.empty()) mix(S.tris.data(), S.tris.size() * sizeof(S.tris[0]));
+    for (const rt::MatRec& m : S.mats) {  // padding words excluded
+        mix(&m.type, 4);
+        mix(&m.a0, 16);
+    }
+    if (!S.nodes.empty()) mix(S.nodes.data(), S.nodes.size() * sizeof(S.nodes[0]));
+    if (!S.tri_orig.empty()) mix(S.tri_orig.data(), S.tri_orig.size() * sizeof(S.tri_orig[0]));
+    const rt::CamRec& k = S.camera;
+    const float cam[21] = {k.origin.x, k.origin.y, k.origin.z, k.lower_left.x, k.lower_left.y, k.lower_left.z,
+                           k.horizontal.x, k.horizontal.y, k.horizontal.z, k.vertical.x, k.vertical.y, k.vertical.z,
+                           k.right.x, k.right.y, k.right.z, k.true_up.x, k.true_up.y, k.true_up.z,
+                           k.lens_radius, k.time0, k.time1};
+    mix(cam, sizeof(cam));
+    *out = h;
     return RT_OK;
 }
 

@@ -230,6 +230,18 @@ class Renderer:
                 "grouped_spheres"]
         return {k: int(out[i]) for i, k in enumerate(keys)}
 
+    def scene_digest(self) -> int:
+        """FNV-1a 64 digest of the committed host tables (rt_scene_digest)."""
+        out = C.c_uint64()
+        self._check(self.L.rt_scene_digest(self.ctx, C.byref(out)))
+        return int(out.value)
+
+    def load_yaml_native(self, path, width, height, models_dir):
+        """The scene file through the library's own reader (rt_load_yaml_scene,
+        initialize() of main.cu:623-786); does not commit."""
+        self._check(self.L.rt_load_yaml_scene(self.ctx, str(path).encode(), str(models_dir).encode(),
+                                              int(width), int(height)))
+
     # ---- render ----
     @staticmethod
     def params(width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,

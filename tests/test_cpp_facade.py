@@ -90,3 +90,46 @@ int main() {
     ppm = (tmp_path / "out.ppm").read_bytes()
     header = b"P6\n37 300\n255\n"
     assert ppm.startswith(header) and b"".join(r[1:] for r in rows) == ppm[len(header):]
+
+
+@pytest.fixture(scope="module")
+def cli_binary():
+    subprocess.run(["make", "-s", "-C", EX, "rtmi_render"], check=True)
+    return os.path.join(EX, "rtmi_render")
+
+
+def test_native_cli_scene_digest_matches_python_loader(cli_binary):
+    # examples/rtmi_render reads the YAML with the library's own reader
+    import raytracingthenextweekcuda_amd as rtmi
+
+    path = os.path.join(S.SCENES, "suzanne_cornellbox.yaml")
+    out = subprocess.run([cli_binary, path, "--device", "-1", "--width", "96", "--height", "64"], check=True,
+                         capture_output=True, text=True).stdout
+    r = rtmi.Renderer(-1)
+    rtmi.load_yaml_scene(r, path, 96, 64)
+    want = r.scene_digest()
+    r.close()
+    assert f"digest {want:016x}" in out, out
+    bad = subprocess.run([cli_binary, os.path.join(S.SCENES, "scene.yaml"), "--device", "-1"],
+                         capture_output=True, text=True)
+    assert bad.returncode == 1 and "line 167" in bad.stderr
+
+
+@pytest.mark.gpu
+def test_native_cli_renders_the_python_frame(cli_binary, tmp_path):
+    # main()-style native program vs the Python host layer: same scene, same frame, same bytes
+    import raytracingthenextweekcuda_amd as rtmi
+    from raytracingthenextweekcuda_amd.canvas import Canvas
+
+    path = os.path.join(S.SCENES, "cornellbox0.yaml")
+    w, h, spp, depth = 64, 48, 4, 6
+    subprocess.run([cli_binary, path, "--width", str(w), "--height", str(h), "--spp", str(spp), "--depth",
+                    str(depth), "--out", str(tmp_path / "native.ppm")], check=True, capture_output=True)
+    with rtmi.Renderer(0) as r:
+        rtmi.load_yaml_scene(r, path, w, h)
+        img = r.render(w, h, spp, depth, lanes_per_pixel=0)
+    want = Canvas(w, h).pixels(img)[::-1].reshape(-1)  # writeToPPM's rows: top first
+    data = (tmp_path / "native.ppm").read_bytes()
+    head = f"P6\n{w} {h}\n255\n".encode()
+    assert data.startswith(head)
+    assert data[len(head):] == want.astype("uint8").tobytes()
