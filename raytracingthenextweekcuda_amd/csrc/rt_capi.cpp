@@ -651,20 +651,29 @@ static rt_status launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLa
         const uint64_t tiles = (uint64_t)L.tiles_x * (uint64_t)((L.local_rows + 7) / 8);
         const uint64_t items = tiles * 64u * (uint64_t)L.lanes_per_pixel;
         const size_t bytes = (size_t)items * 3 * sizeof(float);
-        if (items < 0xFFFFFFFFull && bytes <= ((size_t)1 << 30)) {
-            if (bytes > c->d_partial_bytes) {
-                (void)hipFree(c->d_partial);
-                c->d_partial = nullptr;
-                c->d_partial_bytes = 0;
-                RT_HIP(c, hipMalloc(&c->d_partial, bytes));
+        // partial sums: 12 B per item (up to a few GB of the 288 GB HBM); a frame whose
+        // items do not fit the 32-bit item index or the allocation runs on the static grid
+        bool have = items < 0xFFFFFFFFull && bytes <= ((size_t)16 << 30);
+        if (have && bytes > c->d_partial_bytes) {
+            (void)hipFree(c->d_partial);
+            c->d_partial = nullptr;
+            c->d_partial_bytes = 0;
+            if (hipMalloc(&c->d_partial, bytes) == hipSuccess) {
                 c->d_partial_bytes = bytes;
+            } else {
+                (void)hipGetLastError();  // clear the sticky allocation error
+                have = false;
             }
+        }
+        if (have) {
             L.queue = rt::queue_blocks(c->n_cu);
             L.n_items = (uint32_t)items;
             L.partial = c->d_partial;
             RT_HIP(c, hipMemsetAsync(c->d_queue, 0, rt::kQueueHeadWords * sizeof(uint32_t), st));
         }
     }
+    if (L.queue == 0 && L.lanes_per_pixel > 64)  // the static grid keeps a pixel's sub-streams in one wave
+        return fail(c, RT_ERR_INVALID, "lanes_per_pixel > 64 needs the work queue, which this frame does not fit");
     const bool keep = (p->flags & RT_RENDER_KEEP_COUNTERS) != 0;
     if (!keep) RT_HIP(c, hipMemsetAsync(c->d_counters, 0, rt::kNumCounters * sizeof(unsigned long long), st));
     RT_HIP(c, hipEventRecord(c->ev0, st));

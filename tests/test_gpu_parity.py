@@ -134,6 +134,11 @@ def test_render_errors(rtmi):
             r.render(8, 8, 0, 1)
         with pytest.raises(RTError, match="RT_ERR_INVALID"):
             r.render(8, 8, 1, 1, row_rank=2, row_world=2)
+        # 8192^2 pixels x 128 sub-streams exceed the 32-bit item index: the static grid
+        # cannot hold 128 sub-streams of a pixel in one wave, so the launch is refused
+        rtmi.cornell_box1(r, 8192, 8192)
+        with pytest.raises(RTError, match="needs the work queue"):
+            r.render(8192, 8192, 128, 1, lanes_per_pixel=128)
 
 
 def test_render_into_torch_buffer(rtmi):
