@@ -72,6 +72,14 @@ public:
 private:
     std::vector<Line> L;
     size_t i = 0;
+    int depth = 0;  // nesting guard: scene files nest 4 levels; hostile input must not exhaust the stack
+    static constexpr int kMaxDepth = 128;
+
+    struct Nest {
+        int& d;
+        explicit Nest(int& x) : d(x) { ++d; }
+        ~Nest() { --d; }
+    };
 
     static bool is_item(const std::string& t) { return t == "-" || (t.size() > 1 && t[0] == '-' && t[1] == ' '); }
 
@@ -81,6 +89,8 @@ private:
     }
 
     std::string flow(const std::string& v, size_t& p, int line, Node& out) {
+        Nest guard(depth);
+        if (depth > kMaxDepth) return err_at(line, "nesting too deep");
         skip_ws(v, p);
         out = Node{};
         out.line = line;
@@ -166,6 +176,8 @@ private:
     }
 
     std::string block(size_t start, int indent, Node& out) {
+        Nest guard(depth);
+        if (depth > kMaxDepth) return err_at(L[start].number, "nesting too deep");
         i = start;
         out = Node{};
         out.line = L[i].number;

@@ -109,3 +109,24 @@ def test_native_reader_errors_name_the_problem(tmp_path, text, needle):
 
 def test_missing_scene_file_is_an_io_error():
     assert "RT_ERR_IO" in _native_error("/nonexistent/scene.yaml")
+
+
+def test_reader_survives_mutation_fuzzing_under_sanitizers(tmp_path):
+    """Host-code sanitizers (ASan + UBSan) over the reader with random mutations of
+    every scene file and hostile nesting (tools/yaml_fuzz.cpp)."""
+    import shutil
+    import subprocess
+
+    if shutil.which("g++") is None:
+        pytest.skip("g++ not available")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "yaml_fuzz"
+    subprocess.run(["g++", "-std=c++17", "-g", "-O1", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-I" + os.path.join(repo, "raytracingthenextweekcuda_amd", "csrc"),
+                    os.path.join(repo, "tools", "yaml_fuzz.cpp"),
+                    os.path.join(repo, "raytracingthenextweekcuda_amd", "csrc", "rt_yaml.cpp"), "-o", str(exe)],
+                   check=True)
+    files = sorted(glob.glob(os.path.join(SCENES_DIR, "*.yaml")))
+    out = subprocess.run([str(exe), "400"] + files, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "mutants parsed" in out.stdout
