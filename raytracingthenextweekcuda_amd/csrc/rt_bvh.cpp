@@ -251,8 +251,9 @@ std::string load_ply(const std::string& path, PlyMesh& out) {
                 nf = (unsigned)strtoul(line.c_str() + 12, nullptr, 10);
             } else if (line.compare(0, 10, "end_header") == 0) {
                 inside = true;
-                out.vertices.reserve(nv);
-                out.indices.reserve((size_t)nf * 3);
+                // header counts are untrusted: reserve at most 16M entries up front
+                out.vertices.reserve(std::min<size_t>(nv, (size_t)1 << 24));
+                out.indices.reserve(std::min<size_t>((size_t)nf * 3, (size_t)3 << 24));
             }
         } else if (nv) {
             --nv;

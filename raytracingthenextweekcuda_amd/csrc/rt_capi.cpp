@@ -11,6 +11,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <new>
+#include <stdexcept>
 #include <chrono>
 #include <string>
 #include <vector>
@@ -345,7 +347,7 @@ rt_status rt_cube(rt_ctx* c, int32_t index, const float center[3], const float e
     return RT_OK;
 }
 
-rt_status rt_mesh(rt_ctx* c, int32_t index, const float* v, int32_t n_tris, int32_t material) {
+static rt_status rt_mesh_impl(rt_ctx* c, int32_t index, const float* v, int32_t n_tris, int32_t material) {
     if (!c) return RT_ERR_INVALID;
     if (n_tris < 0 || (n_tris > 0 && !v)) return fail(c, RT_ERR_INVALID, "mesh: bad vertex array");
     for (int64_t i = 0; i < (int64_t)n_tris * 9; ++i)
@@ -360,7 +362,7 @@ rt_status rt_mesh(rt_ctx* c, int32_t index, const float* v, int32_t n_tris, int3
     return RT_OK;
 }
 
-rt_status rt_mesh_obj(rt_ctx* c, int32_t index, const char* path, const float scale[3],
+static rt_status rt_mesh_obj_impl(rt_ctx* c, int32_t index, const char* path, const float scale[3],
                       const float rotate[3], const float offset[3], int32_t material) {
     if (!c) return RT_ERR_INVALID;
     if (!path || !finite3(scale) || !finite3(rotate) || !finite3(offset))
@@ -373,7 +375,7 @@ rt_status rt_mesh_obj(rt_ctx* c, int32_t index, const char* path, const float sc
     return rt_mesh(c, index, verts.data(), (int32_t)(verts.size() / 9), material);
 }
 
-rt_status rt_mesh_ply(rt_ctx* c, int32_t index, const char* path, const float offset[3],
+static rt_status rt_mesh_ply_impl(rt_ctx* c, int32_t index, const char* path, const float offset[3],
                       float max_coord, int32_t material) {
     if (!c) return RT_ERR_INVALID;
     if (!path || !finite3(offset) || !isfinite(max_coord) || max_coord <= 0.0f)
@@ -392,7 +394,7 @@ rt_status rt_mesh_ply(rt_ctx* c, int32_t index, const char* path, const float of
     return rt_mesh(c, index, verts.data(), (int32_t)(verts.size() / 9), material);
 }
 
-rt_status rt_ply_bvh_image(const char* path, const float offset[3], float max_coord,
+static rt_status rt_ply_bvh_image_impl(const char* path, const float offset[3], float max_coord,
                            uint8_t* out, int64_t capacity, int64_t* size) {
     if (!path || !finite3(offset) || !size || !(max_coord > 0.0f)) return RT_ERR_INVALID;
     rt::PlyMesh m;
@@ -406,7 +408,7 @@ rt_status rt_ply_bvh_image(const char* path, const float offset[3], float max_co
     return RT_OK;
 }
 
-rt_status rt_ply_bvh_image_gpu(int32_t device, const char* path, const float offset[3], float max_coord,
+static rt_status rt_ply_bvh_image_gpu_impl(int32_t device, const char* path, const float offset[3], float max_coord,
                                uint8_t* out, int64_t capacity, int64_t* size, double* build_ms) {
     if (device < 0 || !path || !finite3(offset) || !size || !(max_coord > 0.0f)) return RT_ERR_INVALID;
     rt::PlyMesh m;
@@ -445,7 +447,7 @@ int32_t rt_mesh_triangle_count(const rt_ctx* c, int32_t index) {
     return (int32_t)(o.tri_vertices.size() / 9);
 }
 
-rt_status rt_mesh_vertices(const rt_ctx* c, int32_t index, float* out, int32_t max_tris) {
+static rt_status rt_mesh_vertices_impl(const rt_ctx* c, int32_t index, float* out, int32_t max_tris) {
     int32_t n = rt_mesh_triangle_count(c, index);
     if (!c || !out || n == 0) return RT_ERR_INVALID;
     if (max_tris < n) return RT_ERR_INVALID;
@@ -454,7 +456,7 @@ rt_status rt_mesh_vertices(const rt_ctx* c, int32_t index, float* out, int32_t m
 }
 
 // ---- pathTrace scene (main.cu:404-553) ----
-rt_status rt_load_object(rt_ctx* c, const char* path, int32_t reflection_type) {
+static rt_status rt_load_object_impl(rt_ctx* c, const char* path, int32_t reflection_type) {
     if (!c) return RT_ERR_INVALID;
     if (!path || reflection_type < RT_PT_DIFFUSE || reflection_type > RT_PT_COAT)
         return fail(c, RT_ERR_INVALID, "load_object: bad arguments");
@@ -465,7 +467,7 @@ rt_status rt_load_object(rt_ctx* c, const char* path, int32_t reflection_type) {
     return RT_OK;
 }
 
-rt_status rt_process_triangle_data(rt_ctx* c, const float offset[3], float max_coord,
+static rt_status rt_process_triangle_data_impl(rt_ctx* c, const float offset[3], float max_coord,
                                    int32_t out_info[4]) {
     if (!c) return RT_ERR_INVALID;
     if (!finite3(offset) || !isfinite(max_coord) || max_coord <= 0.0f)
@@ -516,7 +518,7 @@ rt_status rt_process_triangle_data(rt_ctx* c, const float offset[3], float max_c
     return RT_OK;
 }
 
-rt_status rt_pathtrace_bvh_image(const rt_ctx* c, uint8_t* out, int64_t capacity, int64_t* size) {
+static rt_status rt_pathtrace_bvh_image_impl(const rt_ctx* c, uint8_t* out, int64_t capacity, int64_t* size) {
     if (!c || !size) return RT_ERR_INVALID;
     if (!c->pt_ready) return RT_ERR_STATE;
     std::vector<uint8_t> img = rt::bvh_image(c->pt_bvh);
@@ -539,7 +541,7 @@ rt_status rt_camera(rt_ctx* c, const float eye[3], const float center[3], const 
     return RT_OK;
 }
 
-rt_status rt_commit(rt_ctx* c) {
+static rt_status rt_commit_impl(rt_ctx* c) {
     if (!c) return RT_ERR_INVALID;
     std::string e = c->scene.flatten();
     if (!e.empty()) return fail(c, RT_ERR_INVALID, e);
@@ -694,7 +696,7 @@ static rt_status launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLa
     return RT_OK;
 }
 
-rt_status rt_render_device(rt_ctx* c, const rt_render_params* p, float* out, void* stream) {
+static rt_status rt_render_device_impl(rt_ctx* c, const rt_render_params* p, float* out, void* stream) {
     if (!c) return RT_ERR_INVALID;
     rt::RenderLaunch L;
     rt_status s = validate(c, p, L);
@@ -703,7 +705,7 @@ rt_status rt_render_device(rt_ctx* c, const rt_render_params* p, float* out, voi
     return launch(c, p, L, out, (hipStream_t)stream);
 }
 
-rt_status rt_accumulate(rt_ctx* c, const rt_render_params* p, float* accum, uint32_t sample_count,
+static rt_status rt_accumulate_impl(rt_ctx* c, const rt_render_params* p, float* accum, uint32_t sample_count,
                         uint8_t* pixels, void* stream) {
     if (!c) return RT_ERR_INVALID;
     rt::RenderLaunch L;
@@ -742,7 +744,7 @@ rt_status rt_sync_stats(rt_ctx* c, rt_render_stats* out) {
     return RT_OK;
 }
 
-rt_status rt_render(rt_ctx* c, const rt_render_params* p, float* out_host) {
+static rt_status rt_render_impl(rt_ctx* c, const rt_render_params* p, float* out_host) {
     if (!c) return RT_ERR_INVALID;
     rt::RenderLaunch L;
     rt_status s = validate(c, p, L);
@@ -767,7 +769,7 @@ rt_status rt_render(rt_ctx* c, const rt_render_params* p, float* out_host) {
     return RT_OK;
 }
 
-rt_status rt_render_multi(rt_ctx* const* ctxs, int32_t n, const rt_render_params* p, float* out_host) {
+static rt_status rt_render_multi_impl(rt_ctx* const* ctxs, int32_t n, const rt_render_params* p, float* out_host) {
     if (!ctxs || n < 1 || !p || !out_host) return RT_ERR_INVALID;
     for (int32_t k = 0; k < n; ++k)
         if (!ctxs[k]) return RT_ERR_INVALID;
@@ -813,7 +815,7 @@ rt_status rt_render_multi(rt_ctx* const* ctxs, int32_t n, const rt_render_params
     return RT_OK;
 }
 
-rt_status rt_render_u8(rt_ctx* c, const rt_render_params* p, uint8_t* out_host) {
+static rt_status rt_render_u8_impl(rt_ctx* c, const rt_render_params* p, uint8_t* out_host) {
     if (!c) return RT_ERR_INVALID;
     rt::RenderLaunch L;
     rt_status s = validate(c, p, L);
@@ -909,7 +911,7 @@ std::string where(const Y::Node* n, const std::string& what) {
 
 extern "C" {
 
-rt_status rt_load_yaml_scene(rt_ctx* c, const char* path, const char* models_dir, int32_t width,
+static rt_status rt_load_yaml_scene_impl(rt_ctx* c, const char* path, const char* models_dir, int32_t width,
                              int32_t height) {
     if (!c) return RT_ERR_INVALID;
     if (!path || !models_dir) return fail(c, RT_ERR_INVALID, "null path");
@@ -1065,4 +1067,176 @@ rt_status rt_scene_digest(const rt_ctx* c, uint64_t* out) {
     return RT_OK;
 }
 
+}  // extern "C"
+
+// Exceptions must not cross the C ABI: host-side allocations (scene tables, BVH
+// builds, file loaders) report RT_ERR_OOM instead of terminating the caller.
+extern "C" {
+
+rt_status rt_mesh(rt_ctx* c, int32_t index, const float* v, int32_t n_tris, int32_t material) {
+    try {
+        return rt_mesh_impl(c, index, v, n_tris, material);
+    } catch (const std::bad_alloc&) {
+        return fail(c, RT_ERR_OOM, "out of host memory");
+    } catch (const std::exception& ex) {
+        return fail(c, RT_ERR_INVALID, std::string("internal error: ") + ex.what());
+    }
+}
+
+rt_status rt_mesh_obj(rt_ctx* c, int32_t index, const char* path, const float scale[3],
+                      const float rotate[3], const float offset[3], int32_t material) {
+    try {
+        return rt_mesh_obj_impl(c, index, path, scale, rotate, offset, material);
+    } catch (const std::bad_alloc&) {
+        return fail(c, RT_ERR_OOM, "out of host memory");
+    } catch (const std::exception& ex) {
+        return fail(c, RT_ERR_INVALID, std::string("internal error: ") + ex.what());
+    }
+}
+
+rt_status rt_mesh_ply(rt_ctx* c, int32_t index, const char* path, const float offset[3],
+                      float max_coord, int32_t material) {
+    try {
+        return rt_mesh_ply_impl(c, index, path, offset, max_coord, material);
+    } catch (const std::bad_alloc&) {
+        return fail(c, RT_ERR_OOM, "out of host memory");
+    } catch (const std::exception& ex) {
+        return fail(c, RT_ERR_INVALID, std::string("internal error: ") + ex.what());
+    }
+}
+
+rt_status rt_ply_bvh_image(const char* path, const float offset[3], float max_coord,
+                           uint8_t* out, int64_t capacity, int64_t* size) {
+    try {
+        return rt_ply_bvh_image_impl(path, offset, max_coord, out, capacity, size);
+    } catch (const std::bad_alloc&) {
+        return RT_ERR_OOM;
+    } catch (const std::exception&) {
+        return RT_ERR_INVALID;
+    }
+}
+
+rt_status rt_ply_bvh_image_gpu(int32_t device, const char* path, const float offset[3], float max_coord,
+                               uint8_t* out, int64_t capacity, int64_t* size, double* build_ms) {
+    try {
+        return rt_ply_bvh_image_gpu_impl(device, path, offset, max_coord, out, capacity, size, build_ms);
+    } catch (const std::bad_alloc&) {
+        return RT_ERR_OOM;
+    } catch (const std::exception&) {
+        return RT_ERR_INVALID;
+    }
+}
+
+rt_status rt_load_object(rt_ctx* c, const char* path, int32_t reflection_type) {
+    try {
+        return rt_load_object_impl(c, path, reflection_type);
+    } catch (const std::bad_alloc&) {
+        return fail(c, RT_ERR_OOM, "out of host memory");
+    } catch (const std::exception& ex) {
+        return fail(c, RT_ERR_INVALID, std::string("internal error: ") + ex.what());
+    }
+}
+
+rt_status rt_process_triangle_data(rt_ctx* c, const float offset[3], float max_coord,
+                                   int32_t out_info[4]) {
+    try {
+        return rt_process_triangle_data_impl(c, offset, max_coord, out_info);
+    } catch (const std::bad_alloc&) {
+        return fail(c, RT_ERR_OOM, "out of host memory");
+    } catch (const std::exception& ex) {
+        return fail(c, RT_ERR_INVALID, std::string("internal error: ") + ex.what());
+    }
+}
+
+rt_status rt_pathtrace_bvh_image(const rt_ctx* c, uint8_t* out, int64_t capacity, int64_t* size) {
+    try {
+        return rt_pathtrace_bvh_image_impl(c, out, capacity, size);
+    } catch (const std::bad_alloc&) {
+        return RT_ERR_OOM;
+    } catch (const std::exception&) {
+        return RT_ERR_INVALID;
+    }
+}
+
+rt_status rt_commit(rt_ctx* c) {
+    try {
+        return rt_commit_impl(c);
+    } catch (const std::bad_alloc&) {
+        return fail(c, RT_ERR_OOM, "out of host memory");
+    } catch (const std::exception& ex) {
+        return fail(c, RT_ERR_INVALID, std::string("internal error: ") + ex.what());
+    }
+}
+
+rt_status rt_load_yaml_scene(rt_ctx* c, const char* path, const char* models_dir, int32_t width,
+                             int32_t height) {
+    try {
+        return rt_load_yaml_scene_impl(c, path, models_dir, width, height);
+    } catch (const std::bad_alloc&) {
+        return fail(c, RT_ERR_OOM, "out of host memory");
+    } catch (const std::exception& ex) {
+        return fail(c, RT_ERR_INVALID, std::string("internal error: ") + ex.what());
+    }
+}
+
+rt_status rt_render(rt_ctx* c, const rt_render_params* p, float* out_host) {
+    try {
+        return rt_render_impl(c, p, out_host);
+    } catch (const std::bad_alloc&) {
+        return fail(c, RT_ERR_OOM, "out of host memory");
+    } catch (const std::exception& ex) {
+        return fail(c, RT_ERR_INVALID, std::string("internal error: ") + ex.what());
+    }
+}
+
+rt_status rt_render_device(rt_ctx* c, const rt_render_params* p, float* out, void* stream) {
+    try {
+        return rt_render_device_impl(c, p, out, stream);
+    } catch (const std::bad_alloc&) {
+        return fail(c, RT_ERR_OOM, "out of host memory");
+    } catch (const std::exception& ex) {
+        return fail(c, RT_ERR_INVALID, std::string("internal error: ") + ex.what());
+    }
+}
+
+rt_status rt_render_u8(rt_ctx* c, const rt_render_params* p, uint8_t* out_host) {
+    try {
+        return rt_render_u8_impl(c, p, out_host);
+    } catch (const std::bad_alloc&) {
+        return fail(c, RT_ERR_OOM, "out of host memory");
+    } catch (const std::exception& ex) {
+        return fail(c, RT_ERR_INVALID, std::string("internal error: ") + ex.what());
+    }
+}
+
+rt_status rt_accumulate(rt_ctx* c, const rt_render_params* p, float* accum, uint32_t sample_count,
+                        uint8_t* pixels, void* stream) {
+    try {
+        return rt_accumulate_impl(c, p, accum, sample_count, pixels, stream);
+    } catch (const std::bad_alloc&) {
+        return fail(c, RT_ERR_OOM, "out of host memory");
+    } catch (const std::exception& ex) {
+        return fail(c, RT_ERR_INVALID, std::string("internal error: ") + ex.what());
+    }
+}
+
+rt_status rt_render_multi(rt_ctx* const* ctxs, int32_t n, const rt_render_params* p, float* out_host) {
+    try {
+        return rt_render_multi_impl(ctxs, n, p, out_host);
+    } catch (const std::bad_alloc&) {
+        return RT_ERR_OOM;
+    } catch (const std::exception&) {
+        return RT_ERR_INVALID;
+    }
+}
+
+rt_status rt_mesh_vertices(const rt_ctx* c, int32_t index, float* out, int32_t max_tris) {
+    try {
+        return rt_mesh_vertices_impl(c, index, out, max_tris);
+    } catch (const std::bad_alloc&) {
+        return RT_ERR_OOM;
+    } catch (const std::exception&) {
+        return RT_ERR_INVALID;
+    }
+}
 }  // extern "C"

@@ -49,6 +49,25 @@ def test_missing_ply_is_an_error():
     assert L.rt_ply_bvh_image(b"/nonexistent.ply", (C.c_float * 3)(), 1.0, None, 0, C.byref(size)) == 3
 
 
+def _ply(tmp_path, nv, nf, body):
+    p = tmp_path / "t.ply"
+    p.write_text(f"ply\nformat ascii 1.0\nelement vertex {nv}\nproperty float x\nproperty float y\n"
+                 f"property float z\nelement face {nf}\nproperty list uchar int vertex_indices\nend_header\n" + body)
+    L = _lib.lib()
+    size = C.c_int64()
+    return L.rt_ply_bvh_image(str(p).encode(), (C.c_float * 3)(), 1.0, None, 0, C.byref(size))
+
+
+def test_hostile_ply_headers_are_handled(tmp_path):
+    tri = "0 0 0\n1 0 0\n0 1 0\n"
+    assert _ply(tmp_path, 3, 1, tri + "3 0 1 2\n") == 0
+    # a face index beyond the vertices is an error, not an out-of-bounds read
+    assert _ply(tmp_path, 3, 1, tri + "3 0 1 7\n") != 0
+    # header counts of 4e9 (48 GB if reserved up front) over a 3-vertex body: the
+    # call returns a status instead of throwing std::bad_alloc through the C ABI
+    assert _ply(tmp_path, 4000000000, 4000000000, tri + "3 0 1 2\n") in (0, 1)
+
+
 def test_fast_split_search_equals_reference_search():
     # the builder's O(N log N) split search (sorted prefix/suffix boxes) must give
     # Recurse's tree byte for byte; RTMI_BVH_REFERENCE_SEARCH=1 runs the
