@@ -294,11 +294,14 @@ bool as_int(const Node& n, long& out) {
 bool as_bool(const Node& n, bool& out) {
     if (n.kind != Node::kScalar) return false;
     const std::string& s = n.scalar;
-    if (s == "true" || s == "True" || s == "TRUE") {
+    // YAML 1.1 booleans, as PyYAML resolves them
+    if (s == "true" || s == "True" || s == "TRUE" || s == "yes" || s == "Yes" || s == "YES" || s == "on" ||
+        s == "On" || s == "ON") {
         out = true;
         return true;
     }
-    if (s == "false" || s == "False" || s == "FALSE") {
+    if (s == "false" || s == "False" || s == "FALSE" || s == "no" || s == "No" || s == "NO" || s == "off" ||
+        s == "Off" || s == "OFF") {
         out = false;
         return true;
     }

@@ -40,6 +40,18 @@ def test_native_reader_builds_the_same_scene(path, w, h):
     assert _native_digest(path, w, h) == _python_digest(path, w, h)
 
 
+@pytest.mark.parametrize("true_word,false_word", [("yes", "no"), ("On", "Off"), ("TRUE", "False")])
+def test_native_reader_yaml11_booleans(tmp_path, true_word, false_word):
+    # twoSide spelled with other YAML 1.1 booleans: PyYAML and the reader agree
+    src = os.path.join(SCENES_DIR, "cornellbox1.yaml")
+    text = open(src).read().replace("twoSide: true", f"twoSide: {true_word}")
+    text = text.replace("twoSide: false", f"twoSide: {false_word}")
+    p = tmp_path / "b.yaml"
+    p.write_text(text)
+    assert yaml.safe_load(text) == yaml.safe_load(open(src).read())
+    assert _native_digest(str(p), 64, 64) == _python_digest(src, 64, 64)
+
+
 def test_digest_sees_the_camera_aspect():
     path = os.path.join(SCENES_DIR, "cornellbox1.yaml")
     assert _native_digest(path, 512, 512)[0] != _native_digest(path, 640, 512)[0]
