@@ -1,5 +1,5 @@
-"""Parity at BASELINE.json's full sizes (SURVEY §8(d) configs C2-C5 and the committed
-pathTrace setup), on the frames bench.py renders.
+"""Parity at BASELINE.json's full sizes (the committed pathTrace
+setup and the published-timing Suzanne scene), on the frames bench.py renders.
 
 The GPU renders each full frame with the automatic sub-stream layout, as the bench
 does. Two checks follow.
@@ -29,9 +29,13 @@ THREADS = min(16, os.cpu_count() or 1)
 
 # scene: (product loader, yaml / json for the oracle, W, H, spp, depth, spot-row tile K, tile ranks)
 CONFIGS = {
+    # C1 is the reference's CPU-runnable case: the oracle renders the whole frame (K = 1)
+    "C1_cornellbox1": ("cornell_box1", "cornellbox1.yaml", 256, 256, 4, 4, 1, (0,)),
     "C2_cornellbox1": ("cornell_box1", "cornellbox1.yaml", 512, 512, 128, 8, 32, (0, 21)),
     "C3_spheres": ("random_spheres", "random_spheres.json", 1280, 720, 256, 10, 720, (7, 181)),
     "C5_media": ("cornell_box_media", "cornellbox_media.yaml", 2048, 2048, 1024, 16, 2048, (300, 1555)),
+    # the scene of the reference's only published timing (images.MD:44-53): 512^2, 32 spp, 10 bounces
+    "suzanne_published": ("suzanne_cornell_box", "suzanne_cornellbox.yaml", 512, 512, 32, 10, 128, (3, 77)),
 }
 
 
