@@ -33,6 +33,7 @@ struct RenderLaunch {
     int32_t queue;
     int32_t tiles_x;
     uint32_t n_items;
+    int32_t refill;  // idle lanes that trigger a wave's refill (set per launch, see rt_capi.cpp)
     uint32_t* q_counter;
     float* partial;
 };

@@ -878,8 +878,13 @@ __device__ __forceinline__ bool queue_item(const RenderLaunch& L, uint32_t item,
 constexpr int kQueueShards = RT_QUEUE_SHARDS;
 static_assert(kQueueShards * 32 <= kQueueHeadWords, "queue heads");
 constexpr int kQueueStride = 32;  // u32 words between heads
-#ifndef RT_QUEUE_REFILL
-#define RT_QUEUE_REFILL 8  // idle lanes that trigger a refill (or all lanes idle); measured 1-32: 4 best before tail stealing, 8 after
+// Idle lanes that trigger a refill (or all lanes idle): L.refill, chosen per launch
+// by the host (8 for long queues, 4 for short shards); -DRT_QUEUE_REFILL=k fixes it
+// for A/B builds.
+#ifdef RT_QUEUE_REFILL
+#define RT_REFILL_AT(L) (RT_QUEUE_REFILL)
+#else
+#define RT_REFILL_AT(L) ((L).refill)
 #endif
 
 // Wave-wide dequeue from shard `sh`: every lane in `need` gets an item index,
@@ -903,7 +908,7 @@ __device__ __forceinline__ void queue_refill(const RenderLaunch& L, int lane, bo
                                              int& shard, int& tried, Start&& start) {
     const bool want = !alive && !exhausted;
     const uint64_t need = __ballot(want);
-    if (need && (__popcll(need) >= RT_QUEUE_REFILL || __ballot(alive) == 0)) {
+    if (need && (__popcll(need) >= RT_REFILL_AT(L) || __ballot(alive) == 0)) {
         const uint32_t it = queue_take(L, shard, need, lane);
         if (__ballot(want && it == ~0u)) {  // this shard ran dry: move on
             ++tried;
