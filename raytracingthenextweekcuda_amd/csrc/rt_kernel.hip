@@ -7,7 +7,8 @@
 //
 // Execution model:
 //  * a persistent grid takes work items (pixel, sub-stream of S = lanes_per_pixel)
-//    from 8 sharded queue heads (one per XCD band); each lane folds its
+//    from 8 sharded queue heads (one per XCD band), one atomic per wave once
+//    L.refill lanes are idle (4 or 8, chosen per launch); each lane folds its
 //    sub-stream's samples in order and stores a partial sum, and combine_kernel
 //    sums a pixel's S partials in a fixed order (the static grid, RTMI_QUEUE=0,
 //    computes the same sums for A/B);
