@@ -672,14 +672,14 @@ static rt_status launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLa
             L.queue = rt::queue_blocks(c->n_cu);
             L.n_items = (uint32_t)items;
             // refill threshold (idle lanes a wave collects before one dequeue): 4 for
-            // short shards, whose tail it shortens, and for long items (>= 32 samples),
+            // short shards, whose tail it shortens, and for long items (>= 16 samples),
             // where waiting for 8 idle lanes wastes lane time; 8 otherwise, where fewer
             // dequeues win. Same-box A/B, ms (profiles/r01/ab_refill*.log), 4 vs 8:
-            // CB1 N = 1 8.63 / 8.58, N = 8 shard 1.213 / 1.230; spheres 79.9 / 79.1;
-            // Suzanne 5.52 / 5.44; bunny 544.9 / 548.2; media 1798 / 1846.
+            // CB1 (4 samples per item) N = 1 8.63 / 8.58, N = 8 shard 1.213 / 1.230; spheres (8)
+            // 79.9 / 79.1; Suzanne (1) 5.52 / 5.44; bunny (16) 544.9 / 548.2; media (128) 1798 / 1846.
             const uint64_t lanes = (uint64_t)L.queue * 256u;
             const int per_item = (L.spp + L.lanes_per_pixel - 1) / L.lanes_per_pixel;
-            L.refill = (items < 16u * lanes || per_item >= 32) ? 4 : 8;
+            L.refill = (items < 16u * lanes || per_item >= 16) ? 4 : 8;
             L.partial = c->d_partial;
             RT_HIP(c, hipMemsetAsync(c->d_queue, 0, rt::kQueueHeadWords * sizeof(uint32_t), st));
         }
