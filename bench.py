@@ -24,6 +24,11 @@ sys.path.insert(0, REPO)
 
 METRIC = "Mrays/sec + ms/frame, Cornell Box 512×512 spp=128, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# VALU issue peak (MI355X_MICROARCH.md, cycle constants: a wave64 v_fma_f32 takes 2 cycles of
+# its SIMD): 4 SIMDs per CU x 2.4 GHz / 2 = 4.8 G wave-instructions/s per CU, 1,228.8 G/s for
+# 256 CUs (x 64 lanes x 2 = the 157.3 TFLOP/s FP32 vector spec). Calibrated against a kernel of
+# known VALU count in profiles/r02/valu_probe.json (tools/valu_probe.hip).
+VALU_GINST_PER_CU = 4 * 2.4 / 2
 
 # Algorithmic bytes per record touched: plane 40 B, sphere
 # 20 B, moving sphere 36 B, mesh AABB 24 B, triangle (v0,E1,E2) 36 B, BVH node
@@ -93,10 +98,22 @@ def object_bytes_per_segment(r) -> int:
         counts["moving_sphere"] * BYTES["moving_sphere"]
 
 
+def host_threads() -> int:
+    """The CPUs this job may use (all cores). On the GPU box the process
+    sees every CPU of the machine, but its share is OMP_NUM_THREADS (16 per GPU), which
+    the harness sets; the affinity mask bounds it elsewhere."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def cpu_baseline(args, threads: int):
     """The CPU restatement (oracle/, a port of the reference's integrator) on a
-    bounded sample of the same workload: the median of 3 runs on `threads`
-    threads, plus one single-thread run on 1/8 of the sample's samples."""
+    bounded sample of the same workload: one warm-up, then the
+    median of 5 runs on `threads` threads, plus one single-thread run on 1/8 of the
+    sample's samples."""
     from oracle import oracle as orc
 
     scenes = os.path.join(REPO, "assets", "scenes")
@@ -125,13 +142,13 @@ def cpu_baseline(args, threads: int):
         def run(spp, nthreads):
             return sc.render(w, h, spp, args.depth, threads=nthreads)[1]
 
-    run(1, threads)  # warm-up (OpenMP pool, page-in)
+    run(max(1, args.cpu_spp // 4), threads)  # warm-up (OpenMP pool, page-in, caches)
     times = []
-    for _ in range(3):
+    for _ in range(5):
         t0 = time.perf_counter()
         st = run(args.cpu_spp, threads)
         times.append(time.perf_counter() - t0)
-    dt = sorted(times)[1]
+    dt = sorted(times)[2]
     spp1 = max(1, args.cpu_spp // 8)
     t0 = time.perf_counter()
     st1 = run(spp1, 1)
@@ -151,15 +168,27 @@ def cpu_baseline(args, threads: int):
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
+        "frame_ms_extrapolated": round(frame_ms, 1),
         "cpu_model": model,
         "host_cpus": os.cpu_count(),
         "value_1thread": st1["segments"] / dt1 / 1e6,
         "sample": (f"{args.scene} {w}x{h} spp={args.cpu_spp} depth={args.depth} (same camera; "
                    f"{w * h * args.cpu_spp} of the frame's {args.width * args.height * args.spp} samples), "
-                   f"median of 3 on {threads} threads: {dt:.2f} s wall, {st['segments']} segments; "
-                   f"ms/frame extrapolated by samples: {frame_ms:.0f}; value_1thread: spp={spp1} on 1 thread, "
-                   f"{dt1:.2f} s"),
+                   f"median of 5 after a warm-up on {threads} threads (this job's CPU share; the host has "
+                   f"{os.cpu_count()}): {dt:.2f} s wall, {st['segments']} segments; spp scale factor "
+                   f"{args.spp / args.cpu_spp:g}, pixel scale factor {args.cpu_div ** 2}; ms/frame "
+                   f"extrapolated by samples: {frame_ms:.0f}; value_1thread: spp={spp1} on 1 thread, {dt1:.2f} s"),
     }
+
+
+def load_valu_profile(workload: str):
+    """VALU wave-instructions per traced segment of this workload's render kernel, from the
+    committed rocprofv3 SQ_INSTS_VALU pass (profiles/valu_issue.json, tools/valu_summary.py)."""
+    path = os.path.join(REPO, "profiles", "valu_issue.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        return json.load(fh).get("workloads", {}).get(workload)
 
 
 def load_pmc_traffic(workload: str):
@@ -197,7 +226,9 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import raytracingthenextweekcuda_amd as rtmi
+    from raytracingthenextweekcuda_amd import _lib
 
+    _lib.require_parity_build("bench.py")  # an ablation / timer build would not measure the shipped kernel
     W, H = args.width, args.height
     r = rtmi.Renderer(device=local)
     getattr(rtmi, SCENES[args.scene][0])(r, W, H)
@@ -251,7 +282,9 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     st = r.stats()  # counters summed over the timed launches
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    launch_ms = [a.elapsed_time(b) for a, b in ev]  # render kernel + the work queue's combine pass
+    assert st["launches"] == args.steps, st["launches"]
+    kern_ms = [st["kernel_ms_sum"] / st["launches"]]  # the megakernel alone (the library's event pairs)
     segs, tri_tests, box_tests, nodes = st["segments"], st["tri_tests"], st["box_tests"], st["node_visits"]
     grp = st["group_sphere_tests"] * BYTES["sphere"] + st["group_moving_sphere_tests"] * BYTES["moving_sphere"]
 
@@ -275,8 +308,8 @@ def main():
         K = args.steps
         ms_frame = dt * 1e3 / K
         mrays = segs / dt / 1e6
-        # Roofline of the megakernel: algorithmic record bytes per launch
-        # (rank 0's launch stands for the per-GPU launch).
+        # Record-byte model of SURVEY §8(d), kept as a side figure: these records are
+        # served by the scalar cache, L1 and L2 (the scene is cache-resident), not HBM.
         seg_launch = segs / K / world
         pt = integrator == "pathTrace"
         alg_bytes = (seg_launch * (6 * BYTES["sphere"] if pt else object_bytes_per_segment(r))
@@ -284,13 +317,20 @@ def main():
                      + box_tests / K / world * BYTES["box"] + nodes / K / world * BYTES["node"]
                      + grp / K / world
                      + rows_tot / world * W * BYTES["pixel"])
-        achieved = alg_bytes / (kmean * 1e-3) / 1e9
+        record_gbs = alg_bytes / (kmean * 1e-3) / 1e9
         workload = f"{args.scene}_{W}x{H}_spp{args.spp}_d{args.depth}_n{world}"
         traffic = load_pmc_traffic(workload)
+        # Roofline: the megakernel is bound by VALU issue. achieved = VALU
+        # wave-instructions per launch (SQ_INSTS_VALU per traced segment, profiled, x this
+        # launch's segments) / the megakernel's mean time; peak = the chip's issue rate.
+        n_cu = torch.cuda.get_device_properties(local).multi_processor_count
+        valu_peak = n_cu * VALU_GINST_PER_CU
+        vp = load_valu_profile(workload)
+        valu_launch = vp["valu_insts_per_segment"] * seg_launch if vp else None
+        valu_achieved = valu_launch / (kmean * 1e-3) / 1e9 if vp else None
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            threads = min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(args, threads)
+            cpu = cpu_baseline(args, host_threads())
         line = {
             "metric": METRIC,
             "value": round(mrays, 3),
@@ -313,17 +353,25 @@ def main():
                 "msamples_per_s": round(W * H * args.spp / (dt / K) / 1e6, 3),
             },
             "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "bound": "valu",
+                "achieved": round(valu_achieved, 2) if vp else None,
+                "peak": round(valu_peak, 1),
+                "unit": "Ginst/s (wave64 VALU instructions)",
+                "frac": round(valu_achieved / valu_peak, 4) if vp else None,
                 "traffic": traffic,
                 "kernel_ms": round(kmean, 4),
-                "algorithmic_bytes_per_launch": int(alg_bytes),
-                "note": ("achieved = record bytes the traversal reads (SURVEY §8d) / kernel time; the "
-                         "scene is cache-resident, so frac can pass 1 - traffic is the L2-miss "
-                         "bytes from rocprofv3 FETCH_SIZE/WRITE_SIZE (profiles/pmc_traffic.json)"),
+                "launch_ms": round(float(np.mean(launch_ms)), 4),
+                "valu_insts_per_launch": int(valu_launch) if vp else None,
+                "valu_profile": vp.get("source") if vp else None,
+                "hbm_frac": round(traffic / (kmean * 1e-3) / (HBM_PEAK_GBS * 1e9), 5) if traffic else None,
+                "record_bytes_per_launch": int(alg_bytes),
+                "record_gbs": round(record_gbs, 1),
+                "note": ("achieved = SQ_INSTS_VALU per segment (rocprofv3 pass on this workload, "
+                         "profiles/valu_issue.json) x this launch's segments / the megakernel's mean time "
+                         "(library event pairs, combine pass excluded); peak = CUs x 4 SIMDs x 2.4 GHz / 2 "
+                         "cycles per wave64 VALU op. traffic = HBM-side bytes per launch (FETCH_SIZE x 2 + "
+                         "WRITE_SIZE, profiles/pmc_traffic.json), hbm_frac its share of 8 TB/s; "
+                         "record_* = SURVEY 8(d)'s cache-served record-byte model"),
             },
             "cpu_baseline": cpu,
         }

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RTMI_ABI_VERSION 7
+#define RTMI_ABI_VERSION 8
 
 typedef int32_t rt_status;
 enum {
@@ -35,7 +35,8 @@ enum {
     RT_ERR_STATE = 4,    /* call out of order (e.g. render before commit) */
     RT_ERR_OOM = 5,      /* allocation failure */
     RT_ERR_NODEV = 6,    /* no GPU / context created without a device */
-    RT_ERR_OVERFLOW = 7  /* BVH traversal stack overflow flagged by the kernel */
+    RT_ERR_OVERFLOW = 7, /* BVH traversal stack overflow flagged by the kernel */
+    RT_ERR_COMM = 8      /* RCCL (communicator / collective) failure */
 };
 
 /* Material kinds (Material.h:8-13 MaterialType) + the isotropic phase function
@@ -87,16 +88,35 @@ typedef struct rt_render_stats {
     uint64_t node_visits;   /* BVH node visits (0 for linear-scan scenes) */
     uint64_t tri_tests;     /* triangle records tested */
     uint64_t box_tests;     /* mesh bounding boxes tested */
-    double kernel_ms;       /* duration of the last render kernel (hipEvent) */
+    double kernel_ms;       /* duration of the last launch's render kernel alone (hipEvents around the
+                               megakernel; the work queue's combine pass is not included) */
     uint32_t overflow;      /* 1 if any lane overflowed the traversal stack */
     uint32_t lanes_per_pixel; /* lane layout used by the last render */
     uint64_t group_sphere_tests;        /* spheres tested in object-BVH leaves */
     uint64_t group_moving_sphere_tests; /* moving spheres tested in object-BVH leaves */
     uint64_t debug[8];      /* diagnostic section timers (instrumented builds only; 0 otherwise) */
+    uint32_t refill;        /* work-queue refill threshold of the last launch (idle lanes per dequeue); 0 = static grid */
+    uint32_t queue_blocks;  /* persistent work-queue workgroups of the last launch; 0 = static grid */
+    uint32_t gather;        /* rt_render_multi*: RT_GATHER_RCCL or RT_GATHER_COPY (first context only) */
+    uint32_t launches;      /* launches summed in these counters (RT_RENDER_KEEP_COUNTERS chains; else 1) */
+    double kernel_ms_sum;   /* render-kernel time summed over those launches (one event pair each) */
 } rt_render_stats;
+
+#define RT_GATHER_RCCL 1 /* one ncclGather over the contexts' devices */
+#define RT_GATHER_COPY 2 /* device-to-device copies (contexts share a device; RCCL needs distinct ones) */
 
 /* ---- context (replaces initialize()/cleanup(), main.cu:555-936) ---- */
 int32_t rt_abi_version(void);
+/* Build options of the loaded library. 0 = the shipped parity build. Non-zero bits:
+ * RT_BUILD_ABLATION: an RT_ABL_* ablation is compiled in (results DIFFER from the
+ * reference restatement: never for parity or bench numbers); RT_BUILD_STAMPS: the
+ * instrumented timer build; RT_BUILD_AB: an A/B variant of the schedule (results
+ * identical, performance not the shipped one). bench.py and smoke() refuse
+ * ABLATION and STAMPS builds. */
+#define RT_BUILD_ABLATION 1u
+#define RT_BUILD_STAMPS 2u
+#define RT_BUILD_AB 4u
+uint32_t rt_build_flags(void);
 /* device >= 0: HIP ordinal. device = -1: scene-building only (no GPU calls). */
 rt_status rt_create(int32_t device, rt_ctx** out);
 void rt_destroy(rt_ctx* ctx);
@@ -183,6 +203,26 @@ rt_status rt_bvh_build_stats(const rt_ctx* ctx, double* build_ms, int32_t* gpu_b
 rt_status rt_ply_bvh_image_gpu(int32_t device, const char* path, const float offset[3], float max_coord,
                                uint8_t* out, int64_t capacity, int64_t* size, double* build_ms);
 
+/* ---- `.bvh` cache files (UpdateBoundingVolumeHierarchy, BVH.cpp:500-554) ----
+ * RT_BVH_CACHE_OFF (default): every BVH is built. RT_BVH_CACHE_READ: a BVH over a PLY
+ * file's triangles is read from `<ply>.bvh` when that file exists and the PLY is not
+ * newer than it (the reference's `plyFileTime > bvhFileTime` rebuild rule), for the
+ * pathTrace scene (the last rt_load_object path, as main.cu:435 passes sceneFile)
+ * and for rt_mesh_ply meshes (read at rt_commit). RT_BVH_CACHE_WRITE: after a build,
+ * write `<ply>.bvh` (BVH.cpp:535-541). READ | WRITE is the reference's behaviour.
+ * Cache files are untrusted input: the header counts must match the file size and
+ * the triangle count, every node index and leaf range must be in bounds, children
+ * must follow their parent (DFS order), the leaves must partition the triangle list
+ * and the list must be a permutation; a file that fails is ignored (rebuilt) and
+ * counted in rt_bvh_cache_stats. */
+#define RT_BVH_CACHE_OFF 0
+#define RT_BVH_CACHE_READ 1
+#define RT_BVH_CACHE_WRITE 2
+rt_status rt_set_bvh_cache(rt_ctx* ctx, int32_t mode);
+/* Since the last rt_commit + rt_process_triangle_data: caches read, written, and
+ * rejected as invalid. */
+rt_status rt_bvh_cache_stats(const rt_ctx* ctx, int32_t* reads, int32_t* writes, int32_t* rejected);
+
 /* ---- pathTrace scene (prepareCUDAscene, main.cu:404-553) ----
  * loadObject (Loader.cpp:207-319): appends a PLY mesh whose triangles carry
  * `reflection_type` (RT_PT_*); indices are offset by the vertices already
@@ -243,15 +283,48 @@ rt_status rt_render(rt_ctx* ctx, const rt_render_params* params, float* out_rgb_
 rt_status rt_render_device(rt_ctx* ctx, const rt_render_params* params, float* out_rgb_device,
                            void* hip_stream);
 rt_status rt_sync_stats(rt_ctx* ctx, rt_render_stats* out);
-/* Single-process multi-device frame: ctxs[k] renders the row tiles of
- * rank k of n (params->row_block; row_rank / row_world are set per context) on its
- * own device, every launch is issued before any is awaited, and the tiles are
- * copied back and de-interleaved into out_rgb_host (height x width x 3 floats).
- * Each context needs the same committed scene and camera. The scaling path is one
- * process per GPU with an RCCL gather (raytracingthenextweekcuda_amd/distributed.py);
- * this is the C-only convenience for one host process. */
+/* ---- multi-GPU frames: pixel-row tiles + one RCCL gather ----
+ * Rank k of n owns the row blocks b = k, k + n, k + 2n, ... of params->row_block rows
+ * (y = 0 at the bottom). The RNG is keyed by the global pixel, so the assembled frame
+ * is bit-identical for every n. */
+int32_t rt_owned_rows(int32_t height, int32_t row_block, int32_t rank, int32_t world);
+/* The largest tile of a frame = the gather's equal per-rank count, in rows. */
+int32_t rt_max_tile_rows(int32_t height, int32_t row_block, int32_t world);
+
+/* Single-process multi-device frame (replaces pathTracing's single renderKernel
+ * launch, main.cu:875-898, with SURVEY §8(b)'s `tiles + ncclGather`): ctxs[k] renders
+ * rank k's tiles on its own device (params->row_rank / row_world are set per
+ * context); all launches are issued before any is awaited. When the contexts sit on
+ * distinct devices the tiles meet on ctxs[0]'s device through ONE ncclGather over
+ * communicators from ncclCommInitAll (created on first use and kept by ctxs[0] for
+ * later frames over the same devices); contexts that share a device are copied
+ * device to device instead (RCCL needs one rank per device). A device kernel then
+ * de-interleaves the rows. Each context needs the same committed scene and camera. */
 rt_status rt_render_multi(rt_ctx* const* ctxs, int32_t n, const rt_render_params* params,
                           float* out_rgb_host);
+/* Same, leaving the frame (height x width x 3 floats) in `frame_device` on ctxs[0]'s
+ * device, ordered on `hip_stream` (of that device; NULL = default). */
+rt_status rt_render_multi_device(rt_ctx* const* ctxs, int32_t n, const rt_render_params* params,
+                                 float* frame_device, void* hip_stream);
+
+/* One process per GPU (the scaling path): communicator plumbing for C/C++ hosts.
+ * Rank 0 calls rt_comm_unique_id and ships the 128 bytes to every rank (MPI, a file,
+ * a socket); every rank calls rt_comm_init for its context's device. `comm` is an
+ * ncclComm_t. */
+rt_status rt_comm_unique_id(uint8_t id[128]);
+rt_status rt_comm_init(rt_ctx* ctx, const uint8_t id[128], int32_t world, int32_t rank, void** comm);
+rt_status rt_comm_destroy(void* comm);
+/* The frame exchange of one rank: `tile_device` holds this rank's rendered tile
+ * (rt_render_device with row_rank = rank, row_world = world) with room for
+ * rt_max_tile_rows rows; ONE ncclGather on `hip_stream` moves every tile to rank 0,
+ * whose device de-interleaves them into `frame_device` (height x width x 3 floats;
+ * ignored on other ranks). Asynchronous. */
+rt_status rt_gather_rows(rt_ctx* ctx, void* comm, const rt_render_params* params, int32_t rank, int32_t world,
+                         const float* tile_device, float* frame_device, void* hip_stream);
+/* The de-interleave alone: `staging_device` = world x rt_max_tile_rows x width x 3
+ * floats, rank-major (what the gather delivers) -> `frame_device`. */
+rt_status rt_assemble_rows(rt_ctx* ctx, const rt_render_params* params, int32_t world,
+                           const float* staging_device, float* frame_device, void* hip_stream);
 /* renderKernel's offline output (Canvas::writePixel(index, color / spp), Canvas.h:58-71):
  * gamma-corrected uint8 RGB of the owned rows, computed on the device. */
 rt_status rt_render_u8(rt_ctx* ctx, const rt_render_params* params, uint8_t* out_rgb8_host);

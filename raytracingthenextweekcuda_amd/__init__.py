@@ -5,7 +5,9 @@ The renderer is librtmi.so (hand-written HIP megakernel for gfx950 + C ABI,
 include/rtmi.h). This package is the host-side mirror of the reference's scene
 API (Camera / create* factories) over that ABI, plus scene ingestion.
 """
-from ._lib import RTError, build  # noqa: F401
+from ._lib import (  # noqa: F401
+    BVH_CACHE_OFF, BVH_CACHE_READ, BVH_CACHE_WRITE, GATHER_COPY, GATHER_RCCL, RTError, build, build_flags,
+)
 from .renderer import (  # noqa: F401
     Camera, MaterialHandle, Renderer, createCube, createDieletricMaterial,
     createEmissionMaterial, createLambertianMaterial, createMesh, createMetalMaterial,

@@ -19,11 +19,15 @@ if os.environ.get("RTMI_LIB"):
 RT_OK = 0
 STATUS_NAMES = {
     0: "RT_OK", 1: "RT_ERR_INVALID", 2: "RT_ERR_HIP", 3: "RT_ERR_IO", 4: "RT_ERR_STATE",
-    5: "RT_ERR_OOM", 6: "RT_ERR_NODEV", 7: "RT_ERR_OVERFLOW",
+    5: "RT_ERR_OOM", 6: "RT_ERR_NODEV", 7: "RT_ERR_OVERFLOW", 8: "RT_ERR_COMM",
 }
+# rtmi.h rt_build_flags() bits; bench.py and smoke() refuse ABLATION / STAMPS builds
+BUILD_ABLATION, BUILD_STAMPS, BUILD_AB = 1, 2, 4
+BVH_CACHE_OFF, BVH_CACHE_READ, BVH_CACHE_WRITE = 0, 1, 2
+GATHER_RCCL, GATHER_COPY = 1, 2
 
 # Every symbol include/rtmi.h declares (checked by tests/test_abi.py).
-ABI_VERSION = 7  # include/rtmi.h RTMI_ABI_VERSION
+ABI_VERSION = 8  # include/rtmi.h RTMI_ABI_VERSION
 
 EXPORTS = [
     "rt_abi_version", "rt_create", "rt_destroy", "rt_last_error", "rt_clear_scene",
@@ -36,6 +40,9 @@ EXPORTS = [
     "rt_camera", "rt_commit", "rt_scene_info", "rt_scene_digest", "rt_load_yaml_scene",
     "rt_render", "rt_render_device", "rt_sync_stats",
     "rt_render_u8", "rt_accumulate", "rt_render_multi", "rt_gamma_u8",
+    "rt_build_flags", "rt_set_bvh_cache", "rt_bvh_cache_stats",
+    "rt_owned_rows", "rt_max_tile_rows", "rt_render_multi_device", "rt_comm_unique_id", "rt_comm_init",
+    "rt_comm_destroy", "rt_gather_rows", "rt_assemble_rows",
 ]
 
 
@@ -61,6 +68,8 @@ class RenderStats(C.Structure):
         ("overflow", C.c_uint32), ("lanes_per_pixel", C.c_uint32),
         ("group_sphere_tests", C.c_uint64), ("group_moving_sphere_tests", C.c_uint64),
         ("debug", C.c_uint64 * 8),
+        ("refill", C.c_uint32), ("queue_blocks", C.c_uint32), ("gather", C.c_uint32), ("launches", C.c_uint32),
+        ("kernel_ms_sum", C.c_double),
     ]
 
 
@@ -134,5 +143,34 @@ def lib():
     L.rt_render_u8.argtypes = [vp, C.POINTER(RenderParams), C.POINTER(C.c_uint8)]
     L.rt_accumulate.argtypes = [vp, C.POINTER(RenderParams), vp, C.c_uint32, vp, vp]
     L.rt_gamma_u8.argtypes = [fp, C.c_int64, C.POINTER(C.c_uint8)]
+    L.rt_build_flags.restype = C.c_uint32
+    L.rt_build_flags.argtypes = []
+    L.rt_set_bvh_cache.argtypes = [vp, i32]
+    L.rt_bvh_cache_stats.argtypes = [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]
+    L.rt_owned_rows.argtypes = [i32, i32, i32, i32]
+    L.rt_owned_rows.restype = i32
+    L.rt_max_tile_rows.argtypes = [i32, i32, i32]
+    L.rt_max_tile_rows.restype = i32
+    L.rt_render_multi_device.argtypes = [C.POINTER(vp), i32, C.POINTER(RenderParams), vp, vp]
+    L.rt_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
+    L.rt_comm_init.argtypes = [vp, C.POINTER(C.c_uint8), i32, i32, C.POINTER(vp)]
+    L.rt_comm_destroy.argtypes = [vp]
+    L.rt_gather_rows.argtypes = [vp, vp, C.POINTER(RenderParams), i32, i32, vp, vp, vp]
+    L.rt_assemble_rows.argtypes = [vp, C.POINTER(RenderParams), i32, vp, vp, vp]
     _lib = L
     return L
+
+
+def build_flags() -> int:
+    """rt_build_flags() of the loaded library (0 = the shipped parity build)."""
+    return int(lib().rt_build_flags())
+
+
+def require_parity_build(what: str) -> None:
+    """Refuses a library compiled with an ablation (results differ from the
+    restatement) or the instrumented timer build: `what` would not measure or
+    check the shipped kernel."""
+    f = build_flags()
+    if f & (BUILD_ABLATION | BUILD_STAMPS):
+        raise RuntimeError(f"{what}: {LIB_PATH} is a non-parity build (rt_build_flags = {f:#x}); "
+                           "rebuild it without EXTRA=-DRT_ABL_* / -DRT_STAMPS")

@@ -9,6 +9,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
+#include <filesystem>
 #include <fstream>
 #include <memory>
 
@@ -412,6 +414,104 @@ std::vector<uint8_t> bvh_image(const CFBvh& b) {
     memcpy(img.data() + 8, b.nodes.data(), (size_t)nn * sizeof(CFNode));
     memcpy(img.data() + 8 + (size_t)nn * sizeof(CFNode), b.tri_index.data(), (size_t)ni * 4);
     return img;
+}
+
+std::string parse_bvh_image(const uint8_t* data, size_t size, const std::vector<v3>& vertices,
+                            const std::vector<uint32_t>& indices, CFBvh& out) {
+    if (!data || size < 8) return "shorter than its 8-byte header";
+    uint32_t nn = 0, ni = 0;
+    memcpy(&nn, data, 4);
+    memcpy(&ni, data + 4, 4);
+    const size_t nt = indices.size() / 3;
+    if (nn == 0) return "no nodes";
+    if ((uint64_t)ni != (uint64_t)nt) return "index count does not match the triangle count";
+    if ((uint64_t)size != 8ull + 32ull * nn + 4ull * ni) return "size does not match the header counts";
+    CFBvh b;
+    b.nodes.resize(nn);
+    b.tri_index.resize(ni);
+    memcpy(b.nodes.data(), data + 8, (size_t)nn * sizeof(CFNode));
+    memcpy(b.tri_index.data(), data + 8 + (size_t)nn * sizeof(CFNode), (size_t)ni * 4);
+    std::vector<uint8_t> seen(nt, 0), covered(ni, 0), parents(nn, 0);
+    for (uint32_t k = 0; k < ni; ++k) {
+        const int32_t t = b.tri_index[k];
+        if (t < 0 || (size_t)t >= nt) return "triangle index out of range";
+        if (seen[(size_t)t]++) return "triangle listed twice";
+    }
+    std::vector<int> depth(nn, 0);
+    for (uint32_t i = 0; i < nn; ++i) {
+        const CFNode& n = b.nodes[i];
+        for (int a = 0; a < 3; ++a)
+            if (!std::isfinite(n.bottom[a]) || !std::isfinite(n.top[a]) || n.bottom[a] > n.top[a])
+                return "bad box at node " + std::to_string(i);
+        if (i > 0 && parents[i] != 1) return "node " + std::to_string(i) + " is not referenced exactly once";
+        if (depth[i] > b.max_depth) b.max_depth = depth[i];
+        auto inside = [&](const float* lo, const float* hi, v3 p) {
+            return p.x >= lo[0] && p.x <= hi[0] && p.y >= lo[1] && p.y <= hi[1] && p.z >= lo[2] && p.z <= hi[2];
+        };
+        if (n.u0 & 0x80000000u) {
+            const uint32_t cnt = n.u0 & 0x7FFFFFFFu, st = n.u1;
+            if (cnt == 0 || (uint64_t)st + cnt > ni) return "leaf range out of bounds at node " + std::to_string(i);
+            for (uint32_t k = st; k < st + cnt; ++k) {
+                if (covered[k]++) return "leaves overlap in the triangle list";
+                const size_t t = (size_t)b.tri_index[k];
+                for (int j = 0; j < 3; ++j)
+                    if (!inside(n.bottom, n.top, vertices[indices[3 * t + (size_t)j]]))
+                        return "leaf box does not contain its triangles at node " + std::to_string(i);
+            }
+        } else {
+            const uint32_t l = n.u0, r = n.u1;
+            if (l <= i || r <= i || l >= nn || r >= nn || l == r) return "bad children at node " + std::to_string(i);
+            for (uint32_t ch : {l, r}) {
+                const CFNode& cn = b.nodes[ch];
+                if (!inside(n.bottom, n.top, v3{cn.bottom[0], cn.bottom[1], cn.bottom[2]}) ||
+                    !inside(n.bottom, n.top, v3{cn.top[0], cn.top[1], cn.top[2]}))
+                    return "child box outside its parent at node " + std::to_string(i);
+                ++parents[ch];
+                depth[ch] = depth[i] + 1;
+            }
+        }
+    }
+    for (uint32_t k = 0; k < ni; ++k)
+        if (!covered[k]) return "triangle list entry not in any leaf";
+    out = std::move(b);
+    return "";
+}
+
+int read_bvh_cache(const std::string& ply_path, const std::vector<v3>& vertices, const std::vector<uint32_t>& indices,
+                   CFBvh& out, std::string* why) {
+    namespace fs = std::filesystem;
+    const std::string cache = ply_path + ".bvh";
+    std::error_code ec;
+    if (!fs::exists(cache, ec) || ec) return 0;
+    if (fs::exists(ply_path, ec) && !ec) {
+        const auto tp = fs::last_write_time(ply_path, ec);
+        const auto tb = ec ? tp : fs::last_write_time(cache, ec);
+        if (!ec && tp > tb) return 0;  // bUpdateBVH = plyFileTime > bvhFileTime (BVH.cpp:508-514)
+    }
+    FILE* fp = fopen(cache.c_str(), "rb");
+    if (!fp) return 0;
+    std::vector<uint8_t> img;
+    uint8_t buf[1 << 16];
+    size_t got;
+    while ((got = fread(buf, 1, sizeof(buf), fp)) > 0) {
+        img.insert(img.end(), buf, buf + got);
+        if (img.size() > ((size_t)1 << 33)) break;  // > 8 GiB: not a cache of any loadable mesh
+    }
+    fclose(fp);
+    const std::string e = parse_bvh_image(img.data(), img.size(), vertices, indices, out);
+    if (!e.empty()) {
+        if (why) *why = cache + ": " + e;
+        return -1;
+    }
+    return 1;
+}
+
+bool write_bvh_cache(const std::string& ply_path, const CFBvh& b) {
+    const std::vector<uint8_t> img = bvh_image(b);
+    FILE* fp = fopen((ply_path + ".bvh").c_str(), "wb");
+    if (!fp) return false;
+    const bool ok = fwrite(img.data(), 1, img.size(), fp) == img.size();
+    return fclose(fp) == 0 && ok;
 }
 
 }  // namespace rt

@@ -89,4 +89,21 @@ std::string append_ply(const std::string& path, PlyMesh& accum);
 // The `.bvh` cache image: u32 nodes, u32 indices, nodes, int32 indices.
 std::vector<uint8_t> bvh_image(const CFBvh& b);
 
+// A `.bvh` cache image read back (UpdateBoundingVolumeHierarchy's reader,
+// BVH.cpp:544-551) as UNTRUSTED input for the triangles (vertices, indices):
+// the header counts must match the size and the triangle count, children must
+// follow their parent (DFS order) and be referenced once, every node reachable,
+// the leaves must partition the triangle list, the list must be a permutation,
+// and every box must contain its triangles / children. Returns "" or why not.
+std::string parse_bvh_image(const uint8_t* data, size_t size, const std::vector<v3>& vertices,
+                            const std::vector<uint32_t>& indices, CFBvh& out);
+
+// UpdateBoundingVolumeHierarchy's cache rule for `<ply>.bvh`: 1 = read and valid,
+// 0 = no usable file (absent, or the PLY is newer: plyFileTime > bvhFileTime),
+// -1 = present and fresh but rejected (*why says why).
+int read_bvh_cache(const std::string& ply_path, const std::vector<v3>& vertices,
+                   const std::vector<uint32_t>& indices, CFBvh& out, std::string* why);
+// The writer (BVH.cpp:535-541): true if `<ply>.bvh` was written.
+bool write_bvh_cache(const std::string& ply_path, const CFBvh& b);
+
 }  // namespace rt

@@ -18,54 +18,12 @@
 #include <vector>
 
 #include "rt_bvh.h"
+#include "rt_ctx.h"
 #include "rt_kernel.h"
 #include "rt_scene.h"
 #include "rt_yaml.h"
 
-struct rt_ctx {
-    int device = -1;
-    std::string err;
-    rt::HostScene scene;
-    bool committed = false;
-
-    // device tables
-    rt::ObjRec* d_objs = nullptr;
-    rt::TriRec* d_tris = nullptr;
-    rt::MatRec* d_mats = nullptr;
-    rt::BvhNode* d_nodes = nullptr;
-    uint32_t* d_tri_orig = nullptr;
-    int n_objs = 0;
-    int n_mats = 0;
-    unsigned long long* d_counters = nullptr;
-    float* d_out = nullptr;   // staging buffer for rt_render (host output)
-    size_t d_out_bytes = 0;
-    uint8_t* d_u8 = nullptr;  // staging buffer for rt_render_u8
-    size_t d_u8_bytes = 0;
-    int n_cu = 0;                 // compute units (persistent work-queue grid)
-    uint32_t* d_queue = nullptr;  // work-queue head
-    float* d_partial = nullptr;   // work-queue partial sums
-    size_t d_partial_bytes = 0;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    bool have_events = false;
-    rt_render_stats last{};
-    bool stats_pending = false;
-    bool launched = false;
-
-    // pathTrace scene (prepareCUDAscene): raw loaded PLY data + device tables
-    rt::PlyMesh pt_raw;
-    std::vector<uint32_t> pt_materials;  // ReflectionType per triangle
-    bool pt_ready = false;
-    int pt_tris = 0;
-    float pt_scale = 0.0f;  // max |coordinate| of the processed triangles
-    rt::CFBvh pt_bvh;  // host copy (the `.bvh` cache image source)
-    rt::KTri* d_pt_tris = nullptr;
-    rt::CFNode* d_pt_nodes = nullptr;
-    int32_t* d_pt_list = nullptr;
-    double pt_build_ms = 0.0;
-    int pt_gpu_builds = 0;
-};
-
-namespace {
+namespace rtc {
 
 rt_status fail(rt_ctx* c, rt_status s, const std::string& msg) {
     if (c) c->err = msg;
@@ -76,11 +34,24 @@ rt_status hip_fail(rt_ctx* c, hipError_t e, const char* what) {
     return fail(c, RT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-#define RT_HIP(c, call)                                 \
-    do {                                                \
-        hipError_t _e = (call);                         \
-        if (_e != hipSuccess) return hip_fail(c, _e, #call); \
-    } while (0)
+rt_status ensure_device(rt_ctx* c, void** buf, size_t* have, size_t bytes) {
+    if (bytes <= *have) return RT_OK;
+    (void)hipFree(*buf);
+    *buf = nullptr;
+    *have = 0;
+    RT_HIP(c, hipMalloc(buf, bytes));
+    *have = bytes;
+    return RT_OK;
+}
+
+}  // namespace rtc
+
+using rtc::fail;
+using rtc::hip_fail;
+using rtc::launch;
+using rtc::validate;
+
+namespace {
 
 bool finite3(const float* v) { return v && isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2]); }
 
@@ -176,6 +147,11 @@ void rt_destroy(rt_ctx* c) {
         (void)hipFree(c->d_u8);
         (void)hipFree(c->d_queue);
         (void)hipFree(c->d_partial);
+        (void)hipFree(c->d_stage);
+        (void)hipFree(c->d_frame);
+        rtc::destroy_multi(c);
+        for (hipEvent_t e : c->kev0) (void)hipEventDestroy(e);
+        for (hipEvent_t e : c->kev1) (void)hipEventDestroy(e);
         if (c->have_events) {
             (void)hipEventDestroy(c->ev0);
             (void)hipEventDestroy(c->ev1);
@@ -193,6 +169,7 @@ rt_status rt_clear_scene(rt_ctx* c) {
     if (c->device >= 0) (void)hipSetDevice(c->device);
     free_pathtrace(c);
     c->pt_raw = rt::PlyMesh();
+    c->pt_last_file.clear();
     c->pt_materials.clear();
     return RT_OK;
 }
@@ -391,7 +368,9 @@ static rt_status rt_mesh_ply_impl(rt_ctx* c, int32_t index, const char* path, co
         verts.push_back(m.vertices[i].y);
         verts.push_back(m.vertices[i].z);
     }
-    return rt_mesh(c, index, verts.data(), (int32_t)(verts.size() / 9), material);
+    rt_status st = rt_mesh(c, index, verts.data(), (int32_t)(verts.size() / 9), material);
+    if (st == RT_OK) c->scene.objects[(size_t)index].bvh_cache = path;  // its `<ply>.bvh` (BVH.cpp:503-504)
+    return st;
 }
 
 static rt_status rt_ply_bvh_image_impl(const char* path, const float offset[3], float max_coord,
@@ -433,6 +412,23 @@ rt_status rt_set_bvh_builder(rt_ctx* c, int32_t builder) {
     return RT_OK;
 }
 
+rt_status rt_set_bvh_cache(rt_ctx* c, int32_t mode) {
+    if (!c) return RT_ERR_INVALID;
+    if (mode & ~(RT_BVH_CACHE_READ | RT_BVH_CACHE_WRITE)) return fail(c, RT_ERR_INVALID, "unknown BVH cache mode");
+    c->scene.bvh_cache_mode = mode;
+    c->committed = false;
+    c->pt_ready = false;
+    return RT_OK;
+}
+
+rt_status rt_bvh_cache_stats(const rt_ctx* c, int32_t* reads, int32_t* writes, int32_t* rejected) {
+    if (!c) return RT_ERR_INVALID;
+    if (reads) *reads = c->scene.cache_reads + c->pt_cache_reads;
+    if (writes) *writes = c->scene.cache_writes + c->pt_cache_writes;
+    if (rejected) *rejected = c->scene.cache_rejected + c->pt_cache_rejected;
+    return RT_OK;
+}
+
 rt_status rt_bvh_build_stats(const rt_ctx* c, double* build_ms, int32_t* gpu_builds) {
     if (!c) return RT_ERR_INVALID;
     if (build_ms) *build_ms = c->scene.bvh_build_ms + c->pt_build_ms;
@@ -462,6 +458,7 @@ static rt_status rt_load_object_impl(rt_ctx* c, const char* path, int32_t reflec
         return fail(c, RT_ERR_INVALID, "load_object: bad arguments");
     std::string e = rt::append_ply(path, c->pt_raw);
     if (!e.empty()) return fail(c, RT_ERR_IO, e);
+    c->pt_last_file = path;  // UpdateBoundingVolumeHierarchy(sceneFile) (main.cu:435)
     c->pt_materials.resize(c->pt_raw.indices.size() / 3, (uint32_t)reflection_type);
     c->pt_ready = false;
     return RT_OK;
@@ -476,6 +473,7 @@ static rt_status rt_process_triangle_data_impl(rt_ctx* c, const float offset[3],
     free_pathtrace(c);
     c->pt_build_ms = 0.0;
     c->pt_gpu_builds = 0;
+    c->pt_cache_reads = c->pt_cache_writes = c->pt_cache_rejected = 0;
     rt::PlyMesh m = c->pt_raw;
     float scale_max = 0.0f;
     std::vector<rt::KTri> kt;
@@ -488,10 +486,22 @@ static rt_status rt_process_triangle_data_impl(rt_ctx* c, const float offset[3],
             scale_max = std::max(scale_max, std::max(fabsf(v.x), std::max(fabsf(v.y), fabsf(v.z))));
         }
         const auto t0 = std::chrono::steady_clock::now();
-        if (c->scene.bvh_gpu && rt::gpu_build_cf_bvh(c->device, m.vertices, m.indices, b, 4, nullptr).empty())
-            c->pt_gpu_builds = 1;
-        else
-            rt::build_cf_bvh(m.vertices, m.indices, b);
+        const int mode = c->scene.bvh_cache_mode;
+        int got = 0;
+        if ((mode & RT_BVH_CACHE_READ) && !c->pt_last_file.empty()) {
+            std::string why;
+            got = rt::read_bvh_cache(c->pt_last_file, m.vertices, m.indices, b, &why);
+            if (got > 0) c->pt_cache_reads = 1;
+            else if (got < 0) c->pt_cache_rejected = 1;
+        }
+        if (got <= 0) {
+            if (c->scene.bvh_gpu && rt::gpu_build_cf_bvh(c->device, m.vertices, m.indices, b, 4, nullptr).empty())
+                c->pt_gpu_builds = 1;
+            else
+                rt::build_cf_bvh(m.vertices, m.indices, b);
+            if ((mode & RT_BVH_CACHE_WRITE) && !c->pt_last_file.empty() && rt::write_bvh_cache(c->pt_last_file, b))
+                c->pt_cache_writes = 1;
+        }
         c->pt_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     if (out_info) {
@@ -588,7 +598,9 @@ rt_status rt_scene_info(const rt_ctx* c, int32_t out[8]) {
     return RT_OK;
 }
 
-static rt_status validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& L) {
+}  // extern "C"
+
+rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& L) {
     if (!p) return fail(c, RT_ERR_INVALID, "null params");
     if (c->device < 0) return fail(c, RT_ERR_NODEV, "context has no device");
     if (p->flags & ~(uint32_t)RT_RENDER_KEEP_COUNTERS) return fail(c, RT_ERR_INVALID, "unknown flags");
@@ -638,7 +650,7 @@ static rt_status validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch
     return RT_OK;
 }
 
-static rt_status launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaunch& L0, float* out,
+rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaunch& L0, float* out,
                         hipStream_t st) {
     RT_HIP(c, hipSetDevice(c->device));
     // The context's work queue, partial sums and counters are reused by every
@@ -687,24 +699,50 @@ static rt_status launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLa
     if (L.queue == 0 && L.lanes_per_pixel > 64)  // the static grid keeps a pixel's sub-streams in one wave
         return fail(c, RT_ERR_INVALID, "lanes_per_pixel > 64 needs the work queue, which this frame does not fit");
     const bool keep = (p->flags & RT_RENDER_KEEP_COUNTERS) != 0;
-    if (!keep) RT_HIP(c, hipMemsetAsync(c->d_counters, 0, rt::kNumCounters * sizeof(unsigned long long), st));
+    if (!keep) {
+        RT_HIP(c, hipMemsetAsync(c->d_counters, 0, rt::kNumCounters * sizeof(unsigned long long), st));
+        c->n_kev = 0;
+    }
+    // this launch's (start, end of megakernel) event pair; kept for every launch of a
+    // KEEP_COUNTERS chain (up to 65,536) so rt_sync_stats can sum them
+    hipEvent_t k0 = nullptr, k1 = nullptr;
+    if (c->n_kev < 65536u) {
+        while (c->kev0.size() <= c->n_kev) {
+            hipEvent_t a = nullptr, b = nullptr;
+            RT_HIP(c, hipEventCreate(&a));
+            if (hipEventCreate(&b) != hipSuccess) {
+                (void)hipEventDestroy(a);
+                return fail(c, RT_ERR_HIP, "hipEventCreate failed");
+            }
+            c->kev0.push_back(a);
+            c->kev1.push_back(b);
+        }
+        k0 = c->kev0[c->n_kev];
+        k1 = c->kev1[c->n_kev];
+        ++c->n_kev;
+    }
     RT_HIP(c, hipEventRecord(c->ev0, st));
+    if (k0) RT_HIP(c, hipEventRecord(k0, st));
     if (p->integrator == RT_INTEGRATOR_PATHTRACE) {
         rt::PtSceneArgs pt{c->d_pt_tris, c->d_pt_nodes, c->d_pt_list};
-        RT_HIP(c, rt::launch_pathtrace(pt, c->scene.camera, L, out, c->d_counters, st));
+        RT_HIP(c, rt::launch_pathtrace(pt, c->scene.camera, L, out, c->d_counters, st, k1));
     } else {
         rt::SceneArgs sc{c->d_objs,   c->d_tris,  c->d_mats,  c->d_nodes,
                          c->d_tri_orig, c->n_objs, c->n_mats, !c->scene.nodes.empty()};
-        RT_HIP(c, rt::launch_render(sc, c->scene.camera, L, out, c->d_counters, st));
+        RT_HIP(c, rt::launch_render(sc, c->scene.camera, L, out, c->d_counters, st, k1));
     }
     RT_HIP(c, hipEventRecord(c->ev1, st));
     const uint64_t prev_samples = keep ? c->last.samples : 0;
     c->last = rt_render_stats{};
     c->last.samples = prev_samples + (uint64_t)L.local_rows * (uint64_t)L.width * (uint64_t)L.spp;
     c->last.lanes_per_pixel = (uint32_t)L.lanes_per_pixel;
+    c->last.refill = L.queue ? (uint32_t)L.refill : 0u;
+    c->last.queue_blocks = (uint32_t)L.queue;
     c->stats_pending = true;
     return RT_OK;
 }
+
+extern "C" {
 
 static rt_status rt_render_device_impl(rt_ctx* c, const rt_render_params* p, float* out, void* stream) {
     if (!c) return RT_ERR_INVALID;
@@ -738,7 +776,15 @@ rt_status rt_sync_stats(rt_ctx* c, rt_render_stats* out) {
         unsigned long long h[rt::kNumCounters];
         RT_HIP(c, hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
         float ms = 0.0f;
-        RT_HIP(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        double sum = 0.0;
+        for (uint32_t k = 0; k < c->n_kev; ++k) {
+            float e = 0.0f;
+            RT_HIP(c, hipEventElapsedTime(&e, c->kev0[k], c->kev1[k]));
+            sum += e;
+            ms = e;
+        }
+        c->last.launches = c->n_kev;
+        c->last.kernel_ms_sum = sum;
         c->last.segments = h[0];
         c->last.tri_tests = h[1];
         c->last.box_tests = h[2];
@@ -776,52 +822,6 @@ static rt_status rt_render_impl(rt_ctx* c, const rt_render_params* p, float* out
     s = rt_sync_stats(c, nullptr);
     if (s != RT_OK) return s;
     if (c->last.overflow) return fail(c, RT_ERR_OVERFLOW, "BVH traversal stack overflow");
-    return RT_OK;
-}
-
-static rt_status rt_render_multi_impl(rt_ctx* const* ctxs, int32_t n, const rt_render_params* p, float* out_host) {
-    if (!ctxs || n < 1 || !p || !out_host) return RT_ERR_INVALID;
-    for (int32_t k = 0; k < n; ++k)
-        if (!ctxs[k]) return RT_ERR_INVALID;
-    // launch every device's row tiles first (asynchronous), then collect
-    std::vector<rt_render_params> pk((size_t)n, *p);
-    for (int32_t k = 0; k < n; ++k) {
-        rt_ctx* c = ctxs[k];
-        pk[k].row_rank = k;
-        pk[k].row_world = n;
-        rt::RenderLaunch L;
-        rt_status s = validate(c, &pk[k], L);
-        if (s != RT_OK) return s;
-        const size_t bytes = (size_t)L.local_rows * L.width * 3 * sizeof(float);
-        RT_HIP(c, hipSetDevice(c->device));
-        if (bytes > c->d_out_bytes) {
-            (void)hipFree(c->d_out);
-            c->d_out = nullptr;
-            c->d_out_bytes = 0;
-            RT_HIP(c, hipMalloc(&c->d_out, bytes));
-            c->d_out_bytes = bytes;
-        }
-        s = launch(c, &pk[k], L, c->d_out, nullptr);
-        if (s != RT_OK) return s;
-    }
-    std::vector<float> tile;
-    const int32_t W = p->width, rb = p->row_block;
-    for (int32_t k = 0; k < n; ++k) {
-        rt_ctx* c = ctxs[k];
-        const int32_t rows = rt::owned_rows(p->height, rb, k, n);
-        RT_HIP(c, hipSetDevice(c->device));
-        RT_HIP(c, hipStreamSynchronize(nullptr));
-        tile.resize((size_t)rows * W * 3);
-        if (rows) RT_HIP(c, hipMemcpy(tile.data(), c->d_out, tile.size() * sizeof(float), hipMemcpyDeviceToHost));
-        for (int32_t j = 0; j < rows; ++j) {  // local row j of rank k -> global row y
-            const int32_t lb = j / rb;
-            const int32_t y = (lb * n + k) * rb + (j - lb * rb);
-            memcpy(out_host + (size_t)y * W * 3, tile.data() + (size_t)j * W * 3, (size_t)W * 3 * sizeof(float));
-        }
-        rt_status s = rt_sync_stats(c, nullptr);
-        if (s != RT_OK) return s;
-        if (c->last.overflow) return fail(c, RT_ERR_OVERFLOW, "BVH traversal stack overflow");
-    }
     return RT_OK;
 }
 
@@ -1227,16 +1227,6 @@ rt_status rt_accumulate(rt_ctx* c, const rt_render_params* p, float* accum, uint
         return fail(c, RT_ERR_OOM, "out of host memory");
     } catch (const std::exception& ex) {
         return fail(c, RT_ERR_INVALID, std::string("internal error: ") + ex.what());
-    }
-}
-
-rt_status rt_render_multi(rt_ctx* const* ctxs, int32_t n, const rt_render_params* p, float* out_host) {
-    try {
-        return rt_render_multi_impl(ctxs, n, p, out_host);
-    } catch (const std::bad_alloc&) {
-        return RT_ERR_OOM;
-    } catch (const std::exception&) {
-        return RT_ERR_INVALID;
     }
 }
 

@@ -44,6 +44,10 @@ struct RenderLaunch {
 // Work-queue launches (the default) take the largest power of two
 // S <= min(32, spp) with pixels * S <= 2^25 items (the partial-sum buffer stays
 // <= 400 MB); static launches the largest with pixels * S <= 2^24 lanes.
+// `pixels` is the FULL frame (width * height), not this shard's rows: every rank
+// of a row-sharded frame then folds a pixel's samples with the same S, so the
+// assembled frame is bit-identical for any world size (and N > 1 shards do the
+// same per-item work as N = 1).
 // Measured on one MI355X, ms/frame (static S=1 -> static auto -> queue auto):
 // CornellBox1 11.9 -> 10.7 -> 8.9, random spheres 245 -> 164 -> 113,
 // materialball 34.5 -> 14.5 -> 11.7, bunny 999 -> 950 -> 765, media 1982 -> 2015 -> 1883.
@@ -51,7 +55,7 @@ inline void choose_layout(RenderLaunch& L, int32_t requested, bool queue) {
     int32_t s = requested;
     if (s <= 0) {
         s = 1;
-        const int64_t px = (int64_t)L.local_rows * L.width;
+        const int64_t px = (int64_t)L.height * L.width;
         const int64_t cap = queue ? (int64_t(1) << 25) : (int64_t(1) << 24);
         while (2 * s <= 32 && 2 * s <= L.spp && px * 2 * s <= cap) s *= 2;
     }
@@ -79,14 +83,25 @@ struct PtSceneArgs {
     const int32_t* tri_list;  // leaf triangle lists in DFS order
 };
 
+// `main_done` (may be null) is recorded on `stream` right after the megakernel,
+// before the work queue's combine pass.
 hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec& cam, const RenderLaunch& L,
-                            float* out, unsigned long long* counters, hipStream_t stream);
+                            float* out, unsigned long long* counters, hipStream_t stream,
+                            hipEvent_t main_done);
 
 // Workgroups of the persistent work-queue grid (n_cu x resident blocks per CU).
 int queue_blocks(int n_cu);
 
 hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLaunch& L,
-                         float* out, unsigned long long* counters, hipStream_t stream);
+                         float* out, unsigned long long* counters, hipStream_t stream, hipEvent_t main_done);
+
+// Frame assembly on the gather root (rt_rows.hip): staging = world tiles of
+// max_rows x width x 3 floats, rank-major -> frame (height x width x 3).
+hipError_t launch_assemble_rows(const float* staging, float* frame, int32_t width, int32_t height,
+                                int32_t row_block, int32_t world, int32_t max_rows, hipStream_t stream);
+
+// Build options compiled into the kernels (rtmi.h RT_BUILD_*).
+uint32_t kernel_build_flags();
 
 // Rows of [0, height) owned by (row_block, row_rank, row_world).
 inline int32_t owned_rows(int32_t height, int32_t block, int32_t rank, int32_t world) {
@@ -96,6 +111,16 @@ inline int32_t owned_rows(int32_t height, int32_t block, int32_t rank, int32_t w
         n += r1 - r0;
     }
     return n;
+}
+
+// The largest owned_rows over the ranks (rank 0 owns the most: blocks are dealt from it).
+inline int32_t max_tile_rows(int32_t height, int32_t block, int32_t world) {
+    int32_t m = 0;
+    for (int32_t k = 0; k < world && k * block < height; ++k) {
+        const int32_t r = owned_rows(height, block, k, world);
+        m = r > m ? r : m;
+    }
+    return m;
 }
 
 }  // namespace rt

@@ -1974,34 +1974,53 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
 }
 
 hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec& cam, const RenderLaunch& L,
-                            float* out, unsigned long long* counters, hipStream_t stream) {
+                            float* out, unsigned long long* counters, hipStream_t stream, hipEvent_t main_done) {
     dim3 block(64 * kWavesPerBlock);
     if (L.queue) {
-        if (L.n_items == 0) return hipSuccess;
+        if (L.n_items == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
         const uint32_t waves = (L.n_items + 63u) / 64u;
         const uint32_t blocks = std::min<uint32_t>((waves + kWavesPerBlock - 1) / kWavesPerBlock,
                                                    (uint32_t)L.queue);
         hipLaunchKernelGGL(pathtrace_kernel<true>, dim3(blocks), block, 0, stream, sc.ktris, sc.nodes,
                            sc.tri_list, cam, L, out, counters);
+        if (main_done) (void)hipEventRecord(main_done, stream);
         const uint32_t pixels = L.n_items / (uint32_t)L.lanes_per_pixel;
         hipLaunchKernelGGL(combine_kernel, dim3((pixels + 255u) / 256u), dim3(256), 0, stream, L, out);
         return hipGetLastError();
     }
     dim3 grid((L.width + 2 * L.tile_w - 1) / (2 * L.tile_w),
               (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
-    if (grid.x == 0 || grid.y == 0) return hipSuccess;
+    if (grid.x == 0 || grid.y == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
     hipLaunchKernelGGL(pathtrace_kernel<false>, grid, block, 0, stream, sc.ktris, sc.nodes,
                        sc.tri_list, cam, L, out, counters);
+    if (main_done) (void)hipEventRecord(main_done, stream);
     return hipGetLastError();
 }
 
 int queue_blocks(int n_cu) { return n_cu * 4; }  // 4 waves/SIMD x 4 SIMDs / 4-wave blocks
 
+// rtmi.h RT_BUILD_*: which non-shipped options this translation unit (and, through
+// the shared EXTRA flags, the whole library) was compiled with.
+uint32_t kernel_build_flags() {
+    uint32_t f = 0;
+#if defined(RT_ABL_FASTMATH) || defined(RT_ABL_NOREJECT) || defined(RT_ABL_FLOATLOG) || RT_ABL_PHILOX_ROUNDS != 10
+    f |= 1u;  // RT_BUILD_ABLATION: results differ from the restatement
+#endif
+#ifdef RT_STAMPS
+    f |= 2u;  // RT_BUILD_STAMPS
+#endif
+#if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
+    !RT_TAIL_STEAL || RT_WAVES_PER_EU != 4
+    f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
+#endif
+    return f;
+}
+
 hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLaunch& L, float* out,
-                         unsigned long long* counters, hipStream_t stream) {
+                         unsigned long long* counters, hipStream_t stream, hipEvent_t main_done) {
     dim3 block(64 * kWavesPerBlock);
     if (L.queue) {
-        if (L.n_items == 0) return hipSuccess;
+        if (L.n_items == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
         const uint32_t lanes_needed = (L.n_items + 63u) / 64u;  // waves
         const uint32_t blocks = std::min<uint32_t>((lanes_needed + kWavesPerBlock - 1) / kWavesPerBlock,
                                                    (uint32_t)L.queue);
@@ -2012,19 +2031,21 @@ hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLau
         else
             hipLaunchKernelGGL((render_kernel<false, true>), grid, block, 0, stream, sc.objs, sc.tris,
                                sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
+        if (main_done) (void)hipEventRecord(main_done, stream);
         const uint32_t pixels = L.n_items / (uint32_t)L.lanes_per_pixel;
         hipLaunchKernelGGL(combine_kernel, dim3((pixels + 255u) / 256u), dim3(256), 0, stream, L, out);
         return hipGetLastError();
     }
     dim3 grid((L.width + 2 * L.tile_w - 1) / (2 * L.tile_w),
               (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
-    if (grid.x == 0 || grid.y == 0) return hipSuccess;
+    if (grid.x == 0 || grid.y == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
     if (sc.has_bvh)
         hipLaunchKernelGGL((render_kernel<true, false>), grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
                            sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
     else
         hipLaunchKernelGGL((render_kernel<false, false>), grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
                            sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
+    if (main_done) (void)hipEventRecord(main_done, stream);
     return hipGetLastError();
 }
 

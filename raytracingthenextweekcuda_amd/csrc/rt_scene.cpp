@@ -231,10 +231,20 @@ std::string load_obj_transformed(const std::string& path, v3 scl, v3 rot, v3 off
     return "";
 }
 
-void HostScene::build_bvh(const std::vector<v3>& vs, const std::vector<uint32_t>& ix, CFBvh& b) {
+void HostScene::build_bvh(const std::vector<v3>& vs, const std::vector<uint32_t>& ix, CFBvh& b,
+                          const std::string& cache_ply) {
     const auto t0 = std::chrono::steady_clock::now();
-    if (bvh_gpu && gpu_build_cf_bvh(bvh_device, vs, ix, b, 4, nullptr).empty()) ++bvh_gpu_builds;
-    else build_cf_bvh(vs, ix, b);
+    int got = 0;
+    if (!cache_ply.empty() && (bvh_cache_mode & 1)) {
+        got = read_bvh_cache(cache_ply, vs, ix, b, &cache_last_reject);
+        if (got > 0) ++cache_reads;
+        else if (got < 0) ++cache_rejected;
+    }
+    if (got <= 0) {
+        if (bvh_gpu && gpu_build_cf_bvh(bvh_device, vs, ix, b, 4, nullptr).empty()) ++bvh_gpu_builds;
+        else build_cf_bvh(vs, ix, b);
+        if (!cache_ply.empty() && (bvh_cache_mode & 2) && write_bvh_cache(cache_ply, b)) ++cache_writes;
+    }
     bvh_build_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
@@ -248,6 +258,7 @@ void HostScene::build_bvh_boxes(const std::vector<v3>& lo, const std::vector<v3>
 std::string HostScene::flatten() {
     bvh_build_ms = 0.0;
     bvh_gpu_builds = 0;
+    cache_reads = cache_writes = cache_rejected = 0;
     objs.clear();
     n_scan = 0;
     tris.clear();
@@ -333,7 +344,7 @@ std::string HostScene::flatten() {
                     ix[k] = (uint32_t)k;
                 }
                 CFBvh b;
-                build_bvh(vs, ix, b);  // reference leaves (larger: measured slower)
+                build_bvh(vs, ix, b, o.bvh_cache);  // reference leaves (larger: measured slower)
                 if (b.max_depth >= kBvhStackDepth)
                     return "mesh " + std::to_string(i) + ": BVH depth " + std::to_string(b.max_depth) +
                            " exceeds the traversal stack (" + std::to_string(kBvhStackDepth) + ")";

@@ -119,6 +119,7 @@ struct HostObject {
     uint32_t two_side = 1;
     float f[12] = {0};
     std::vector<float> tri_vertices;  // mesh: 9 floats / triangle
+    std::string bvh_cache;            // rt_mesh_ply: the PLY path (its `<ply>.bvh` cache)
 };
 constexpr uint32_t kHostCube = 100;
 
@@ -143,11 +144,19 @@ struct HostScene {
     int bvh_device = -1;
     double bvh_build_ms = 0.0;  // summed wall time of the last flatten()'s builds
     int bvh_gpu_builds = 0;     // builds the GPU ran in the last flatten()
+    // `.bvh` caches (rt_set_bvh_cache: bit 1 read, bit 2 write) and what the last
+    // flatten() did with them
+    int bvh_cache_mode = 0;
+    int cache_reads = 0, cache_writes = 0, cache_rejected = 0;
+    std::string cache_last_reject;
 
     // Returns "" on success or an error message.
     std::string flatten();
     std::string group_spheres();
-    void build_bvh(const std::vector<v3>& vs, const std::vector<uint32_t>& ix, CFBvh& b);
+    // A mesh BVH: read from `<cache_ply>.bvh` when the cache mode allows and the file is
+    // fresh and valid, else built (and written when the mode says so).
+    void build_bvh(const std::vector<v3>& vs, const std::vector<uint32_t>& ix, CFBvh& b,
+                   const std::string& cache_ply = std::string());
     void build_bvh_boxes(const std::vector<v3>& lo, const std::vector<v3>& hi, CFBvh& b);
 };
 

@@ -190,6 +190,16 @@ class Renderer:
         code = {"host": 0, "gpu": 1}[builder]
         self._check(self.L.rt_set_bvh_builder(self.ctx, code))
 
+    def set_bvh_cache(self, mode: int = 3):
+        """rt_set_bvh_cache: 1 = read `<ply>.bvh` when fresh (UpdateBoundingVolumeHierarchy,
+        BVH.cpp:500-554), 2 = write it after a build, 3 = both (the reference), 0 = off."""
+        self._check(self.L.rt_set_bvh_cache(self.ctx, int(mode)))
+
+    def bvh_cache_stats(self) -> dict:
+        r, w, x = C.c_int32(), C.c_int32(), C.c_int32()
+        self._check(self.L.rt_bvh_cache_stats(self.ctx, C.byref(r), C.byref(w), C.byref(x)))
+        return {"reads": r.value, "writes": w.value, "rejected": x.value}
+
     def bvh_build_stats(self) -> dict:
         """Wall time of the last commit's + process_triangle_data's BVH builds, and
         how many the GPU builder ran."""
@@ -290,6 +300,13 @@ class Renderer:
         data_ptr()) on a HIP stream (torch.cuda.Stream.cuda_stream)."""
         self._check(self.L.rt_render_device(self.ctx, C.byref(params), C.c_void_p(out_ptr),
                                             C.c_void_p(stream_ptr)))
+
+    def assemble_rows_device(self, params: RenderParams, world: int, staging_ptr: int, frame_ptr: int,
+                             stream_ptr: int = 0):
+        """rt_assemble_rows: the gather root's row de-interleave (world tiles of
+        rt_max_tile_rows rows, rank-major) into a (height, width, 3) device frame."""
+        self._check(self.L.rt_assemble_rows(self.ctx, C.byref(params), int(world), C.c_void_p(staging_ptr),
+                                            C.c_void_p(frame_ptr), C.c_void_p(stream_ptr)))
 
     def stats(self) -> dict:
         s = RenderStats()

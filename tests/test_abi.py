@@ -14,7 +14,7 @@ HEADER = os.path.join(S.REPO, "include", "rtmi.h")
 
 def declared_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:rt_status|int32_t|void|const char\*)\s+(rt_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:rt_status|int32_t|uint32_t|void|const char\*)\s+(rt_\w+)\s*\(", txt, re.M)))
 
 
 def test_header_and_binding_agree():

@@ -1,0 +1,66 @@
+// tools/valu_probe.hip — calibration of the VALU-issue roofline.
+//
+// A kernel whose VALU work is known exactly: each wave runs `iters` trips of 8
+// independent v_fma_f32 chains (inline asm, so nothing is folded). Two runs that
+// differ only in `iters` differ by exactly waves x 8 x d_iters VALU wave-instructions,
+// which calibrates rocprofv3's SQ_INSTS_VALU (is it the whole chip? per XCD?), and the
+// timed run gives the chip's sustained VALU issue rate against the spec peak
+// (1024 SIMDs x 2.4 GHz / 2 cycles per wave64 v_fma_f32, MI355X_MICROARCH.md).
+//   ./valu_probe [iters=20000] [waves_per_simd=4]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+__global__ __launch_bounds__(256) void valu_probe(float* out, int iters) {
+    float a0 = threadIdx.x * 1e-3f, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;
+    float a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    const float x = 0.999f, y = 1e-4f;
+    for (int i = 0; i < iters; ++i) {
+        asm volatile(
+            "v_fma_f32 %0, %8, %9, %0\n\t"
+            "v_fma_f32 %1, %8, %9, %1\n\t"
+            "v_fma_f32 %2, %8, %9, %2\n\t"
+            "v_fma_f32 %3, %8, %9, %3\n\t"
+            "v_fma_f32 %4, %8, %9, %4\n\t"
+            "v_fma_f32 %5, %8, %9, %5\n\t"
+            "v_fma_f32 %6, %8, %9, %6\n\t"
+            "v_fma_f32 %7, %8, %9, %7"
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+            : "v"(x), "v"(y));
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+}
+
+int main(int argc, char** argv) {
+    const int iters = argc > 1 ? atoi(argv[1]) : 20000;
+    const int wps = argc > 2 ? atoi(argv[2]) : 4;
+    int dev = 0, n_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1;
+    const int blocks = n_cu * wps;  // 4 waves per block: wps waves per SIMD
+    float* out = nullptr;
+    if (hipMalloc(&out, (size_t)blocks * 256 * sizeof(float)) != hipSuccess) return 1;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipLaunchKernelGGL(valu_probe, dim3(blocks), dim3(256), 0, nullptr, out, iters);  // warm-up
+    float best = 1e30f;
+    for (int rep = 0; rep < 5; ++rep) {
+        hipEventRecord(e0, nullptr);
+        hipLaunchKernelGGL(valu_probe, dim3(blocks), dim3(256), 0, nullptr, out, iters);
+        hipEventRecord(e1, nullptr);
+        hipEventSynchronize(e1);
+        float ms = 0;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (ms < best) best = ms;
+    }
+    const double waves = (double)blocks * 4;
+    const double insts = waves * 8.0 * iters;  // loop body only; the prologue/epilogue add a few per wave
+    const double peak = (double)n_cu * 4 * 2.4e9 / 2.0;
+    printf("{\"iters\": %d, \"cus\": %d, \"waves\": %.0f, \"loop_valu_insts\": %.6g, \"best_ms\": %.4f, "
+           "\"inst_per_s\": %.6g, \"spec_peak_inst_per_s\": %.6g, \"frac_of_spec\": %.4f, \"launches\": 6}\n",
+           iters, n_cu, waves, insts, best, insts / (best * 1e-3), peak, insts / (best * 1e-3) / peak);
+    hipFree(out);
+    return 0;
+}
