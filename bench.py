@@ -188,7 +188,16 @@ def load_valu_profile(workload: str):
     if not os.path.exists(path):
         return None
     with open(path) as fh:
-        return json.load(fh).get("workloads", {}).get(workload)
+        wl = json.load(fh).get("workloads", {})
+    if workload in wl:
+        return wl[workload]
+    # N > 1 shards trace the same segments: the frame's per-segment count applies
+    base = workload.rsplit("_n", 1)[0] + "_n1"
+    if base in wl:
+        ent = dict(wl[base])
+        ent["source"] = ent["source"] + " (the N = 1 frame's per-segment count)"
+        return ent
+    return None
 
 
 def load_pmc_traffic(workload: str):

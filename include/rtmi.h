@@ -58,7 +58,8 @@ typedef struct rt_ctx rt_ctx;
  * Rows are numbered with y = 0 at the BOTTOM (reference convention,
  * main.cu:183). Row tiling: global row y belongs to this call iff
  * (y / row_block) % row_world == row_rank. Output holds only the owned rows,
- * in increasing y, each width*3 floats. row_world = 1 renders the full frame. */
+ * in increasing y, each width*3 floats (col_count*3 with a column window).
+ * row_world = 1 renders the full frame. */
 typedef struct rt_render_params {
     int32_t width;
     int32_t height;
@@ -79,6 +80,11 @@ typedef struct rt_render_params {
     uint32_t flags;         /* RT_RENDER_KEEP_COUNTERS: add this launch's counters to the
                                previous ones instead of resetting them (one rt_sync_stats
                                after many launches, no per-launch host sync) */
+    /* Column window of every owned row: columns [col_begin, col_begin + col_count);
+     * col_count = 0 = the whole width. Output rows are col_count wide. The pixels are
+     * those of the full frame (camera and RNG keyed by the frame position). */
+    int32_t col_begin;
+    int32_t col_count;
 } rt_render_params;
 enum { RT_RENDER_KEEP_COUNTERS = 1 };
 

@@ -55,7 +55,8 @@ def lib():
         L.orc_length.argtypes = [fp]
         L.orc_length.restype = C.c_float
         L.orc_render.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_uint32,
-                                 C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, fp, C.POINTER(C.c_uint64)]
+                                 C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, fp, C.POINTER(C.c_uint64),
+                                 C.c_int, C.c_int]
         L.orc_philox.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.orc_uniforms.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, fp]
         L.orc_trace.argtypes = [vp, fp, fp, C.c_float, fp, fp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
@@ -66,7 +67,7 @@ def lib():
         L.orc_pt_set_bvh.argtypes = [vp, C.POINTER(C.c_uint8), C.c_int64]
         L.orc_pt_render.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_uint32,
                                     C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, fp,
-                                    C.POINTER(C.c_uint64)]
+                                    C.POINTER(C.c_uint64), C.c_int, C.c_int]
         L.orc_pt_sinf.argtypes = [C.c_float]
         L.orc_pt_sinf.restype = C.c_float
         L.orc_pt_cosf.argtypes = [C.c_float]
@@ -176,13 +177,13 @@ class OracleScene:
         return float(t.value), tuple(n), bool(front.value), int(mat.value)
 
     def render(self, width, height, spp, depth, seed=1984, sample_offset=0, row_block=1,
-               row_rank=0, row_world=1, threads=0, lanes_per_pixel=1):
+               row_rank=0, row_world=1, threads=0, lanes_per_pixel=1, col_begin=0, col_count=0):
         rows = owned_rows(height, row_block, row_rank, row_world)
-        out = np.zeros((rows, width, 3), np.float32)
+        out = np.zeros((rows, col_count or width, 3), np.float32)
         stats = (C.c_uint64 * 2)()
         rc = self.L.orc_render(self.h, width, height, spp, depth, seed, sample_offset, row_block,
                                row_rank, row_world, lanes_per_pixel, threads,
-                               out.ctypes.data_as(C.POINTER(C.c_float)), stats)
+                               out.ctypes.data_as(C.POINTER(C.c_float)), stats, col_begin, col_count)
         if rc != 0:
             raise RuntimeError(f"orc_render failed with {rc}")
         return out, {"segments": int(stats[0]), "tri_tests": int(stats[1])}
@@ -220,13 +221,14 @@ class OraclePathTrace:
             raise ValueError(f"bad .bvh image ({rc})")
 
     def render(self, cam: OracleScene, width, height, spp, bounces=5, seed=1984, sample_offset=0,
-               row_block=1, row_rank=0, row_world=1, threads=0, lanes_per_pixel=1):
+               row_block=1, row_rank=0, row_world=1, threads=0, lanes_per_pixel=1, col_begin=0,
+               col_count=0):
         rows = owned_rows(height, row_block, row_rank, row_world)
-        out = np.zeros((rows, width, 3), np.float32)
+        out = np.zeros((rows, col_count or width, 3), np.float32)
         stats = (C.c_uint64 * 3)()
         rc = self.L.orc_pt_render(self.h, cam.h, width, height, spp, bounces, seed, sample_offset,
                                   row_block, row_rank, row_world, lanes_per_pixel, threads,
-                                  out.ctypes.data_as(C.POINTER(C.c_float)), stats)
+                                  out.ctypes.data_as(C.POINTER(C.c_float)), stats, col_begin, col_count)
         if rc != 0:
             raise RuntimeError(f"orc_pt_render failed with {rc}")
         return out, {"segments": int(stats[0]), "tri_tests": int(stats[1]), "overflow": int(stats[2])}

@@ -947,11 +947,15 @@ static int owned_rows(int h, int blk, int rank, int world) {
  * stats (may be NULL): [0] segments, [1] triangle tests. */
 int orc_render(const Scene* s, int width, int height, int spp, int bounces, uint32_t seed,
                uint32_t sample_offset, int row_block, int row_rank, int row_world,
-               int lanes_per_pixel, int threads, float* out, uint64_t* stats) {
+               int lanes_per_pixel, int threads, float* out, uint64_t* stats, int col_begin,
+               int col_count) {
     const int S = lanes_per_pixel;
     if (!s->has_camera || width < 2 || height < 2 || spp < 1 || bounces < 0 || row_block < 1 ||
-        row_world < 1 || row_rank < 0 || row_rank >= row_world || S < 1 || S > 64 || (S & (S - 1)))
+        row_world < 1 || row_rank < 0 || row_rank >= row_world || S < 1 || S > 128 || (S & (S - 1)))
         return 1;
+    /* column window (rt_render_params.col_begin / col_count): columns [c0, c0 + cols) */
+    if (col_begin < 0 || col_count < 0 || col_begin + col_count > width) return 1;
+    const int c0 = col_count ? col_begin : 0, cols = col_count ? col_count : width;
     for (int i = 0; i < s->n_objs; ++i) {
         const Object* o = &s->objs[i];
         if (!o->defined) continue;
@@ -966,7 +970,7 @@ int orc_render(const Scene* s, int width, int height, int spp, int bounces, uint
     for (int lr = 0; lr < local_rows; ++lr) {
         int lb = lr / row_block;
         int y = (lb * row_world + row_rank) * row_block + (lr - lb * row_block);
-        for (int x = 0; x < width; ++x) {
+        for (int x = c0; x < c0 + cols; ++x) {
             uint32_t pixel = (uint32_t)y * (uint32_t)width + (uint32_t)x;
             /* renderKernel's `color += rayColor(...)` over samples in order. With
              * S > 1 (the product's lanes_per_pixel) sub-stream c sums samples
@@ -989,7 +993,7 @@ int orc_render(const Scene* s, int width, int height, int spp, int bounces, uint
                 color = c == 0 ? part : vadd(color, part);
             }
             V3 m = vdiv(color, (float)spp);
-            float* o = out + ((size_t)lr * width + x) * 3;
+            float* o = out + ((size_t)lr * cols + (x - c0)) * 3;
             o[0] = m.x; o[1] = m.y; o[2] = m.z;
         }
     }
@@ -1423,11 +1427,14 @@ static V3 pt_path(const PtScene* p, V3 o, V3 d, int bounces, RandState* rs, uint
  * [1] triangles tested, [2] overflow flag. */
 int orc_pt_render(const PtScene* p, const Scene* cam, int width, int height, int spp, int bounces,
                   uint32_t seed, uint32_t sample_offset, int row_block, int row_rank, int row_world,
-                  int lanes_per_pixel, int threads, float* out, uint64_t* stats) {
+                  int lanes_per_pixel, int threads, float* out, uint64_t* stats, int col_begin,
+                  int col_count) {
     const int S = lanes_per_pixel;
     if (!cam->has_camera || width < 2 || height < 2 || spp < 1 || bounces < 1 || row_block < 1 ||
-        row_world < 1 || row_rank < 0 || row_rank >= row_world || S < 1 || S > 64 || (S & (S - 1)))
+        row_world < 1 || row_rank < 0 || row_rank >= row_world || S < 1 || S > 128 || (S & (S - 1)))
         return 1;
+    if (col_begin < 0 || col_count < 0 || col_begin + col_count > width) return 1;
+    const int c0 = col_count ? col_begin : 0, cols = col_count ? col_count : width;
     if (p->n_tris > 0 && p->n_nodes == 0) return 2;
     int local_rows = owned_rows(height, row_block, row_rank, row_world);
     uint64_t segs = 0, tests = 0;
@@ -1439,7 +1446,7 @@ int orc_pt_render(const PtScene* p, const Scene* cam, int width, int height, int
     for (int lr = 0; lr < local_rows; ++lr) {
         int lb = lr / row_block;
         int y = (lb * row_world + row_rank) * row_block + (lr - lb * row_block);
-        for (int x = 0; x < width; ++x) {
+        for (int x = c0; x < c0 + cols; ++x) {
             uint32_t pixel = (uint32_t)y * (uint32_t)width + (uint32_t)x;
             V3 color = v3(0.0f, 0.0f, 0.0f);
             for (int c = 0; c < S; ++c) {
@@ -1457,7 +1464,7 @@ int orc_pt_render(const PtScene* p, const Scene* cam, int width, int height, int
                 color = c == 0 ? part : vadd(color, part);
             }
             V3 m = vdiv(color, (float)spp);
-            float* o = out + ((size_t)lr * width + x) * 3;
+            float* o = out + ((size_t)lr * cols + (x - c0)) * 3;
             o[0] = m.x; o[1] = m.y; o[2] = m.z;
         }
     }

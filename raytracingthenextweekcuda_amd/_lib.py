@@ -58,6 +58,7 @@ class RenderParams(C.Structure):
         ("max_depth", C.c_int32), ("seed", C.c_uint32), ("sample_offset", C.c_uint32),
         ("row_block", C.c_int32), ("row_rank", C.c_int32), ("row_world", C.c_int32),
         ("lanes_per_pixel", C.c_int32), ("integrator", C.c_int32), ("flags", C.c_uint32),
+        ("col_begin", C.c_int32), ("col_count", C.c_int32),
     ]
 
 

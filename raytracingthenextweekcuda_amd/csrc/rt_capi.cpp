@@ -628,6 +628,11 @@ rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& 
     L.row_rank = p->row_rank;
     L.row_world = p->row_world;
     L.local_rows = rt::owned_rows(p->height, p->row_block, p->row_rank, p->row_world);
+    if (p->col_begin < 0 || p->col_count < 0 || (int64_t)p->col_begin + p->col_count > p->width ||
+        (p->col_count == 0 && p->col_begin != 0))
+        return fail(c, RT_ERR_INVALID, "bad column window");
+    L.col0 = p->col_begin;
+    L.cols = p->col_count ? p->col_count : p->width;
     const int32_t s = p->lanes_per_pixel;
     const char* qenv = getenv("RTMI_QUEUE");
     const bool queue = !(qenv && qenv[0] == '0');  // RTMI_QUEUE=0: static grid (A/B only)
@@ -640,7 +645,7 @@ rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& 
     L.accum_scale = 0.0f;
     L.u8 = nullptr;
     L.queue = 0;
-    L.tiles_x = (p->width + 7) / 8;
+    L.tiles_x = (L.cols + 7) / 8;
     L.n_items = 0;
     L.refill = 8;
     L.q_counter = c->d_queue;
@@ -734,7 +739,7 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
     RT_HIP(c, hipEventRecord(c->ev1, st));
     const uint64_t prev_samples = keep ? c->last.samples : 0;
     c->last = rt_render_stats{};
-    c->last.samples = prev_samples + (uint64_t)L.local_rows * (uint64_t)L.width * (uint64_t)L.spp;
+    c->last.samples = prev_samples + (uint64_t)L.local_rows * (uint64_t)L.cols * (uint64_t)L.spp;
     c->last.lanes_per_pixel = (uint32_t)L.lanes_per_pixel;
     c->last.refill = L.queue ? (uint32_t)L.refill : 0u;
     c->last.queue_blocks = (uint32_t)L.queue;
@@ -805,7 +810,7 @@ static rt_status rt_render_impl(rt_ctx* c, const rt_render_params* p, float* out
     rt::RenderLaunch L;
     rt_status s = validate(c, p, L);
     if (s != RT_OK) return s;
-    size_t bytes = (size_t)L.local_rows * L.width * 3 * sizeof(float);
+    size_t bytes = (size_t)L.local_rows * L.cols * 3 * sizeof(float);
     if (!out_host && bytes) return fail(c, RT_ERR_INVALID, "null output");
     RT_HIP(c, hipSetDevice(c->device));
     if (bytes > c->d_out_bytes) {
@@ -830,7 +835,7 @@ static rt_status rt_render_u8_impl(rt_ctx* c, const rt_render_params* p, uint8_t
     rt::RenderLaunch L;
     rt_status s = validate(c, p, L);
     if (s != RT_OK) return s;
-    const size_t n = (size_t)L.local_rows * L.width * 3;
+    const size_t n = (size_t)L.local_rows * L.cols * 3;
     if (!out_host && n) return fail(c, RT_ERR_INVALID, "null output");
     RT_HIP(c, hipSetDevice(c->device));
     if (n * sizeof(float) > c->d_out_bytes) {

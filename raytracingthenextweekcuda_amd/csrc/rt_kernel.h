@@ -13,7 +13,8 @@ struct RenderLaunch {
     int32_t width, height, spp, max_depth;
     uint32_t seed, sample_offset;
     int32_t row_block, row_rank, row_world;
-    int32_t local_rows;  // rows owned by this shard (output has local_rows * width pixels)
+    int32_t local_rows;  // rows owned by this shard (output has local_rows * cols pixels)
+    int32_t col0, cols;  // column window [col0, col0 + cols) of each owned row (full: 0, width)
     int32_t lanes_per_pixel;  // S: power of two in [1, 64]
     int32_t tile_w, tile_h;   // per-wave pixel tile, tile_w * tile_h = 64 / S
     int32_t pt_has_mesh;      // pathTrace: a triangle BVH is present

@@ -857,16 +857,18 @@ __device__ __forceinline__ void store_partial(const RenderLaunch& L, uint32_t it
     p[2] = sum.z;
 }
 
-// Work-queue item -> (sub-stream, local pixel); false for items past the shard edge.
+// Work-queue item -> (sub-stream, frame column, local row); false for items past the
+// window's or the shard's edge.
 __device__ __forceinline__ bool queue_item(const RenderLaunch& L, uint32_t item, int& c, int& px,
                                            int& lrow) {
     const int SP = L.lanes_per_pixel;
     c = (int)(item & (uint32_t)(SP - 1));
     const uint32_t pl = item / (uint32_t)SP;
     const uint32_t tile = pl >> 6, w = pl & 63u;
-    px = (int)(tile % (uint32_t)L.tiles_x) * 8 + (int)(w & 7u);
+    const int lpx = (int)(tile % (uint32_t)L.tiles_x) * 8 + (int)(w & 7u);  // column in the window
+    px = L.col0 + lpx;
     lrow = (int)(tile / (uint32_t)L.tiles_x) * 8 + (int)(w >> 3);
-    return px < L.width && lrow < L.local_rows;
+    return lpx < L.cols && lrow < L.local_rows;
 }
 
 // Work-queue shards: the item range is split into kQueueShards contiguous
@@ -935,7 +937,7 @@ __global__ __launch_bounds__(256) void combine_kernel(RenderLaunch L, float* __r
         p += stride;
         acc = add(acc, v3{p[0], p[1], p[2]});
     }
-    write_pixel(L, out, ((size_t)lrow * (size_t)L.width + (size_t)px) * 3, acc, (float)L.spp);
+    write_pixel(L, out, ((size_t)lrow * (size_t)L.cols + (size_t)(px - L.col0)) * 3, acc, (float)L.spp);
 }
 
 #ifndef RT_TAIL_STEAL
@@ -1065,7 +1067,7 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     int c = lane & (SP - 1);
     const int pix = lane / SP;
     const int tw = L.tile_w, th = L.tile_h;
-    int px = blockIdx.x * (2 * tw) + (wave & 1) * tw + (pix % tw);
+    int px = L.col0 + blockIdx.x * (2 * tw) + (wave & 1) * tw + (pix % tw);
     int lrow = blockIdx.y * (2 * th) + (wave >> 1) * th + (pix / tw);
     // Row tiling: local row -> global row (y = 0 is the bottom row).
     auto global_row = [&](int lr) {
@@ -1073,7 +1075,7 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
         return (lb * L.row_world + L.row_rank) * L.row_block + (lr - lb * L.row_block);
     };
     int y = global_row(lrow);
-    bool valid = !kQueue && (px < L.width) && (lrow < L.local_rows) && (y < L.height);
+    bool valid = !kQueue && (px - L.col0 < L.cols) && (lrow < L.local_rows) && (y < L.height);
     uint32_t pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
     uint32_t item = 0;
     bool exhausted = false;
@@ -1266,7 +1268,7 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
 
     if (!kQueue && valid && c == 0) {
         const float fs = (float)L.spp;
-        write_pixel(L, out, ((size_t)lrow * (size_t)L.width + (size_t)px) * 3, sum, fs);
+        write_pixel(L, out, ((size_t)lrow * (size_t)L.cols + (size_t)(px - L.col0)) * 3, sum, fs);
     }
 
     const uint64_t ws = wave_sum_u64(cnt.segs);
@@ -1723,14 +1725,14 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
     int c = lane & (SP - 1);
     const int pix = lane / SP;
     const int tw = L.tile_w, th = L.tile_h;
-    int px = blockIdx.x * (2 * tw) + (wave & 1) * tw + (pix % tw);
+    int px = L.col0 + blockIdx.x * (2 * tw) + (wave & 1) * tw + (pix % tw);
     int lrow = blockIdx.y * (2 * th) + (wave >> 1) * th + (pix / tw);
     auto global_row = [&](int lr) {
         const int lb = lr / L.row_block;
         return (lb * L.row_world + L.row_rank) * L.row_block + (lr - lb * L.row_block);
     };
     int y = global_row(lrow);
-    const bool valid = !kQueue && (px < L.width) && (lrow < L.local_rows) && (y < L.height);
+    const bool valid = !kQueue && (px - L.col0 < L.cols) && (lrow < L.local_rows) && (y < L.height);
     uint32_t pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
     uint32_t item = 0;
     bool exhausted = false;
@@ -1959,7 +1961,7 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
     }
     if (!kQueue && valid && c == 0) {
         const float fs = (float)L.spp;
-        write_pixel(L, out, ((size_t)lrow * (size_t)L.width + (size_t)px) * 3, sum, fs);
+        write_pixel(L, out, ((size_t)lrow * (size_t)L.cols + (size_t)(px - L.col0)) * 3, sum, fs);
     }
     const uint64_t ws = wave_sum_u64(cnt.segs);
     const uint64_t wt = wave_sum_u64(cnt.tri_tests);
@@ -1988,7 +1990,7 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec& cam, const Rend
         hipLaunchKernelGGL(combine_kernel, dim3((pixels + 255u) / 256u), dim3(256), 0, stream, L, out);
         return hipGetLastError();
     }
-    dim3 grid((L.width + 2 * L.tile_w - 1) / (2 * L.tile_w),
+    dim3 grid((L.cols + 2 * L.tile_w - 1) / (2 * L.tile_w),
               (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
     if (grid.x == 0 || grid.y == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
     hipLaunchKernelGGL(pathtrace_kernel<false>, grid, block, 0, stream, sc.ktris, sc.nodes,
@@ -2036,7 +2038,7 @@ hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLau
         hipLaunchKernelGGL(combine_kernel, dim3((pixels + 255u) / 256u), dim3(256), 0, stream, L, out);
         return hipGetLastError();
     }
-    dim3 grid((L.width + 2 * L.tile_w - 1) / (2 * L.tile_w),
+    dim3 grid((L.cols + 2 * L.tile_w - 1) / (2 * L.tile_w),
               (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
     if (grid.x == 0 || grid.y == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
     if (sc.has_bvh)

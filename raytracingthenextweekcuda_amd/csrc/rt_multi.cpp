@@ -48,6 +48,8 @@ rt_status check_frame(rt_ctx* c, const rt_render_params* p, int32_t world) {
     if (!p) return fail(c, RT_ERR_INVALID, "null params");
     if (p->width < 2 || p->height < 2 || p->row_block < 1 || world < 1)
         return fail(c, RT_ERR_INVALID, "bad frame or row tiling");
+    if (p->col_begin != 0 || (p->col_count != 0 && p->col_count != p->width))
+        return fail(c, RT_ERR_INVALID, "multi-GPU frames cover the whole width (no column window)");
     if ((int64_t)p->width * p->height > (int64_t)1 << 31) return fail(c, RT_ERR_INVALID, "frame too large");
     return RT_OK;
 }

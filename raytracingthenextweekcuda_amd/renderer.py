@@ -256,22 +256,25 @@ class Renderer:
     @staticmethod
     def params(width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,
                row_rank=0, row_world=1, lanes_per_pixel=1, integrator="rayColor",
-               keep_counters=False) -> RenderParams:
+               keep_counters=False, col_begin=0, col_count=0) -> RenderParams:
         return RenderParams(width, height, spp, max_depth, seed, sample_offset, row_block,
                             row_rank, row_world, lanes_per_pixel, _integrator(integrator),
-                            KEEP_COUNTERS if keep_counters else 0)
+                            KEEP_COUNTERS if keep_counters else 0, col_begin, col_count)
 
     def render(self, width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,
-               row_rank=0, row_world=1, lanes_per_pixel=1, integrator="rayColor") -> np.ndarray:
+               row_rank=0, row_world=1, lanes_per_pixel=1, integrator="rayColor",
+               col_begin=0, col_count=0) -> np.ndarray:
         """Mean radiance of the owned rows, shape (rows, width, 3), y = 0 bottom.
         lanes_per_pixel=1 keeps the reference's sequential per-pixel sample sum;
         0 lets the library pick a lane layout that fills the GPU. integrator
         "pathTrace" runs CUDAPathTracer.cu's integrator over the
-        load_object/process_triangle_data scene (max_depth = its 5 bounces)."""
+        load_object/process_triangle_data scene (max_depth = its 5 bounces).
+        col_count > 0 renders only columns [col_begin, col_begin + col_count) of the
+        frame's rows (shape (rows, col_count, 3)); the pixels are the full frame's."""
         p = self.params(width, height, spp, max_depth, seed, sample_offset, row_block, row_rank,
-                        row_world, lanes_per_pixel, integrator)
+                        row_world, lanes_per_pixel, integrator, False, col_begin, col_count)
         rows = owned_rows(height, row_block, row_rank, row_world)
-        out = np.zeros((rows, width, 3), np.float32)
+        out = np.zeros((rows, col_count or width, 3), np.float32)
         self._check(self.L.rt_render(self.ctx, C.byref(p), out.ctypes.data_as(C.POINTER(C.c_float))))
         return out
 

@@ -410,3 +410,28 @@ def test_tail_stealing_keeps_the_fold_order(rtmi, spp, lanes, row_world):
     rows = owned_row_ids(h, block, rank, row_world)
     assert np.array_equal(img, ref[rows])
     assert st["samples"] == len(rows) * w * spp
+
+
+@pytest.mark.parametrize("queue", ["1", "0"])
+def test_column_window_equals_full_frame_pixels(monkeypatch, queue):
+    """rt_render_params.col_begin / col_count: a window of the owned rows, bit-identical to
+    the full frame's pixels (work queue and static grid; rayColor with a BVH mesh scene and
+    pathTrace), with the samples counted for the window only."""
+    import raytracingthenextweekcuda_amd as rtmi
+
+    monkeypatch.setenv("RTMI_QUEUE", queue)
+    W, H = 70, 33
+    with rtmi.Renderer(0) as r:
+        rtmi.bunny_cornell_box(r, W, H)
+        full = r.render(W, H, 4, 6, lanes_per_pixel=4)
+        win = r.render(W, H, 4, 6, lanes_per_pixel=4, row_block=3, row_rank=1, row_world=2,
+                       col_begin=9, col_count=45)
+        assert r.stats()["samples"] == rtmi.owned_rows(H, 3, 1, 2) * 45 * 4
+        assert np.array_equal(win, full[rtmi.owned_row_ids(H, 3, 1, 2), 9:54])
+    with rtmi.Renderer(0) as r:
+        rtmi.materialball(r, W, H)
+        full = r.render(W, H, 2, 5, lanes_per_pixel=2, integrator="pathTrace")
+        win = r.render(W, H, 2, 5, lanes_per_pixel=2, integrator="pathTrace", col_begin=61, col_count=9)
+        assert np.array_equal(win, full[:, 61:70])
+        with pytest.raises(rtmi.RTError):
+            r.render(W, H, 2, 5, col_begin=62, col_count=9)  # past the right edge

@@ -149,3 +149,22 @@ def test_cornellbox1_segments_per_sample():
     img, st = sc.render(128, 128, 4, 4)
     assert 3.38 < st["segments"] / (128 * 128 * 4) < 3.48
     assert np.isfinite(img).all() and img.min() >= 0
+
+
+def test_oracle_column_window_equals_the_full_rows():
+    """rt_render_params' column window, restated: columns [c0, c0 + n) of a row are the full
+    frame's pixels (camera and RNG keyed by the frame position), for both integrators."""
+    from oracle import oracle as orc
+
+    W, H = 40, 24
+    sc = orc.yaml_scene(os.path.join(S.SCENES, "cornellbox1.yaml"), S.MODELS, W, H)
+    full, _ = sc.render(W, H, 4, 4, row_block=1, row_rank=5, row_world=6, lanes_per_pixel=2)
+    win, st = sc.render(W, H, 4, 4, row_block=1, row_rank=5, row_world=6, lanes_per_pixel=2,
+                        col_begin=7, col_count=13)
+    assert win.shape == (full.shape[0], 13, 3)
+    assert np.array_equal(win, full[:, 7:20])
+    cam = orc.yaml_scene(os.path.join(S.SCENES, "cornellbox2.yaml"), S.MODELS, W, H)
+    pt, _ = S.build_pathtrace_oracle("materialball")
+    fullp, _ = pt.render(cam, W, H, 2, 5, row_block=2, row_rank=1, row_world=3)
+    winp, _ = pt.render(cam, W, H, 2, 5, row_block=2, row_rank=1, row_world=3, col_begin=30, col_count=10)
+    assert np.array_equal(winp, fullp[:, 30:40])
