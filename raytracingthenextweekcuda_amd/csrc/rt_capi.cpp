@@ -121,6 +121,7 @@ rt_status rt_create(int32_t device, rt_ctx** out) {
         }
         if (hipSetDevice(device) != hipSuccess ||
             hipMalloc(&c->d_counters, rt::kNumCounters * sizeof(unsigned long long)) != hipSuccess ||
+            hipMalloc(&c->d_cam, sizeof(rt::CamRec)) != hipSuccess ||
             hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
             delete c;
             return RT_ERR_HIP;
@@ -143,6 +144,7 @@ void rt_destroy(rt_ctx* c) {
         free_device(c);
         free_pathtrace(c);
         (void)hipFree(c->d_counters);
+        (void)hipFree(c->d_cam);
         (void)hipFree(c->d_out);
         (void)hipFree(c->d_u8);
         (void)hipFree(c->d_queue);
@@ -647,10 +649,17 @@ rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& 
     L.queue = 0;
     L.tiles_x = (L.cols + 7) / 8;
     L.n_items = 0;
+    L.n_pix = 0;
+    L.tiles_x_div = rt::make_udiv((uint32_t)L.tiles_x);
+    L.row_block_div = rt::make_udiv((uint32_t)L.row_block);
     L.refill = 8;
     L.q_counter = c->d_queue;
     L.partial = nullptr;
     L.pt_has_mesh = c->pt_tris > 0 ? 1 : 0;
+    // LDS traversal stacks hold one pending subtree per level below the root: the scene's
+    // deepest BVH (rayColor meshes and sphere groups, or the pathTrace tree) sizes them
+    const int depth = p->integrator == RT_INTEGRATOR_PATHTRACE ? c->pt_bvh.max_depth : c->scene.bvh_max_depth;
+    L.stack_depth = depth > 0 ? depth : 1;
     L.pt_scale = c->pt_scale;
     return RT_OK;
 }
@@ -688,6 +697,7 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
         if (have) {
             L.queue = rt::queue_blocks(c->n_cu);
             L.n_items = (uint32_t)items;
+            L.n_pix = (uint32_t)(items >> L.sp_log2);
             // refill threshold (idle lanes a wave collects before one dequeue): 4 for
             // short shards, whose tail it shortens, and for long items (>= 16 samples),
             // where waiting for 8 idle lanes wastes lane time; 8 otherwise, where fewer
@@ -726,15 +736,24 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
         k1 = c->kev1[c->n_kev];
         ++c->n_kev;
     }
+    // the kernels read the camera from device memory; refresh it when it changed (after
+    // the previous launch, which may still be reading it, has finished)
+    if (!c->cam_uploaded || memcmp(&c->cam_on_device, &c->scene.camera, sizeof(rt::CamRec)) != 0) {
+        if (c->launched_before) RT_HIP(c, hipEventSynchronize(c->ev1));
+        RT_HIP(c, hipMemcpy(c->d_cam, &c->scene.camera, sizeof(rt::CamRec), hipMemcpyHostToDevice));
+        c->cam_on_device = c->scene.camera;
+        c->cam_uploaded = true;
+    }
+    c->launched_before = true;
     RT_HIP(c, hipEventRecord(c->ev0, st));
     if (k0) RT_HIP(c, hipEventRecord(k0, st));
     if (p->integrator == RT_INTEGRATOR_PATHTRACE) {
         rt::PtSceneArgs pt{c->d_pt_tris, c->d_pt_nodes, c->d_pt_list};
-        RT_HIP(c, rt::launch_pathtrace(pt, c->scene.camera, L, out, c->d_counters, st, k1));
+        RT_HIP(c, rt::launch_pathtrace(pt, c->d_cam, L, out, c->d_counters, st, k1));
     } else {
         rt::SceneArgs sc{c->d_objs,   c->d_tris,  c->d_mats,  c->d_nodes,
                          c->d_tri_orig, c->n_objs, c->n_mats, !c->scene.nodes.empty()};
-        RT_HIP(c, rt::launch_render(sc, c->scene.camera, L, out, c->d_counters, st, k1));
+        RT_HIP(c, rt::launch_render(sc, c->d_cam, L, out, c->d_counters, st, k1));
     }
     RT_HIP(c, hipEventRecord(c->ev1, st));
     const uint64_t prev_samples = keep ? c->last.samples : 0;

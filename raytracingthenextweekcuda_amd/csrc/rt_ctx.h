@@ -32,6 +32,10 @@ struct rt_ctx {
     int n_objs = 0;
     int n_mats = 0;
     unsigned long long* d_counters = nullptr;
+    rt::CamRec* d_cam = nullptr;  // device copy of scene.camera read by the kernels
+    rt::CamRec cam_on_device{};   // what d_cam holds (valid when cam_uploaded)
+    bool cam_uploaded = false;
+    bool launched_before = false;  // ev1 has been recorded by a launch
     float* d_out = nullptr;   // staging buffer for rt_render (host output)
     size_t d_out_bytes = 0;
     uint8_t* d_u8 = nullptr;  // staging buffer for rt_render_u8

@@ -8,6 +8,33 @@
 
 namespace rt {
 
+// Unsigned division by a launch-invariant divisor without a divide: the multiply-high
+// with add-back of Granlund & Montgomery (the sequence compilers emit for constant
+// divisors), exact for every 32-bit dividend. The kernel's generic divisions by
+// launch parameters otherwise keep per-lane reciprocal constants alive in VGPRs for
+// the whole persistent loop (and the traversal kernel spilled them to scratch).
+struct UDiv {
+    uint32_t d, m, s1, s2;
+};
+inline UDiv make_udiv(uint32_t d) {
+    uint32_t l = 0;
+    while (l < 32 && ((uint64_t)1 << l) < d) ++l;  // ceil(log2 d)
+    UDiv r;
+    r.d = d;
+    r.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1);
+    r.s1 = l < 1 ? l : 1;
+    r.s2 = l > 1 ? l - 1 : 0;
+    return r;
+}
+__host__ __device__ __forceinline__ uint32_t udiv(uint32_t x, const UDiv& D) {
+#ifdef __HIP_DEVICE_COMPILE__
+    const uint32_t t = __umulhi(x, D.m);
+#else
+    const uint32_t t = (uint32_t)(((uint64_t)x * D.m) >> 32);
+#endif
+    return (t + ((x - t) >> D.s1)) >> D.s2;
+}
+
 // Per-launch parameters (rt_render_params after validation).
 struct RenderLaunch {
     int32_t width, height, spp, max_depth;
@@ -15,9 +42,13 @@ struct RenderLaunch {
     int32_t row_block, row_rank, row_world;
     int32_t local_rows;  // rows owned by this shard (output has local_rows * cols pixels)
     int32_t col0, cols;  // column window [col0, col0 + cols) of each owned row (full: 0, width)
-    int32_t lanes_per_pixel;  // S: power of two in [1, 64]
+    int32_t lanes_per_pixel;  // S: power of two in [1, 128]
+    int32_t sp_log2;          // log2 S
     int32_t tile_w, tile_h;   // per-wave pixel tile, tile_w * tile_h = 64 / S
     int32_t pt_has_mesh;      // pathTrace: a triangle BVH is present
+    int32_t stack_depth;      // BVH traversal stack entries per lane = the scene's BVH depth (>= 1): an
+                              // ordered traversal holds at most one pending subtree per level below the
+                              // root, so the LDS stacks are sized per scene (dynamic LDS)
     float pt_scale;           // pathTrace: max |coordinate| of the triangles
     // Pixel output (Canvas.h:58-98): accumulate = 0 writes the mean color/spp to
     // `out` (and gamma(mean) to u8 when set: writePixel); accumulate = 1 adds the
@@ -34,6 +65,9 @@ struct RenderLaunch {
     int32_t queue;
     int32_t tiles_x;
     uint32_t n_items;
+    uint32_t n_pix;           // n_items / S: the pixels of the launch (one partial-sum plane)
+    UDiv tiles_x_div;         // tile -> (tile row, tile column)
+    UDiv row_block_div;       // local row -> local row block
     int32_t refill;  // idle lanes that trigger a wave's refill (set per launch, see rt_capi.cpp)
     uint32_t* q_counter;
     float* partial;
@@ -61,6 +95,8 @@ inline void choose_layout(RenderLaunch& L, int32_t requested, bool queue) {
         while (2 * s <= 32 && 2 * s <= L.spp && px * 2 * s <= cap) s *= 2;
     }
     L.lanes_per_pixel = s;
+    L.sp_log2 = 0;
+    while ((1 << L.sp_log2) < s) ++L.sp_log2;
     const int32_t p = s <= 64 ? 64 / s : 1;  // S > 64 (work queue only): no static tile
     L.tile_w = p >= 8 ? 8 : p;
     L.tile_h = p / L.tile_w;
@@ -86,14 +122,15 @@ struct PtSceneArgs {
 
 // `main_done` (may be null) is recorded on `stream` right after the megakernel,
 // before the work queue's combine pass.
-hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec& cam, const RenderLaunch& L,
+// `cam`: the camera record in device memory (rt_capi.cpp keeps it current).
+hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const RenderLaunch& L,
                             float* out, unsigned long long* counters, hipStream_t stream,
                             hipEvent_t main_done);
 
 // Workgroups of the persistent work-queue grid (n_cu x resident blocks per CU).
 int queue_blocks(int n_cu);
 
-hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLaunch& L,
+hipError_t launch_render(const SceneArgs& sc, const CamRec* cam, const RenderLaunch& L,
                          float* out, unsigned long long* counters, hipStream_t stream, hipEvent_t main_done);
 
 // Frame assembly on the gather root (rt_rows.hip): staging = world tiles of

@@ -203,13 +203,26 @@ struct Hit {
 struct WaveLds {
     unsigned long long key[64];  // per-ray (t bits << 32 | triangle) minima
     int32_t src[64];             // rank -> lane of the rays wanting a mesh
+    uint32_t grp_s[64], grp_m[64];  // per-lane sphere-group test counts (Counters::grp drained per trip)
 #if RT_MESH_TWO_PHASE
     uint16_t ring[128];          // pair ids that passed the backface cull, awaiting the full test
 #endif
 };
 
+// Event counters of one wave, laid out to keep the VGPR file free for the traversal:
+// amounts that differ per lane stay per lane (node visits, BVH-leaf triangle tests);
+// events counted at wave-uniform points (segments, mesh-box tests, brute-force
+// triangle tests) accumulate as wave-uniform scalars from ballots (SGPRs); the two
+// sphere-group counts share one VGPR (16 | 16 bits, drained to LDS every loop trip);
+// a stack overflow is a flag stored straight into the device counters.
 struct Counters {
-    uint32_t segs, tri_tests, box_tests, node_visits, overflow, grp_spheres, grp_moving;
+    uint32_t tri_tests, node_visits;     // per lane
+    uint32_t grp;                        // per lane, this trip: spheres | moving spheres << 16
+    uint32_t segs, box_tests, tri_wave;  // wave-uniform
+    unsigned long long* overflow_flag;   // counters[4]
+    // low word only (the counters are zeroed per launch): a 32-bit constant the compiler
+    // rematerialises instead of keeping a 64-bit one in two VGPRs for the whole kernel
+    __device__ __forceinline__ void overflow() const { *reinterpret_cast<uint32_t*>(overflow_flag) = 1u; }
 };
 
 // Diagnostic build only (RT_STAMPS): wave-uniform s_memtime section timers,
@@ -229,6 +242,13 @@ __device__ __forceinline__ uint64_t stamp() {
 #define RT_ACC(slot, a, b)
 #endif
 
+// Sets an LDS 64-bit minimum slot to +inf (all ones).
+__device__ __forceinline__ void key_reset(unsigned long long& k) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(&k);
+    w[0] = ~0u;
+    w[1] = ~0u;
+}
+
 // The lane's rank among the set bits of `mask` below it.
 __device__ __forceinline__ int lane_rank(uint64_t mask) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
@@ -240,21 +260,21 @@ __device__ __forceinline__ int lane_rank(uint64_t mask) {
 // mesh box. The result equals the reference's sequential scan: the smallest t
 // below the caller's closestSoFar, ties resolved to the lowest triangle index.
 __device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, uint32_t base,
-                                             uint32_t m, bool want, v3 o, v3 d, Hit& h, int32_t obj,
+                                             uint32_t m, uint32_t mesh_magic, bool want, v3 o, v3 d, Hit& h, int32_t obj,
                                              uint32_t order, WaveLds& W, int lane) {
     const uint64_t mask = __ballot(want);
     if (mask == 0) return;
     const int rank = lane_rank(mask);
     if (want) {
         W.src[rank] = lane;
-        W.key[rank] = ~0ull;
+        key_reset(W.key[rank]);
     }
     __builtin_amdgcn_wave_barrier();
     const uint32_t total = (uint32_t)__popcll(mask) * m;
     const float t0 = h.t;
     // p / m as a multiply-high: magic = ceil(2^32 / m) is exact for p < 2^26 (p < 64 * 64
     // here); m = 1 (2^32 does not fit) divides by itself
-    const uint32_t magic = m > 1u ? 0xFFFFFFFFu / m + 1u : 0u;
+    const uint32_t magic = mesh_magic;  // ceil(2^32 / m), precomputed at commit (rt_scene.cpp)
 #if RT_MESH_TWO_PHASE
     // Phase 1 runs only TriangleMesh.cu:72's backface cull over the packed pairs and
     // queues the survivors (about half of a closed mesh's pairs) in a 128-entry LDS
@@ -341,7 +361,7 @@ __device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, ui
                                          const uint32_t* __restrict__ tri_orig,
                                          const BvhNode* __restrict__ nodes, uint32_t root, bool want,
                                          v3 o, v3 d, v3 inv, Hit& h, int32_t obj, uint32_t order,
-                                         uint32_t* stack, Counters& cnt) {
+                                         uint32_t* stack, Counters& cnt, int cap) {
     if (!want) return;
     const float t0 = h.t;
     float best = t0;
@@ -383,8 +403,8 @@ __device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, ui
         const bool hl = node_hit(nl, o, inv, best, tl);
         const bool hr = node_hit(nr, o, inv, best, tr);
         if (hl && hr) {
-            if (sp + 1 > kStackDepth) {
-                cnt.overflow = 1;
+            if (sp + 1 > cap) {
+                cnt.overflow();
                 break;
             }
             const bool left_first = tl <= tr;
@@ -422,10 +442,10 @@ __device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
                                               const BvhNode* __restrict__ nodes, uint32_t root, uint32_t base,
                                               bool want, v3 o, v3 d, v3 inv, Hit& h, int32_t obj,
                                               uint32_t order, uint32_t* wstack, WaveLds& W, int lane,
-                                              Counters& cnt) {
+                                              Counters& cnt, int cap) {
     const uint64_t wm = __ballot(want);
     if (wm == 0) return;
-    W.key[lane] = ~0ull;
+    key_reset(W.key[lane]);
     int owner = lane;
     v3 ro = o, rd = d, ri = inv;
     float t0 = h.t;    // the ray's closestSoFar: accept t <= t0
@@ -454,22 +474,25 @@ __device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
             int vic = lane;
             const bool thief = idle && lane_rank(im) < nv;
             if (thief) vic = W.src[lane_rank(im)];
-            const int vb = __shfl(bot, vic, 64);
-            const int v_owner = __shfl(owner, vic, 64);
-            const v3 v_o{__shfl(ro.x, vic, 64), __shfl(ro.y, vic, 64), __shfl(ro.z, vic, 64)};
-            const v3 v_d{__shfl(rd.x, vic, 64), __shfl(rd.y, vic, 64), __shfl(rd.z, vic, 64)};
-            const v3 v_i{__shfl(ri.x, vic, 64), __shfl(ri.y, vic, 64), __shfl(ri.z, vic, 64)};
-            const float v_t0 = __shfl(t0, vic, 64), v_best = __shfl(best, vic, 64);
-            const int vt = vb;  // the victim's oldest pending subtree (newest: same speed, measured)
+            const int vt = __shfl(bot, vic, 64);  // the victim's oldest pending subtree (newest: same speed)
+            if (thief) flush();  // publish this lane's result for its old ray first
+            // take over the victim's ray one register at a time (few temporaries live at once)
+            auto take = [&](float& x) {
+                const float v = __shfl(x, vic, 64);
+                if (thief) x = v;
+            };
+            {
+                const int v_owner = __shfl(owner, vic, 64);
+                if (thief) owner = v_owner;
+            }
+            take(ro.x); take(ro.y); take(ro.z);
+            take(rd.x); take(rd.y); take(rd.z);
+            take(ri.x); take(ri.y); take(ri.z);
+            take(t0);
+            take(best);
             if (thief) {
                 const uint32_t entry = wstack[vt * 64 + vic];
-                flush();
-                owner = v_owner;
-                ro = v_o;
-                rd = v_d;
-                ri = v_i;
-                t0 = v_t0;
-                best = fminf(v_best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
+                best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
                 sp = bot = 0;
                 cur = nodes[entry];
                 ++cnt.node_visits;
@@ -516,8 +539,8 @@ __device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
         const bool hl = node_hit(nl, ro, ri, best, tl);
         const bool hr = node_hit(nr, ro, ri, best, tr);
         if (hl && hr) {
-            if (sp + 1 > kStackDepth) {
-                cnt.overflow = 1;
+            if (sp + 1 > cap) {
+                cnt.overflow();
                 has = false;
                 sp = bot = 0;
                 continue;
@@ -587,7 +610,7 @@ __device__ __forceinline__ float sphere_candidate(const ObjRec& ob, v3 o, v3 d, 
 __device__ __forceinline__ void sphere_group(const ObjRec* __restrict__ objs,
                                              const BvhNode* __restrict__ nodes, uint32_t root,
                                              bool live, const Ray& ray, v3 inv, Hit& h,
-                                             uint32_t* stack, Counters& cnt) {
+                                             uint32_t* stack, Counters& cnt, int cap) {
     if (!live) return;
     const v3 o = ray.o, d = ray.d;
     BvhNode cur = nodes[root];
@@ -607,8 +630,7 @@ __device__ __forceinline__ void sphere_group(const ObjRec* __restrict__ objs,
             const uint32_t n = cur.b & 0x7FFFFFFFu;
             for (uint32_t k = cur.a; k < cur.a + n; ++k) {
                 const ObjRec ob = load_obj(objs, (int)k);
-                if (ob.type == kObjMovingSphere) ++cnt.grp_moving;
-                else ++cnt.grp_spheres;
+                cnt.grp += ob.type == kObjMovingSphere ? 0x10000u : 1u;
                 h.merge(sphere_candidate(ob, o, d, ray.time), ob.order, true, (int32_t)k, -1);
             }
             has = false;
@@ -621,8 +643,8 @@ __device__ __forceinline__ void sphere_group(const ObjRec* __restrict__ objs,
         const bool hl = node_hit(nl, o, inv, h.t, tl);
         const bool hr = node_hit(nr, o, inv, h.t, tr);
         if (hl && hr) {
-            if (sp + 1 > kStackDepth) {
-                cnt.overflow = 1;
+            if (sp + 1 > cap) {
+                cnt.overflow();
                 break;
             }
             const bool left_first = tl <= tr;
@@ -750,28 +772,27 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             // TriangleMesh::hit (TriangleMesh.cu:34-117): the AABB early-out
             // gates the triangle scan exactly as in the reference.
             const bool want = live && box_hit(f, o, inv);
-            const uint32_t root = ob.u2;
-            if (live) {
-                ++cnt.box_tests;
-                if (want && root == kNoBvh) cnt.tri_tests += ob.u1;
-            }
+            const uint32_t root = ob.u2;  // wave-uniform (scalar record)
+            cnt.box_tests += (uint32_t)__popcll(__ballot(live));
+            if (root == kNoBvh) cnt.tri_wave += (uint32_t)__popcll(__ballot(want)) * ob.u1;
             if (!kBvh || root == kNoBvh) {
                 RT_STAMP(t_m0);
-                mesh_compact(S.tris, ob.u0, ob.u1, want, o, d, h, i, ob.order, W, lane);
+                mesh_compact(S.tris, ob.u0, ob.u1, __float_as_uint(ob.f[6]), want, o, d, h, i, ob.order, W, lane);
                 RT_STAMP(t_m1);
                 RT_ACC(3, t_m0, t_m1);
             } else {
 #if RT_BVH_STEAL
                 mesh_bvh_coop(S.tris, S.tri_orig, S.nodes, root, ob.u0, want, o, d, inv, h, i, ob.order,
-                              stack - lane, W, lane, cnt);
+                              stack - lane, W, lane, cnt, S.stack_cap);
 #else
-                mesh_bvh(S.tris, S.tri_orig, S.nodes, root, want, o, d, inv, h, i, ob.order, stack, cnt);
+                mesh_bvh(S.tris, S.tri_orig, S.nodes, root, want, o, d, inv, h, i, ob.order, stack, cnt,
+                         S.stack_cap);
 #endif
             }
         } else if (ob.type == kObjMedium) {
             h.merge(live ? medium_candidate(ob, o, d, rng) : __builtin_nanf(""), ob.order, false, i, -1);
         } else if (kBvh) {  // kObjSphereGroup
-            sphere_group(S.objs, S.nodes, ob.u2, live, ray, inv, h, stack, cnt);
+            sphere_group(S.objs, S.nodes, ob.u2, live, ray, inv, h, stack, cnt, S.stack_cap);
         }
     }
     h.finish();
@@ -780,8 +801,19 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
 
 // renderKernel sample loop body (main.cu:179-185) + Camera::getRay
 // (Camera.h:151-168): starts sample s's stream and returns its camera ray.
-__device__ __forceinline__ Ray camera_sample(const CamRec& cam, const RenderLaunch& L, Rng& rng,
+// The camera record is re-read from its device copy (scalar loads, K$ hits) at each
+// sample start instead of being held in 21 SGPRs for the whole persistent loop: the empty asm makes the pointer opaque, so the loads cannot be
+// hoisted. SGPRs are the scarce resource of the megakernels (their spills take VGPR
+// lanes and VALU readlane/writelane instructions).
+template <typename T>
+__device__ __forceinline__ const T* opaque(const T* p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+__device__ __forceinline__ Ray camera_sample(const CamRec* camp, const RenderLaunch& L, Rng& rng,
                                              uint32_t pixel, int px, int y, int s, float fw, float fh) {
+    const CamRec cam = *opaque(camp);
     rng.begin(L.seed, pixel, L.sample_offset + (uint32_t)s);
     const float rx = rng.next();
     const float ry = rng.next();
@@ -850,8 +882,8 @@ __device__ __forceinline__ void write_pixel(const RenderLaunch& L, float* __rest
 // Partial sums are stored sub-stream major, [c][pixel][3], so the combine pass
 // reads them coalesced.
 __device__ __forceinline__ void store_partial(const RenderLaunch& L, uint32_t item, v3 sum) {
-    const uint32_t S = (uint32_t)L.lanes_per_pixel, npix = L.n_items / S;
-    float* p = L.partial + ((size_t)(item & (S - 1)) * npix + item / S) * 3;
+    const uint32_t S = (uint32_t)L.lanes_per_pixel;
+    float* p = L.partial + ((size_t)(item & (S - 1)) * L.n_pix + (item >> L.sp_log2)) * 3;
     p[0] = sum.x;
     p[1] = sum.y;
     p[2] = sum.z;
@@ -863,11 +895,12 @@ __device__ __forceinline__ bool queue_item(const RenderLaunch& L, uint32_t item,
                                            int& lrow) {
     const int SP = L.lanes_per_pixel;
     c = (int)(item & (uint32_t)(SP - 1));
-    const uint32_t pl = item / (uint32_t)SP;
+    const uint32_t pl = item >> L.sp_log2;
     const uint32_t tile = pl >> 6, w = pl & 63u;
-    const int lpx = (int)(tile % (uint32_t)L.tiles_x) * 8 + (int)(w & 7u);  // column in the window
+    const uint32_t trow = udiv(tile, L.tiles_x_div);
+    const int lpx = (int)(tile - trow * (uint32_t)L.tiles_x) * 8 + (int)(w & 7u);  // column in the window
     px = L.col0 + lpx;
-    lrow = (int)(tile / (uint32_t)L.tiles_x) * 8 + (int)(w >> 3);
+    lrow = (int)trow * 8 + (int)(w >> 3);
     return lpx < L.cols && lrow < L.local_rows;
 }
 
@@ -930,7 +963,7 @@ __global__ __launch_bounds__(256) void combine_kernel(RenderLaunch L, float* __r
     const int SP = L.lanes_per_pixel;
     int c, px, lrow;
     if (pl * (uint32_t)SP >= L.n_items || !queue_item(L, pl * (uint32_t)SP, c, px, lrow)) return;
-    const size_t stride = (size_t)(L.n_items / (uint32_t)SP) * 3;  // one sub-stream plane
+    const size_t stride = (size_t)L.n_pix * 3;  // one sub-stream plane
     const float* p = L.partial + (size_t)pl * 3;
     v3 acc{p[0], p[1], p[2]};
     for (int j = 1; j < SP; ++j) {
@@ -945,8 +978,8 @@ __global__ __launch_bounds__(256) void combine_kernel(RenderLaunch L, float* __r
 #endif
 
 // End (exclusive) of sub-stream c's sample sequence c, c + SP, ... < spp.
-__device__ __forceinline__ int sub_end(int spp, int c, int SP) {
-    return spp > c ? c + ((spp - c + SP - 1) / SP) * SP : c;
+__device__ __forceinline__ int sub_end(int spp, int c, int SP, int sp_log2) {
+    return spp > c ? c + (((spp - c + SP - 1) >> sp_log2) << sp_log2) : c;
 }
 
 // A sample's path finished with radiance `contrib`. Owners fold it into the
@@ -1014,7 +1047,7 @@ __device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, i
     // 2. pair the r-th idle lane with the r-th lane that has a spare (unstarted, not
     //    current) sample; items of at most 4 samples (one byte per position in tl_pack)
     const bool idle = !alive && !waiting && !held;
-    const bool spare = alive && towner < 0 && s + SP < own_end && sub_end(L.spp, c, SP) - c <= 4 * SP;
+    const bool spare = alive && towner < 0 && s + SP < own_end && sub_end(L.spp, c, SP, L.sp_log2) - c <= 4 * SP;
     const uint64_t im = __ballot(idle), vm = __ballot(spare);
     if (im == 0 || vm == 0) return;
     const int nv = __popcll(vm), ni = __popcll(im);
@@ -1029,7 +1062,7 @@ __device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, i
     const uint32_t v_pixel = (uint32_t)__shfl((int)pixel, vic, 64);
     if (spare && rv < ni) {  // robbed: its last unstarted sample goes to the thief of the same rank
         own_end -= SP;
-        const int pos = (own_end - c) / SP;
+        const int pos = (own_end - c) >> L.sp_log2;
         tl_pack |= ((uint32_t)W.key[rv] + 1u) << (8 * pos);
     }
     if (thief) {
@@ -1049,16 +1082,19 @@ template <bool kBvh, bool kQueue>
 __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
     const MatRec* __restrict__ mats, const BvhNode* __restrict__ nodes,
-    const uint32_t* __restrict__ tri_orig, int n_objs, CamRec cam, RenderLaunch L,
+    const uint32_t* __restrict__ tri_orig, int n_objs, const CamRec* __restrict__ cam, RenderLaunch L,
     float* __restrict__ out, unsigned long long* __restrict__ counters) {
-    const SceneArgs S{objs, tris, mats, nodes, tri_orig, n_objs, 0, kBvh};
+    const SceneArgs S{objs, tris, mats, nodes, tri_orig, n_objs, 0, kBvh, L.stack_depth};
     __shared__ WaveLds lds[kWavesPerBlock];
-    __shared__ uint32_t stacks[kBvh ? kWavesPerBlock : 1][kBvh ? kStackDepth * 64 : 1];
+    // traversal stacks (kBvh): kWavesPerBlock x L.stack_depth x 64 lanes, sized per scene at launch
+    extern __shared__ uint32_t dyn_stacks[];
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     WaveLds& W = lds[wave];
-    uint32_t* stack = kBvh ? &stacks[wave][lane] : nullptr;
+    W.grp_s[lane] = 0;
+    W.grp_m[lane] = 0;
+    uint32_t* stack = kBvh ? dyn_stacks + (size_t)wave * L.stack_depth * 64 + lane : nullptr;
 
     // Lane layout: SP = lanes_per_pixel adjacent lanes share one pixel and split
     // its samples (sub-lane c takes samples c, c+SP, c+2SP, ...). A wave covers
@@ -1071,7 +1107,7 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     int lrow = blockIdx.y * (2 * th) + (wave >> 1) * th + (pix / tw);
     // Row tiling: local row -> global row (y = 0 is the bottom row).
     auto global_row = [&](int lr) {
-        const int lb = lr / L.row_block;
+        const int lb = (int)udiv((uint32_t)lr, L.row_block_div);
         return (lb * L.row_world + L.row_rank) * L.row_block + (lr - lb * L.row_block);
     };
     int y = global_row(lrow);
@@ -1082,12 +1118,12 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     int shard = (int)(blockIdx.x % kQueueShards), shards_tried = 0;  // wave-uniform
 
     v3 sum{0.0f, 0.0f, 0.0f};
-    Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    Counters cnt{0, 0, 0, 0, 0, 0, counters + 4};
     int s = c;
     bool alive = valid && s < L.spp;
     // the sub-stream's samples are c, c + SP, ... < own_end; at the end of the queue
     // other lanes of the wave may take the last unstarted ones (tail stealing)
-    int own_end = sub_end(L.spp, c, SP);
+    int own_end = sub_end(L.spp, c, SP, L.sp_log2);
     uint32_t tl_pack = 0;  // owner: thief lane + 1 per stolen item position (8 bits each)
     int towner = -1;       // thief: the lane whose sample it traces
     bool held = false;     // thief: finished, its sample's radiance waits in `thr`
@@ -1113,7 +1149,7 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
                 s = c;
                 sum = v3{0.0f, 0.0f, 0.0f};
                 alive = s < L.spp;
-                own_end = sub_end(L.spp, c, SP);
+                own_end = sub_end(L.spp, c, SP, L.sp_log2);
                 // a sub-stream with no samples (S > spp) still owns its partial-sum slot
                 if (!alive) store_partial(L, item, sum);
                 need_cam = true;
@@ -1152,8 +1188,13 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
         );
         RT_STAMP(t_c);
         RT_ACC(1, t_b, t_c);
+        cnt.segs += (uint32_t)__popcll(__ballot(live));
+        if (kBvh && __ballot(cnt.grp != 0)) {  // drain the 16-bit sphere-group counts
+            W.grp_s[lane] += cnt.grp & 0xFFFFu;
+            W.grp_m[lane] += cnt.grp >> 16;
+            cnt.grp = 0;
+        }
         if (!live) continue;
-        ++cnt.segs;
 
         bool done;
         v3 contrib;
@@ -1271,13 +1312,12 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
         write_pixel(L, out, ((size_t)lrow * (size_t)L.cols + (size_t)(px - L.col0)) * 3, sum, fs);
     }
 
-    const uint64_t ws = wave_sum_u64(cnt.segs);
-    const uint64_t wt = wave_sum_u64(cnt.tri_tests);
-    const uint64_t wb = wave_sum_u64(cnt.box_tests);
+    const uint64_t ws = cnt.segs;
+    const uint64_t wt = wave_sum_u64(cnt.tri_tests) + cnt.tri_wave;
+    const uint64_t wb = cnt.box_tests;
     const uint64_t wn = wave_sum_u64(cnt.node_visits);
-    const uint64_t wo = wave_sum_u64(cnt.overflow);
-    const uint64_t wgs = wave_sum_u64(cnt.grp_spheres);
-    const uint64_t wgm = wave_sum_u64(cnt.grp_moving);
+    const uint64_t wgs = wave_sum_u64(W.grp_s[lane] + (cnt.grp & 0xFFFFu));
+    const uint64_t wgm = wave_sum_u64(W.grp_m[lane] + (cnt.grp >> 16));
 #ifdef RT_STAMPS
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(&counters[8 + k], (unsigned long long)tm[k]);
@@ -1287,7 +1327,6 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
         atomicAdd(&counters[1], (unsigned long long)wt);
         atomicAdd(&counters[2], (unsigned long long)wb);
         if (wn) atomicAdd(&counters[3], (unsigned long long)wn);
-        if (wo) atomicAdd(&counters[4], (unsigned long long)wo);
         if (wgs) atomicAdd(&counters[5], (unsigned long long)wgs);
         if (wgm) atomicAdd(&counters[6], (unsigned long long)wgm);
     }
@@ -1477,7 +1516,7 @@ __device__ __forceinline__ void pt_leaf(const KTri* __restrict__ ktris,
                                             const CFNode* __restrict__ nodes,
                                             const int32_t* __restrict__ tri_list,
                                             uint32_t* stack, const PtRay& r, int avoid,
-                                            float len_d, float eps, PtBest& b, Counters& cnt) {
+                                            float len_d, float eps, PtBest& b, Counters& cnt, int cap) {
     auto pruned = [&](float tw) { return tw > 0.0f && tw * len_d > b.dist * 1.0001f + eps; };
     CFNode cur = nodes[0];
     ++cnt.node_visits;
@@ -1523,8 +1562,8 @@ __device__ __forceinline__ void pt_leaf(const KTri* __restrict__ ktris,
         h0 = h0 && !pruned(w0);
         h1 = h1 && !pruned(w1);
         if (h0 && h1) {
-            if (sp + 1 > kStackDepth) {
-                cnt.overflow = 1;
+            if (sp + 1 > cap) {
+                cnt.overflow();
                 break;
             }
             const bool first0 = o0 <= o1;
@@ -1553,10 +1592,10 @@ __device__ __forceinline__ void pt_traverse_coop(const KTri* __restrict__ ktris,
                                                  const int32_t* __restrict__ tri_list, uint32_t* wstack,
                                                  unsigned long long* keys, int32_t* vlist, int lane, bool want,
                                                  const PtRay& ray, int avoid_in, float len_in, float eps_in,
-                                                 PtBest& out, Counters& cnt) {
+                                                 PtBest& out, Counters& cnt, int cap) {
     const uint64_t wm = __ballot(want);
     if (wm == 0) return;
-    keys[lane] = ~0ull;
+    key_reset(keys[lane]);
     int owner = lane;
     PtRay r = ray;
     int avoid = avoid_in;
@@ -1667,8 +1706,8 @@ __device__ __forceinline__ void pt_traverse_coop(const KTri* __restrict__ ktris,
         h0 = h0 && !pruned(w0);
         h1 = h1 && !pruned(w1);
         if (h0 && h1) {
-            if (sp + 1 > kStackDepth) {
-                cnt.overflow = 1;
+            if (sp + 1 > cap) {
+                cnt.overflow();
                 has = false;
                 sp = bot = 0;
                 continue;
@@ -1712,14 +1751,14 @@ __device__ __forceinline__ void pt_traverse_coop(const KTri* __restrict__ ktris,
 template <bool kQueue>
 __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
     const KTri* __restrict__ ktris, const CFNode* __restrict__ nodes,
-    const int32_t* __restrict__ tri_list, CamRec cam, RenderLaunch L, float* __restrict__ out,
+    const int32_t* __restrict__ tri_list, const CamRec* __restrict__ cam, RenderLaunch L, float* __restrict__ out,
     unsigned long long* __restrict__ counters) {
-    __shared__ uint32_t stacks[kWavesPerBlock][kStackDepth * 64];
+    extern __shared__ uint32_t dyn_stacks[];  // kWavesPerBlock x L.stack_depth x 64, sized at launch
     __shared__ unsigned long long pt_keys[kWavesPerBlock][64];  // per-ray minima (cooperative traversal)
     __shared__ int32_t pt_vlist[kWavesPerBlock][64];            // victims of a steal round
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    uint32_t* stack = &stacks[wave][lane];
+    uint32_t* stack = dyn_stacks + (size_t)wave * L.stack_depth * 64 + lane;
 
     const int SP = L.lanes_per_pixel;
     int c = lane & (SP - 1);
@@ -1728,7 +1767,7 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
     int px = L.col0 + blockIdx.x * (2 * tw) + (wave & 1) * tw + (pix % tw);
     int lrow = blockIdx.y * (2 * th) + (wave >> 1) * th + (pix / tw);
     auto global_row = [&](int lr) {
-        const int lb = lr / L.row_block;
+        const int lb = (int)udiv((uint32_t)lr, L.row_block_div);
         return (lb * L.row_world + L.row_rank) * L.row_block + (lr - lb * L.row_block);
     };
     int y = global_row(lrow);
@@ -1739,7 +1778,7 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
     int shard = (int)(blockIdx.x % kQueueShards), shards_tried = 0;  // wave-uniform
 
     v3 sum{0.0f, 0.0f, 0.0f};
-    Counters cnt{0, 0, 0, 0, 0, 0, 0};
+    Counters cnt{0, 0, 0, 0, 0, 0, counters + 4};
     int s = c;
     bool alive = valid && s < L.spp;
     bool need_cam = true;
@@ -1797,13 +1836,14 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
             r.pad_t = v3{eps * fabsf(r.inv.x), eps * fabsf(r.inv.y), eps * fabsf(r.inv.z)};
 #if RT_BVH_STEAL
             pt_traverse_coop(ktris, nodes, tri_list, stack - lane, pt_keys[wave], pt_vlist[wave], lane, alive, r,
-                             avoid, fsqrt(dot(d, d)), eps, best, cnt);
+                             avoid, fsqrt(dot(d, d)), eps, best, cnt, L.stack_depth);
 #else
-            if (alive) pt_traverse(ktris, nodes, tri_list, stack, r, avoid, fsqrt(dot(d, d)), eps, best, cnt);
+            if (alive)
+                pt_traverse(ktris, nodes, tri_list, stack, r, avoid, fsqrt(dot(d, d)), eps, best, cnt, L.stack_depth);
 #endif
         }
+        cnt.segs += (uint32_t)__popcll(__ballot(alive));
         if (!alive) continue;
-        ++cnt.segs;
         const int best_idx = best.idx;
         const v3 best_hit = best.hit;
         const uint32_t best_mat = best_idx >= 0 ? (uint32_t)ktris[best_idx].material : kDiffuse;
@@ -1963,19 +2003,22 @@ __global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
         const float fs = (float)L.spp;
         write_pixel(L, out, ((size_t)lrow * (size_t)L.cols + (size_t)(px - L.col0)) * 3, sum, fs);
     }
-    const uint64_t ws = wave_sum_u64(cnt.segs);
+    const uint64_t ws = cnt.segs;
     const uint64_t wt = wave_sum_u64(cnt.tri_tests);
     const uint64_t wn = wave_sum_u64(cnt.node_visits);
-    const uint64_t wo = wave_sum_u64(cnt.overflow);
     if (lane == 0) {
         atomicAdd(&counters[0], (unsigned long long)ws);
         atomicAdd(&counters[1], (unsigned long long)wt);
         if (wn) atomicAdd(&counters[3], (unsigned long long)wn);
-        if (wo) atomicAdd(&counters[4], (unsigned long long)wo);
     }
 }
 
-hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec& cam, const RenderLaunch& L,
+// Dynamic LDS of a traversal kernel: the per-lane stacks of its 4 waves.
+static size_t stack_bytes(const RenderLaunch& L) {
+    return (size_t)kWavesPerBlock * (size_t)(L.stack_depth > 0 ? L.stack_depth : 1) * 64 * sizeof(uint32_t);
+}
+
+hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const RenderLaunch& L,
                             float* out, unsigned long long* counters, hipStream_t stream, hipEvent_t main_done) {
     dim3 block(64 * kWavesPerBlock);
     if (L.queue) {
@@ -1983,7 +2026,7 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec& cam, const Rend
         const uint32_t waves = (L.n_items + 63u) / 64u;
         const uint32_t blocks = std::min<uint32_t>((waves + kWavesPerBlock - 1) / kWavesPerBlock,
                                                    (uint32_t)L.queue);
-        hipLaunchKernelGGL(pathtrace_kernel<true>, dim3(blocks), block, 0, stream, sc.ktris, sc.nodes,
+        hipLaunchKernelGGL(pathtrace_kernel<true>, dim3(blocks), block, stack_bytes(L), stream, sc.ktris, sc.nodes,
                            sc.tri_list, cam, L, out, counters);
         if (main_done) (void)hipEventRecord(main_done, stream);
         const uint32_t pixels = L.n_items / (uint32_t)L.lanes_per_pixel;
@@ -1993,7 +2036,7 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec& cam, const Rend
     dim3 grid((L.cols + 2 * L.tile_w - 1) / (2 * L.tile_w),
               (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
     if (grid.x == 0 || grid.y == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
-    hipLaunchKernelGGL(pathtrace_kernel<false>, grid, block, 0, stream, sc.ktris, sc.nodes,
+    hipLaunchKernelGGL(pathtrace_kernel<false>, grid, block, stack_bytes(L), stream, sc.ktris, sc.nodes,
                        sc.tri_list, cam, L, out, counters);
     if (main_done) (void)hipEventRecord(main_done, stream);
     return hipGetLastError();
@@ -2018,7 +2061,7 @@ uint32_t kernel_build_flags() {
     return f;
 }
 
-hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLaunch& L, float* out,
+hipError_t launch_render(const SceneArgs& sc, const CamRec* cam, const RenderLaunch& L, float* out,
                          unsigned long long* counters, hipStream_t stream, hipEvent_t main_done) {
     dim3 block(64 * kWavesPerBlock);
     if (L.queue) {
@@ -2028,7 +2071,7 @@ hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLau
                                                    (uint32_t)L.queue);
         dim3 grid(blocks, 1);
         if (sc.has_bvh)
-            hipLaunchKernelGGL((render_kernel<true, true>), grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
+            hipLaunchKernelGGL((render_kernel<true, true>), grid, block, stack_bytes(L), stream, sc.objs, sc.tris, sc.mats,
                                sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
         else
             hipLaunchKernelGGL((render_kernel<false, true>), grid, block, 0, stream, sc.objs, sc.tris,
@@ -2042,7 +2085,7 @@ hipError_t launch_render(const SceneArgs& sc, const CamRec& cam, const RenderLau
               (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
     if (grid.x == 0 || grid.y == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
     if (sc.has_bvh)
-        hipLaunchKernelGGL((render_kernel<true, false>), grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
+        hipLaunchKernelGGL((render_kernel<true, false>), grid, block, stack_bytes(L), stream, sc.objs, sc.tris, sc.mats,
                            sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
     else
         hipLaunchKernelGGL((render_kernel<false, false>), grid, block, 0, stream, sc.objs, sc.tris, sc.mats,

@@ -333,6 +333,10 @@ std::string HostScene::flatten() {
             }
             r.f[0] = lo.x; r.f[1] = lo.y; r.f[2] = lo.z;
             r.f[3] = hi.x; r.f[4] = hi.y; r.f[5] = hi.z;
+            // the compaction's pair -> ray division p / nt as a multiply-high:
+            // magic = ceil(2^32 / nt), exact for p < 2^26 (rt_kernel.hip mesh_compact)
+            const uint32_t magic = nt > 1 ? 0xFFFFFFFFu / (uint32_t)nt + 1u : 0u;
+            memcpy(&r.f[6], &magic, 4);
             std::vector<int32_t> order(nt);
             for (size_t t = 0; t < nt; ++t) order[t] = (int32_t)t;
             if (nt > kBvhMinTris) {

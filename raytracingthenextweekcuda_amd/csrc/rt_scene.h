@@ -42,7 +42,8 @@ struct alignas(16) ObjRec {
     // moving sphere: center0 xyz, center1 xyz, time0, time1, radius
     // plane: position xyz, normal xyz, rectangle bounds (lo_a, hi_a, lo_b, hi_b) on the
     //        orientation's axes a, b (XY: x, y; YZ: y, z; XZ: x, z)
-    // mesh: boundsMin xyz, boundsMax xyz (computeMeshAABB, main.cu:261-281)
+    // mesh: boundsMin xyz, boundsMax xyz (computeMeshAABB, main.cu:261-281), f[6] = the bits of
+    //       ceil(2^32 / triangle count) (the brute-force compaction's division)
     float f[10];
 };
 constexpr uint32_t kNoBvh = 0xFFFFFFFFu;
@@ -101,6 +102,7 @@ struct SceneArgs {
     int32_t n_objs;            // records scanned by hit(); sphere-group members follow them
     int32_t n_mats;
     bool has_bvh;  // any mesh carries a BVH (selects the kernel variant)
+    int32_t stack_cap = kBvhStackDepth;  // traversal stack entries per lane (the scene's BVH depth)
 };
 
 // ----------------------------------------------------------------------------
