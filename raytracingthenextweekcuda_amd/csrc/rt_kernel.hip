@@ -242,11 +242,25 @@ __device__ __forceinline__ uint64_t stamp() {
 #define RT_ACC(slot, a, b)
 #endif
 
+// A constant materialised at its use (the empty asm makes each call a fresh VGPR):
+// the register allocator otherwise keeps shared constant tuples - a zero vector,
+// a 64-bit all-ones - live across the whole persistent loop, and in the BVH kernel
+// spilled them to scratch instead of rematerialising them.
+__device__ __forceinline__ uint32_t fresh_u32(uint32_t v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ float fresh_f32(float v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
 // Sets an LDS 64-bit minimum slot to +inf (all ones).
 __device__ __forceinline__ void key_reset(unsigned long long& k) {
+    const uint32_t ones = fresh_u32(~0u);
     uint32_t* w = reinterpret_cast<uint32_t*>(&k);
-    w[0] = ~0u;
-    w[1] = ~0u;
+    w[0] = ones;
+    w[1] = ones;
 }
 
 // The lane's rank among the set bits of `mask` below it.
@@ -739,10 +753,13 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
     Hit h{kInf, -1, -1, 0xFFFFFFFFu, -1, 0u};
     const v3 o = ray.o, d = ray.d;
     const int n = S.n_objs;
+#ifndef RT_OBJ_PREFETCH
+#define RT_OBJ_PREFETCH 1
+#endif
     ObjRec cur = load_obj(S.objs, 0);
     for (int i = 0; i < n; ++i) {
-        const ObjRec ob = cur;
-        if (i + 1 < n) cur = load_obj(S.objs, i + 1);
+        const ObjRec ob = RT_OBJ_PREFETCH ? cur : load_obj(S.objs, i);
+        if (RT_OBJ_PREFETCH && i + 1 < n) cur = load_obj(S.objs, i + 1);
         const float* f = ob.f;
         if (ob.type == kObjPlane) {
             // Plane::hit (Plane.cu:4-52); t is only used when `proceed` holds.
@@ -1015,8 +1032,9 @@ __device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, i
 // therefore bit-identical; only the tail of the launch gets shorter.
 [[maybe_unused]] __device__ __forceinline__ void tail_steal(const RenderLaunch& L, WaveLds& W, int lane, int SP, bool& alive,
                                            bool& waiting, bool& held, int& towner, uint32_t& tl_pack,
-                                           int& own_end, int& c, int& s, int& px, int& y, uint32_t& pixel,
-                                           uint32_t item, v3& sum, v3& thr, bool& need_cam) {
+                                           int& own_end, int& s, uint32_t& item, v3& sum, v3& thr,
+                                           bool& need_cam) {
+    const int c = (int)(item & (uint32_t)(SP - 1));  // the item's sub-stream
     // 1. owners whose stolen samples are all held fold them in and write the partial
     if (__ballot(waiting || held) != 0) {
         bool ready = true;
@@ -1057,21 +1075,17 @@ __device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, i
     __builtin_amdgcn_wave_barrier();
     const bool thief = idle && ri < nv;
     const int vic = thief ? W.src[ri] : lane;
-    const int v_end = __shfl(own_end, vic, 64), v_c = __shfl(c, vic, 64), v_px = __shfl(px, vic, 64);
-    const int v_y = __shfl(y, vic, 64);
-    const uint32_t v_pixel = (uint32_t)__shfl((int)pixel, vic, 64);
+    const int v_end = __shfl(own_end, vic, 64);
+    const uint32_t v_item = (uint32_t)__shfl((int)item, vic, 64);
     if (spare && rv < ni) {  // robbed: its last unstarted sample goes to the thief of the same rank
         own_end -= SP;
         const int pos = (own_end - c) >> L.sp_log2;
         tl_pack |= ((uint32_t)W.key[rv] + 1u) << (8 * pos);
     }
-    if (thief) {
+    if (thief) {  // the thief's own item is finished: it carries the victim's (pixel, sub-stream)
         towner = vic;
-        c = v_c;
+        item = v_item;
         s = v_end - SP;
-        px = v_px;
-        y = v_y;
-        pixel = v_pixel;
         alive = true;
         need_cam = true;
     }
@@ -1141,15 +1155,17 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     for (;;) {
         if (kQueue) {
             // lanes without work take the next items once enough lanes are idle
+            // (queue mode keeps only `item` across the loop: the pixel and sub-stream are
+            // derived from it where needed, which keeps four VGPRs out of the traversal)
             queue_refill(L, lane, alive, exhausted, shard, shards_tried, [&](uint32_t it) {
-                if (!queue_item(L, it, c, px, lrow)) return;  // past the frame edge: ask again
+                int ic, ipx, ilr;
+                if (!queue_item(L, it, ic, ipx, ilr)) return;  // past the frame edge: ask again
                 item = it;
-                y = global_row(lrow);
-                pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
-                s = c;
-                sum = v3{0.0f, 0.0f, 0.0f};
+                s = ic;
+                const float z = fresh_f32(0.0f);
+                sum = v3{z, z, z};
                 alive = s < L.spp;
-                own_end = sub_end(L.spp, c, SP, L.sp_log2);
+                own_end = sub_end(L.spp, ic, SP, L.sp_log2);
                 // a sub-stream with no samples (S > spp) still owns its partial-sum slot
                 if (!alive) store_partial(L, item, sum);
                 need_cam = true;
@@ -1157,12 +1173,17 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
         }
 #if RT_TAIL_STEAL
         if (kQueue && exhausted)
-            tail_steal(L, W, lane, SP, alive, waiting, held, towner, tl_pack, own_end, c, s, px, y, pixel, item,
-                       sum, thr, need_cam);
+            tail_steal(L, W, lane, SP, alive, waiting, held, towner, tl_pack, own_end, s, item, sum, thr, need_cam);
 #endif
         if (__ballot(alive || waiting || held || (kQueue && !exhausted)) == 0) break;  // wave-uniform exit
         RT_STAMP(t_a);
         if (alive && need_cam) {
+            if (kQueue) {
+                int ic, ilr;
+                queue_item(L, item, ic, px, ilr);
+                y = global_row(ilr);
+                pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
+            }
             ray = camera_sample(cam, L, rng, pixel, px, y, s, fw, fh);
             thr = v3{1.0f, 1.0f, 1.0f};
             depth = 0;

@@ -107,8 +107,15 @@ RT_HD u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
 
 // curand's _curand_uniform: x * CURAND_2POW32_INV + CURAND_2POW32_INV/2 -> (0, 1].
 RT_HD float u01(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // RN(RN(x) 2^-32 + 2^-33) = RN(RN(x) + 0.5) 2^-32 (power-of-two scaling commutes with
+    // rounding; no subnormals): the same bits from an add with the inline constant 0.5 and
+    // an exact ldexp, with no 32-bit literal constants to keep in registers
+    return __builtin_ldexpf((float)x + 0.5f, -32);
+#else
     const float inv = 2.3283064e-10f;  // 2^-32
     return (float)x * inv + (inv / 2.0f);
+#endif
 }
 
 RT_HD uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
