@@ -44,9 +44,9 @@ SCENES = {
     "spheres": ("random_spheres", 1280, 720, 256, 10, "RTNW final scene (488 spheres, 388 moving; object BVH)"),
     "bunny": ("bunny_cornell_box", 1024, 1024, 512, 8, "bun_zipper.ply (69,451 triangles, SAH BVH) in CornellBox1 walls"),
     "media": ("cornell_box_media", 2048, 2048, 1024, 16, "CornellBox1 walls + 2 constant-medium boxes + glass sphere (media: build extension)"),
-    # the scene of the reference's only published timings (images.MD:44-53, 3,857 ms/frame on
-    # an unstated sm_61 GPU; scene inferred from the image); not a BASELINE config
-    "suzanne": ("suzanne_cornell_box", 512, 512, 32, 10, "cornellbox3.yaml (suzanne_small.obj, 968 triangles) + metal and glass spheres (images.MD published-timing scene)"),
+    # Suzanne box: the geometry of the image behind the reference's only published timing
+    # (images.MD:44-53); its radiance does not match that image; not a BASELINE config
+    "suzanne": ("suzanne_cornell_box", 512, 512, 32, 10, "cornellbox3.yaml (suzanne_small.obj, 968 triangles) + metal and glass spheres (geometry of the images.MD timing image; radiance differs)"),
     # the reference's committed renderKernel configuration (pathTrace, main.cu:187;
     # samplesPerPixel 32, 5 bounces); not a BASELINE config, reported separately
     "materialball": ("materialball", 512, 512, 32, 5, "materialball.ply (46,816 triangles, COAT) + 6 spheres, pathTrace integrator"),

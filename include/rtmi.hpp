@@ -220,6 +220,9 @@ public:
     // BVH builds of commit() / processTriangleData(): RT_BVH_HOST (Recurse on the host,
     // BVH.cpp:94-497) or RT_BVH_GPU (its byte-identical GPU restatement).
     void setBVHBuilder(int32_t builder) { check(rt_set_bvh_builder(ctx_, builder)); }
+    // UpdateBoundingVolumeHierarchy's `.bvh` cache (BVH.cpp:500-554): RT_BVH_CACHE_READ |
+    // RT_BVH_CACHE_WRITE is the reference's read-if-fresh / write-after-build behaviour.
+    void setBVHCache(int32_t mode) { check(rt_set_bvh_cache(ctx_, mode)); }
     double lastBVHBuildMs() const {
         double ms = 0.0;
         check(rt_bvh_build_stats(ctx_, &ms, nullptr));
@@ -277,6 +280,22 @@ private:
     std::vector<std::unique_ptr<Material>> mat_slots_, obj_slots_;
     std::vector<Material*> mat_ptrs_, obj_ptrs_;
 };
+
+// pathTracing over several GPUs from one process: contexts[k] renders the
+// row tiles of rank k (same scene on each, committed here), one ncclGather brings them to
+// contexts[0]'s device, where the rows are de-interleaved; the frame lands in `canvas`.
+inline void pathTracingMulti(const std::vector<Context*>& contexts, Canvas& canvas, int32_t spp,
+                             int32_t bounces, int32_t rowBlock = 2, uint32_t seed = 1984) {
+    if (contexts.empty()) throw Error(RT_ERR_INVALID, "no contexts");
+    std::vector<rt_ctx*> raw;
+    for (Context* c : contexts) {
+        c->commit();
+        raw.push_back(c->raw());
+    }
+    rt_render_params p{canvas.getWidth(), canvas.getHeight(), spp, bounces, seed, 0,
+                       rowBlock, 0, 1, 0, RT_INTEGRATOR_RAYCOLOR, 0};
+    contexts[0]->check(rt_render_multi(raw.data(), (int32_t)raw.size(), &p, canvas.data()));
+}
 
 namespace detail {
 inline int32_t mat_index(Material* m) {

@@ -932,7 +932,9 @@ constexpr int kQueueShards = RT_QUEUE_SHARDS;
 static_assert(kQueueShards * 32 <= kQueueHeadWords, "queue heads");
 constexpr int kQueueStride = 32;  // u32 words between heads
 // Idle lanes that trigger a refill (or all lanes idle): L.refill, chosen per launch
-// by the host (8 for long queues, 4 for short shards); -DRT_QUEUE_REFILL=k fixes it
+// by the host (rt_capi.cpp launch(): 4 for short shards (< 16 items per resident lane)
+// and for long items (>= 16 samples each), else 8; reported as rt_render_stats.refill);
+// -DRT_QUEUE_REFILL=k fixes it
 // for A/B builds.
 #ifdef RT_QUEUE_REFILL
 #define RT_REFILL_AT(L) (RT_QUEUE_REFILL)
@@ -2076,7 +2078,7 @@ uint32_t kernel_build_flags() {
     f |= 2u;  // RT_BUILD_STAMPS
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
-    !RT_TAIL_STEAL || RT_WAVES_PER_EU != 4
+    !RT_TAIL_STEAL || RT_WAVES_PER_EU != 4 || defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;

@@ -107,7 +107,7 @@ RT_HD u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
 
 // curand's _curand_uniform: x * CURAND_2POW32_INV + CURAND_2POW32_INV/2 -> (0, 1].
 RT_HD float u01(uint32_t x) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(RT_U01_MULADD)  // RT_U01_MULADD: A/B builds only
     // RN(RN(x) 2^-32 + 2^-33) = RN(RN(x) + 0.5) 2^-32 (power-of-two scaling commutes with
     // rounding; no subnormals): the same bits from an add with the inline constant 0.5 and
     // an exact ldexp, with no 32-bit literal constants to keep in registers

@@ -111,10 +111,12 @@ def cornell_box_media(r: Renderer, width: int, height: int, commit: bool = True)
 
 
 def suzanne_cornell_box(r: Renderer, width: int, height: int, commit: bool = True) -> Camera:
-    """The scene of the reference's only published timings (R/images/images.MD:44-53:
-    512x512, 32 spp, 10 bounces, 3,857 ms on an unstated sm_61 GPU), as inferred from its
-    image: cornellbox3.yaml (suzanne_small.obj, 968 triangles) + the metal and glass
-    spheres of cornellbox0.yaml (assets/scenes/suzanne_cornellbox.yaml)."""
+    """Suzanne box: the GEOMETRY of the image behind the reference's only published timings
+    (R/images/images.MD:44-53: 512x512, 32 spp, 10 bounces, 3,857 ms on an unstated sm_61
+    GPU): cornellbox3.yaml (suzanne_small.obj, 968 triangles) + the metal and glass spheres
+    of cornellbox0.yaml (assets/scenes/suzanne_cornellbox.yaml). Its radiance does not match
+    that image (12-16 levels brighter at 32 spp: the image predates the repository's
+    material/light model), so it is not the published scene."""
     return load_yaml_scene(r, os.path.join(SCENES_DIR, "suzanne_cornellbox.yaml"), width, height,
                            commit=commit)
 

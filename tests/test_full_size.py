@@ -1,5 +1,5 @@
 """Parity at BASELINE.json's full sizes (the committed pathTrace
-setup and the published-timing Suzanne scene), on the frames bench.py renders.
+setup and the Suzanne box), on the frames bench.py renders.
 
 The GPU renders each full frame with the automatic sub-stream layout, as the bench
 does. Two checks follow.
@@ -13,8 +13,11 @@ does. Two checks follow.
    bench.py --gpus 8 (row_block 2) reassembles to the full frame bit for bit. The
    per-rank segment counts sum to the full frame's count (a checksum of checksums).
    The bunny has 69,451 triangles and the restatement tests them linearly, which is
-   too slow for rows at 1024 x 512 spp, so it gets only the property checks and the
-   host/GPU BVH builder identity at full size.
+   too slow for whole rows at 1024 x 512 spp: it gets two 64-pixel column windows against
+   the oracle (test_full_frame_bunny_oracle_window), the property checks and the host/GPU
+   BVH builder identity at full size.
+3. The north-star tolerance against the reference's sequential per-pixel sum (S = 1) on
+   the first spot row of every config that folds S > 1 sub-streams.
 """
 import os
 
@@ -34,7 +37,7 @@ CONFIGS = {
     "C2_cornellbox1": ("cornell_box1", "cornellbox1.yaml", 512, 512, 128, 8, 32, (0, 21)),
     "C3_spheres": ("random_spheres", "random_spheres.json", 1280, 720, 256, 10, 720, (7, 181)),
     "C5_media": ("cornell_box_media", "cornellbox_media.yaml", 2048, 2048, 1024, 16, 2048, (300, 1555)),
-    # the scene of the reference's only published timing (images.MD:44-53): 512^2, 32 spp, 10 bounces
+    # Suzanne box (the geometry of the images.MD:44-53 timing image): 512^2, 32 spp, 10 bounces
     "suzanne_published": ("suzanne_cornell_box", "suzanne_cornellbox.yaml", 512, 512, 32, 10, 128, (3, 77)),
 }
 

@@ -5,6 +5,7 @@ HBM bytes per launch of the render kernel = FETCH_SIZE x 2 (gfx950 counts half
 of the streamed reads, MI355X_MICROARCH.md) + WRITE_SIZE, both in KB (1024 B),
 averaged over the kernel's launches in the PMC pass.
 Usage: python tools/pmc_summary.py <round> [scene ...]
+       RTMI_PMC_SRC=gpurun_out/<tag> python tools/pmc_summary.py <round> [scene ...]
 """
 import csv
 import glob
@@ -14,7 +15,7 @@ import shutil
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(REPO, "gpurun_out")
+OUT = os.path.join(REPO, os.environ.get("RTMI_PMC_SRC", "gpurun_out"))
 KERNELS = ("render_kernel", "pathtrace_kernel")
 
 
