@@ -127,8 +127,11 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
                             float* out, unsigned long long* counters, hipStream_t stream,
                             hipEvent_t main_done);
 
-// Workgroups of the persistent work-queue grid (n_cu x resident blocks per CU).
-int queue_blocks(int n_cu);
+// Workgroups of the persistent work-queue grid (n_cu x resident 4-wave blocks per CU),
+// and the occupancy each kernel is compiled for (waves per SIMD).
+int queue_blocks(int n_cu, int waves_per_simd);
+int render_queue_waves(bool bvh);
+int pathtrace_queue_waves();
 
 hipError_t launch_render(const SceneArgs& sc, const CamRec* cam, const RenderLaunch& L,
                          float* out, unsigned long long* counters, hipStream_t stream, hipEvent_t main_done);

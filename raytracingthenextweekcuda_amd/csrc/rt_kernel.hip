@@ -853,17 +853,29 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 
 }  // namespace
 
-#ifndef RT_WAVES_PER_EU
-#define RT_WAVES_PER_EU 4  // min waves per SIMD (caps VGPRs at 128; measured best)
+// Occupancy per kernel (min waves per SIMD; VGPR budget 512 / waves): the BVH rayColor
+// kernel at 4 (128 VGPRs, spill-free), the linear-scan rayColor and the pathTrace kernels
+// at RT_SCAN_WAVES (same-box A/B in DESIGN.md §4). -DRT_WAVES_PER_EU=k forces all to k.
+#ifndef RT_BVH_WAVES
+#define RT_BVH_WAVES 4
 #endif
-#if RT_WAVES_PER_EU > 0
-#define RT_OCC __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
-#else
-#define RT_OCC
+#ifndef RT_SCAN_WAVES
+#define RT_SCAN_WAVES 5
 #endif
+#ifndef RT_PT_WAVES
+#define RT_PT_WAVES 5
+#endif
+#ifdef RT_WAVES_PER_EU
+#undef RT_BVH_WAVES
+#undef RT_SCAN_WAVES
+#undef RT_PT_WAVES
+#define RT_BVH_WAVES RT_WAVES_PER_EU
+#define RT_SCAN_WAVES RT_WAVES_PER_EU
+#define RT_PT_WAVES RT_WAVES_PER_EU
+#endif
+template <bool kBvh>
+constexpr int render_waves() { return kBvh ? RT_BVH_WAVES : RT_SCAN_WAVES; }
 
-// kBvh: the scene has BVH meshes (needs the 32 KB/block LDS traversal stacks,
-// which would otherwise cap occupancy for scenes that never use them).
 // Canvas::gamma (Canvas.h:198-200) with clamp = fmaxf(a, fminf(f, b)).
 __device__ __forceinline__ uint8_t gamma_u8(float c) {
     const float v = fmaxf(0.0f, fminf(fsqrt(c), 0.999f));
@@ -1095,7 +1107,7 @@ __device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, i
 }
 
 template <bool kBvh, bool kQueue>
-__global__ __launch_bounds__(256) RT_OCC void render_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_waves<kBvh>()))) void render_kernel(
     const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
     const MatRec* __restrict__ mats, const BvhNode* __restrict__ nodes,
     const uint32_t* __restrict__ tri_orig, int n_objs, const CamRec* __restrict__ cam, RenderLaunch L,
@@ -1108,8 +1120,10 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     WaveLds& W = lds[wave];
-    W.grp_s[lane] = 0;
-    W.grp_m[lane] = 0;
+    if (kBvh) {  // sphere groups exist only in BVH scenes
+        W.grp_s[lane] = 0;
+        W.grp_m[lane] = 0;
+    }
     uint32_t* stack = kBvh ? dyn_stacks + (size_t)wave * L.stack_depth * 64 + lane : nullptr;
 
     // Lane layout: SP = lanes_per_pixel adjacent lanes share one pixel and split
@@ -1339,8 +1353,8 @@ __global__ __launch_bounds__(256) RT_OCC void render_kernel(
     const uint64_t wt = wave_sum_u64(cnt.tri_tests) + cnt.tri_wave;
     const uint64_t wb = cnt.box_tests;
     const uint64_t wn = wave_sum_u64(cnt.node_visits);
-    const uint64_t wgs = wave_sum_u64(W.grp_s[lane] + (cnt.grp & 0xFFFFu));
-    const uint64_t wgm = wave_sum_u64(W.grp_m[lane] + (cnt.grp >> 16));
+    const uint64_t wgs = kBvh ? wave_sum_u64(W.grp_s[lane] + (cnt.grp & 0xFFFFu)) : 0;
+    const uint64_t wgm = kBvh ? wave_sum_u64(W.grp_m[lane] + (cnt.grp >> 16)) : 0;
 #ifdef RT_STAMPS
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(&counters[8 + k], (unsigned long long)tm[k]);
@@ -1772,7 +1786,7 @@ __device__ __forceinline__ void pt_traverse_coop(const KTri* __restrict__ ktris,
 }  // namespace
 
 template <bool kQueue>
-__global__ __launch_bounds__(256) RT_OCC void pathtrace_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES))) void pathtrace_kernel(
     const KTri* __restrict__ ktris, const CFNode* __restrict__ nodes,
     const int32_t* __restrict__ tri_list, const CamRec* __restrict__ cam, RenderLaunch L, float* __restrict__ out,
     unsigned long long* __restrict__ counters) {
@@ -2065,7 +2079,10 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
     return hipGetLastError();
 }
 
-int queue_blocks(int n_cu) { return n_cu * 4; }  // 4 waves/SIMD x 4 SIMDs / 4-wave blocks
+// A persistent grid fills the resident waves: waves per SIMD x 4 SIMDs / 4-wave blocks per CU.
+int queue_blocks(int n_cu, int waves_per_simd) { return n_cu * waves_per_simd; }
+int render_queue_waves(bool bvh) { return bvh ? render_waves<true>() : render_waves<false>(); }
+int pathtrace_queue_waves() { return RT_PT_WAVES; }
 
 // rtmi.h RT_BUILD_*: which non-shipped options this translation unit (and, through
 // the shared EXTRA flags, the whole library) was compiled with.
@@ -2078,7 +2095,8 @@ uint32_t kernel_build_flags() {
     f |= 2u;  // RT_BUILD_STAMPS
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
-    !RT_TAIL_STEAL || RT_WAVES_PER_EU != 4 || defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH
+    !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 5 || RT_PT_WAVES != 5 || \
+    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;
