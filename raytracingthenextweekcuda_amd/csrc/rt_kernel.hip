@@ -854,13 +854,14 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }  // namespace
 
 // Occupancy per kernel (min waves per SIMD; VGPR budget 512 / waves): the BVH rayColor
-// kernel at 4 (128 VGPRs, spill-free), the linear-scan rayColor and the pathTrace kernels
-// at RT_SCAN_WAVES (same-box A/B in DESIGN.md §4). -DRT_WAVES_PER_EU=k forces all to k.
+// kernel at 4 (128 VGPRs, spill-free), the linear-scan rayColor kernel at 6 and the
+// pathTrace kernel at 5 (same-box A/B in DESIGN.md §4; profiles/r02/ab_occ.txt).
+// -DRT_WAVES_PER_EU=k forces all to k.
 #ifndef RT_BVH_WAVES
 #define RT_BVH_WAVES 4
 #endif
 #ifndef RT_SCAN_WAVES
-#define RT_SCAN_WAVES 5
+#define RT_SCAN_WAVES 6
 #endif
 #ifndef RT_PT_WAVES
 #define RT_PT_WAVES 5
@@ -1169,6 +1170,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
     uint64_t tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
     for (;;) {
+        RT_STAMP(t_q);
         if (kQueue) {
             // lanes without work take the next items once enough lanes are idle
             // (queue mode keeps only `item` across the loop: the pixel and sub-stream are
@@ -1193,6 +1195,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
 #endif
         if (__ballot(alive || waiting || held || (kQueue && !exhausted)) == 0) break;  // wave-uniform exit
         RT_STAMP(t_a);
+        RT_ACC(7, t_q, t_a);
         if (alive && need_cam) {
             if (kQueue) {
                 int ic, ilr;
@@ -2095,7 +2098,7 @@ uint32_t kernel_build_flags() {
     f |= 2u;  // RT_BUILD_STAMPS
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
-    !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 5 || RT_PT_WAVES != 5 || \
+    !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_PT_WAVES != 5 || \
     defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
