@@ -701,15 +701,14 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
             L.queue = rt::queue_blocks(c->n_cu, waves);
             L.n_items = (uint32_t)items;
             L.n_pix = (uint32_t)(items >> L.sp_log2);
-            // refill threshold (idle lanes a wave collects before one dequeue): 4 for
-            // short shards, whose tail it shortens, and for long items (>= 16 samples),
-            // where waiting for 8 idle lanes wastes lane time; 8 otherwise, where fewer
-            // dequeues win. Same-box A/B, ms (profiles/r01/ab_refill*.log), 4 vs 8:
-            // CB1 (4 samples per item) N = 1 8.63 / 8.58, N = 8 shard 1.213 / 1.230; spheres (8)
-            // 79.9 / 79.1; Suzanne (1) 5.52 / 5.44; bunny (16) 544.9 / 548.2; media (128) 1798 / 1846.
-            const uint64_t lanes = (uint64_t)L.queue * 256u;
+            // refill threshold (idle lanes a wave collects before one dequeue): 4 for long
+            // items (>= 16 samples each: waiting for 8 idle lanes wastes lane time), else 8
+            // (fewer dequeues). Same-box A/B, ms, 4 vs 8: bunny (16 samples/item) 544.9 / 548.2,
+            // media (128) 1798 / 1846 (profiles/r01/ab_refill*.log); N = 8 shards (4 samples/item,
+            // profiles/r02/refill_shards.log) CB1 1.205 / 1.207, spheres 10.86 / 10.81, Suzanne
+            // 0.876 / 0.860 - round 1's extra "short shard -> 4" rule is not supported there.
             const int per_item = (L.spp + L.lanes_per_pixel - 1) / L.lanes_per_pixel;
-            L.refill = (items < 16u * lanes || per_item >= 16) ? 4 : 8;
+            L.refill = per_item >= 16 ? 4 : 8;
             L.partial = c->d_partial;
             RT_HIP(c, hipMemsetAsync(c->d_queue, 0, rt::kQueueHeadWords * sizeof(uint32_t), st));
         }

@@ -945,8 +945,8 @@ constexpr int kQueueShards = RT_QUEUE_SHARDS;
 static_assert(kQueueShards * 32 <= kQueueHeadWords, "queue heads");
 constexpr int kQueueStride = 32;  // u32 words between heads
 // Idle lanes that trigger a refill (or all lanes idle): L.refill, chosen per launch
-// by the host (rt_capi.cpp launch(): 4 for short shards (< 16 items per resident lane)
-// and for long items (>= 16 samples each), else 8; reported as rt_render_stats.refill);
+// by the host (rt_capi.cpp launch(): 4 for long items (>= 16 samples each), else 8;
+// reported as rt_render_stats.refill);
 // -DRT_QUEUE_REFILL=k fixes it
 // for A/B builds.
 #ifdef RT_QUEUE_REFILL
