@@ -686,7 +686,17 @@ int orc_mesh(Scene* s, int idx, const float* verts, int n_tris, int mat) {
     return 0;
 }
 
-/* tinyobjloader tryParseDouble (tiny_obj_loader.h:837-965) */
+/* tinyobjloader tryParseDouble (tiny_obj_loader.h:837-965), restated.
+ * tinyobjloader: The MIT License (MIT), Copyright (c) 2012-Present, Syoyo Fujita
+ * and many contributors. Permission is hereby granted, free of charge, to any
+ * person obtaining a copy of this software and associated documentation files
+ * (the "Software"), to deal in the Software without restriction, including
+ * without limitation the rights to use, copy, modify, merge, publish, distribute,
+ * sublicense, and/or sell copies of the Software, and to permit persons to whom
+ * the Software is furnished to do so, subject to the following conditions: The
+ * above copyright notice and this permission notice shall be included in all
+ * copies or substantial portions of the Software. THE SOFTWARE IS PROVIDED
+ * "AS IS", WITHOUT WARRANTY OF ANY KIND, EXPRESS OR IMPLIED. */
 static int obj_parse_double(const char* s, const char* e, double* result) {
     if (s >= e) return 0;
     double mantissa = 0.0;

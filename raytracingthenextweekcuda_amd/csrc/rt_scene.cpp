@@ -73,6 +73,19 @@ TriRec make_triangle(v3 p0, v3 p1, v3 p2) {
 // :967-975), 1-based / negative index fix-up, and the quad split on the
 // shorter diagonal (:1397-1495). n-gons (> 4 vertices) use tinyobjloader's
 // ear clipping, which this loader does not restate: they are rejected.
+//
+// tinyobjloader is distributed under the MIT licence:
+//   The MIT License (MIT)
+//   Copyright (c) 2012-Present, Syoyo Fujita and many contributors.
+//   Permission is hereby granted, free of charge, to any person obtaining a copy
+//   of this software and associated documentation files (the "Software"), to deal
+//   in the Software without restriction, including without limitation the rights
+//   to use, copy, modify, merge, publish, distribute, sublicense, and/or sell
+//   copies of the Software, and to permit persons to whom the Software is
+//   furnished to do so, subject to the following conditions: The above copyright
+//   notice and this permission notice shall be included in all copies or
+//   substantial portions of the Software. THE SOFTWARE IS PROVIDED "AS IS",
+//   WITHOUT WARRANTY OF ANY KIND, EXPRESS OR IMPLIED.
 // ---------------------------------------------------------------------------
 namespace {
 
