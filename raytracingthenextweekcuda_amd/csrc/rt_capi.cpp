@@ -579,6 +579,9 @@ static rt_status rt_commit_impl(rt_ctx* c) {
     RT_HIP(c, up(&c->d_tri_orig, S.tri_orig));
     c->n_objs = S.n_scan;
     c->n_mats = (int)S.mats.size();
+    c->has_media = false;
+    for (int32_t i = 0; i < S.n_scan && i < (int32_t)S.objs.size(); ++i)
+        if (S.objs[(size_t)i].type == rt::kObjMedium) c->has_media = true;
     c->committed = true;
     return RT_OK;
 }
@@ -755,6 +758,7 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
     } else {
         rt::SceneArgs sc{c->d_objs,   c->d_tris,  c->d_mats,  c->d_nodes,
                          c->d_tri_orig, c->n_objs, c->n_mats, !c->scene.nodes.empty()};
+        sc.has_media = c->has_media;
         RT_HIP(c, rt::launch_render(sc, c->d_cam, L, out, c->d_counters, st, k1));
     }
     RT_HIP(c, hipEventRecord(c->ev1, st));

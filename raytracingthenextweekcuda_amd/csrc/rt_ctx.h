@@ -30,6 +30,7 @@ struct rt_ctx {
     rt::BvhNode* d_nodes = nullptr;
     uint32_t* d_tri_orig = nullptr;
     int n_objs = 0;
+    bool has_media = false;   // the committed scan list holds a participating medium (kernel variant)
     int n_mats = 0;
     unsigned long long* d_counters = nullptr;
     rt::CamRec* d_cam = nullptr;  // device copy of scene.camera read by the kernels

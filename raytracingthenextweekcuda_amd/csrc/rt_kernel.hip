@@ -200,9 +200,17 @@ struct Hit {
 #define RT_MESH_TWO_PHASE 1  // cull-filtered compaction (mesh_compact); 0 = one pass (A/B only)
 #endif
 
+#ifndef RT_MESH_RUN
+#define RT_MESH_RUN 1  // runs of equal brute-force meshes share one compaction (mesh_run); 0 = per mesh (A/B)
+#endif
+constexpr int kMaxRun = (int)kMeshRunMax;  // meshes per run (rt_scene.cpp marks the runs)
+
 struct WaveLds {
     unsigned long long key[64];  // per-ray (t bits << 32 | triangle) minima
     int32_t src[64];             // rank -> lane of the rays wanting a mesh
+#if RT_MESH_RUN
+    uint32_t slot[kMaxRun * 64];  // mesh_run: ray slot -> lane | triangle base << 6
+#endif
     uint32_t grp_s[64], grp_m[64];  // per-lane sphere-group test counts (Counters::grp drained per trip)
 #if RT_MESH_TWO_PHASE
     uint16_t ring[128];          // pair ids that passed the backface cull, awaiting the full test
@@ -607,6 +615,88 @@ __device__ __forceinline__ ObjRec load_obj(const ObjRec* __restrict__ objs, int 
     return r;
 }
 
+#if RT_MESH_RUN
+// A run of g consecutive brute-force meshes with the same triangle count m (instances
+// of one model; rt_scene.cpp stores g in the first record's f[7], 0 in the others)
+// compacted together: the rays wanting each mesh (box early-out, TriangleMesh.cu:34-38)
+// are listed one after the other as ray slots (lane, the mesh's triangle base), and the
+// slot x triangle pairs of the whole run are packed over the 64 lanes as in
+// mesh_compact. One partial batch per run instead of one per mesh. Triangles of
+// consecutive meshes are consecutive in `tris` (their bases rise with scan order), so
+// the per-lane minimum of (t, global triangle index) over the run is the candidate the
+// sequential hit() keeps: smallest t, then the earliest mesh, then its lowest triangle.
+__device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
+                                         int i0, uint32_t g, uint32_t m, uint32_t magic, bool live, v3 o, v3 d,
+                                         v3 inv, Hit& h, Counters& cnt, WaveLds& W, int lane) {
+    uint32_t nslot = 0;  // wave-uniform
+    bool any = false;
+    const uint32_t lives = (uint32_t)__popcll(__ballot(live));
+    for (uint32_t j = 0; j < g; ++j) {
+        const ObjRec ob = load_obj(objs, i0 + (int)j);
+        const bool want = live && box_hit(ob.f, o, inv);
+        const uint64_t mask = __ballot(want);
+        cnt.box_tests += lives;
+        cnt.tri_wave += (uint32_t)__popcll(mask) * m;
+        if (want) W.slot[nslot + (uint32_t)lane_rank(mask)] = (uint32_t)lane | (ob.u0 << 6);
+        nslot += (uint32_t)__popcll(mask);
+        any = any || want;
+    }
+    if (nslot == 0) return;
+    if (any) key_reset(W.key[lane]);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t total = nslot * m;
+    const float t0 = h.t;
+    uint32_t queued = 0, tested = 0;  // wave-uniform ring positions (two phases as in mesh_compact)
+    auto full_test = [&](uint32_t count) {
+        const uint32_t i = tested + (uint32_t)lane;
+        const bool act = (uint32_t)lane < count;
+        const uint32_t p = act ? (uint32_t)W.ring[i & 127u] : 0u;
+        const uint32_t r = m > 1u ? __umulhi(p, magic) : p;
+        const uint32_t e = W.slot[r];
+        const int src = (int)(e & 63u);
+        const uint32_t tri = (e >> 6) + (p - r * m);
+        const v3 ro{__shfl(o.x, src, 64), __shfl(o.y, src, 64), __shfl(o.z, src, 64)};
+        const v3 rd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
+        const float rt0 = __shfl(t0, src, 64);
+        if (act) {
+            const float t = tri_t_culled(tris[tri], ro, rd);
+            if (t <= rt0) atomicMin(&W.key[src], ((unsigned long long)__float_as_uint(t) << 32) | tri);
+        }
+        tested += count;
+    };
+    for (uint32_t p0 = 0; p0 < total; p0 += 64) {
+        const uint32_t p = p0 + (uint32_t)lane;
+        const bool act = p < total;
+        const uint32_t r = act ? (m > 1u ? __umulhi(p, magic) : p) : 0u;
+        const uint32_t e = W.slot[r];
+        const int src = (int)(e & 63u);
+        const v3 rd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
+        bool keep = false;
+        if (act) {
+            const TriRec& tr = tris[(e >> 6) + (p - r * m)];
+            keep = !(dot(rd, v3{tr.nx, tr.ny, tr.nz}) > kFltEpsilon);  // TriangleMesh.cu:72
+        }
+        const uint64_t km = __ballot(keep);
+        if (keep) W.ring[(queued + (uint32_t)lane_rank(km)) & 127u] = (uint16_t)p;
+        queued += (uint32_t)__popcll(km);
+        __builtin_amdgcn_wave_barrier();
+        if (queued - tested >= 64u) full_test(64u);
+    }
+    if (queued > tested) full_test(queued - tested);
+    __builtin_amdgcn_wave_barrier();
+    if (any) {
+        const unsigned long long key = W.key[lane];
+        if (key != ~0ull) {
+            const uint32_t tri = (uint32_t)(key & 0xFFFFFFFFu);
+            const uint32_t base0 = objs[i0].u0;  // wave-uniform
+            const uint32_t j = m > 1u ? __umulhi(tri - base0, magic) : tri - base0;  // the mesh in the run
+            h.merge(__uint_as_float((uint32_t)(key >> 32)), objs[i0].order + j, false, i0 + (int)j, (int32_t)tri);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+#endif
+
 // Candidate root of a (moving) sphere independent of closestSoFar: the near
 // root if >= tMin, else the far root (Sphere.cu:20-31 with tMax = +inf; the
 // sequential tMax test is applied by Hit::merge). NaN = no candidate.
@@ -742,7 +832,17 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
 // wave active; `live` masks lanes without a path. Records are fetched one
 // object ahead (scalar loads overlap the current object's VALU work), and the
 // per-object tests are branch-free candidates merged with Hit's tie rule.
-template <bool kBvh>
+#ifndef RT_MED_MERGE1
+#define RT_MED_MERGE1 1  // the media variant merges once per object (0: per branch, A/B)
+#endif
+#ifndef RT_MED_VARIANT
+#define RT_MED_VARIANT 1  // media scenes without BVHs take render_kernel<false, *, true> (0: A/B)
+#endif
+// kMed: the scan-kernel variant for scenes with participating media (rt_capi.cpp picks it):
+// no record prefetch (the medium test is long and the next record's 16 SGPRs stay live
+// across it) and one merge per object (the type branches yield a candidate instead of
+// each updating the Hit state). Both were measured slower on the other scenes.
+template <bool kBvh, bool kMed = false>
 __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v3 inv, bool live,
                                            Rng& rng, WaveLds& W, uint32_t* stack, int lane,
                                            Counters& cnt
@@ -756,11 +856,22 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
 #ifndef RT_OBJ_PREFETCH
 #define RT_OBJ_PREFETCH 1
 #endif
+    constexpr bool kPf = RT_OBJ_PREFETCH && !kMed;
     ObjRec cur = load_obj(S.objs, 0);
     for (int i = 0; i < n; ++i) {
-        const ObjRec ob = RT_OBJ_PREFETCH ? cur : load_obj(S.objs, i);
-        if (RT_OBJ_PREFETCH && i + 1 < n) cur = load_obj(S.objs, i + 1);
+        const ObjRec ob = kPf ? cur : load_obj(S.objs, i);
+        if (kPf && i + 1 < n) cur = load_obj(S.objs, i + 1);
         const float* f = ob.f;
+        float tc = __builtin_nanf("");  // kMed: this object's candidate, merged once below
+        bool tsph = false;
+        auto cand = [&](float t, bool sphere) {
+            if constexpr (kMed && RT_MED_MERGE1) {
+                tc = t;
+                tsph = sphere;
+            } else {
+                h.merge(t, ob.order, sphere, i, -1);
+            }
+        };
         if (ob.type == kObjPlane) {
             // Plane::hit (Plane.cu:4-52); t is only used when `proceed` holds.
             const v3 nrm{f[3], f[4], f[5]};
@@ -782,14 +893,27 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             }
             const bool in = (pa > f[6]) & (pa < f[7]) & (pb > f[8]) & (pb < f[9]);
             const bool ok = proceed & (t >= kTMin) & in;
-            h.merge(ok ? t : __builtin_nanf(""), ob.order, false, i, -1);
+            cand(ok ? t : __builtin_nanf(""), false);
         } else if (ob.type == kObjSphere || ob.type == kObjMovingSphere) {
-            h.merge(sphere_candidate(ob, o, d, ray.time), ob.order, true, i, -1);
+            cand(sphere_candidate(ob, o, d, ray.time), true);
         } else if (ob.type == kObjMesh) {
             // TriangleMesh::hit (TriangleMesh.cu:34-117): the AABB early-out
             // gates the triangle scan exactly as in the reference.
-            const bool want = live && box_hit(f, o, inv);
             const uint32_t root = ob.u2;  // wave-uniform (scalar record)
+#if RT_MESH_RUN
+            if (!kBvh || root == kNoBvh) {
+                const uint32_t g = __float_as_uint(ob.f[7]);  // run length (0: inside a run)
+                RT_STAMP(t_m0);
+                if (g != 0u)
+                    mesh_run(S.objs, S.tris, i, g, ob.u1, __float_as_uint(ob.f[6]), live, o, d, inv, h, cnt, W,
+                             lane);
+                RT_STAMP(t_m1);
+                RT_ACC(3, t_m0, t_m1);
+            } else {
+                const bool want = live && box_hit(f, o, inv);
+                cnt.box_tests += (uint32_t)__popcll(__ballot(live));
+#else
+            const bool want = live && box_hit(f, o, inv);
             cnt.box_tests += (uint32_t)__popcll(__ballot(live));
             if (root == kNoBvh) cnt.tri_wave += (uint32_t)__popcll(__ballot(want)) * ob.u1;
             if (!kBvh || root == kNoBvh) {
@@ -798,6 +922,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 RT_STAMP(t_m1);
                 RT_ACC(3, t_m0, t_m1);
             } else {
+#endif
 #if RT_BVH_STEAL
                 mesh_bvh_coop(S.tris, S.tri_orig, S.nodes, root, ob.u0, want, o, d, inv, h, i, ob.order,
                               stack - lane, W, lane, cnt, S.stack_cap);
@@ -807,10 +932,11 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
 #endif
             }
         } else if (ob.type == kObjMedium) {
-            h.merge(live ? medium_candidate(ob, o, d, rng) : __builtin_nanf(""), ob.order, false, i, -1);
+            cand(live ? medium_candidate(ob, o, d, rng) : __builtin_nanf(""), false);
         } else if (kBvh) {  // kObjSphereGroup
             sphere_group(S.objs, S.nodes, ob.u2, live, ray, inv, h, stack, cnt, S.stack_cap);
         }
+        if constexpr (kMed && RT_MED_MERGE1) h.merge(tc, ob.order, tsph, i, -1);  // NaN: no candidate
     }
     h.finish();
     return h;
@@ -1107,7 +1233,7 @@ __device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, i
     __builtin_amdgcn_wave_barrier();
 }
 
-template <bool kBvh, bool kQueue>
+template <bool kBvh, bool kQueue, bool kMed = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_waves<kBvh>()))) void render_kernel(
     const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
     const MatRec* __restrict__ mats, const BvhNode* __restrict__ nodes,
@@ -1221,7 +1347,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
 #endif
 
         const v3 inv = rcp(ray.d);
-        const Hit h = closest_hit<kBvh>(S, ray, inv, live, rng, W, stack, lane, cnt
+        const Hit h = closest_hit<kBvh, kMed>(S, ray, inv, live, rng, W, stack, lane, cnt
 #ifdef RT_STAMPS
                                         , tm
 #endif
@@ -2099,7 +2225,7 @@ uint32_t kernel_build_flags() {
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
     !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_PT_WAVES != 5 || \
-    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH
+    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;
@@ -2117,6 +2243,9 @@ hipError_t launch_render(const SceneArgs& sc, const CamRec* cam, const RenderLau
         if (sc.has_bvh)
             hipLaunchKernelGGL((render_kernel<true, true>), grid, block, stack_bytes(L), stream, sc.objs, sc.tris, sc.mats,
                                sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
+        else if (sc.has_media && RT_MED_VARIANT)
+            hipLaunchKernelGGL((render_kernel<false, true, true>), grid, block, 0, stream, sc.objs, sc.tris,
+                               sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
         else
             hipLaunchKernelGGL((render_kernel<false, true>), grid, block, 0, stream, sc.objs, sc.tris,
                                sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
@@ -2130,6 +2259,9 @@ hipError_t launch_render(const SceneArgs& sc, const CamRec* cam, const RenderLau
     if (grid.x == 0 || grid.y == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
     if (sc.has_bvh)
         hipLaunchKernelGGL((render_kernel<true, false>), grid, block, stack_bytes(L), stream, sc.objs, sc.tris, sc.mats,
+                           sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
+    else if (sc.has_media && RT_MED_VARIANT)
+        hipLaunchKernelGGL((render_kernel<false, false, true>), grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
                            sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
     else
         hipLaunchKernelGGL((render_kernel<false, false>), grid, block, 0, stream, sc.objs, sc.tris, sc.mats,

@@ -417,7 +417,35 @@ std::string HostScene::flatten() {
         r.f[9] = pb + eb;
     }
     n_scan = (int)objs.size();
-    return group_spheres();
+    const std::string err = group_spheres();
+    if (!err.empty()) return err;
+    mark_mesh_runs();
+    return "";
+}
+
+// Runs for the kernel's mesh_run: consecutive brute-force meshes of the final scan list
+// with the same triangle count, consecutive triangle ranges and consecutive scan orders
+// (up to kMeshRunMax). The first record of a run carries its length in f[7] (as u32
+// bits), the others 0; a brute-force mesh outside any run is a run of 1.
+void HostScene::mark_mesh_runs() {
+    auto brute = [&](size_t k) { return objs[k].type == kObjMesh && objs[k].u2 == kNoBvh; };
+    const size_t n = (size_t)n_scan;
+    for (size_t k = 0; k < n;) {
+        if (!brute(k)) {
+            ++k;
+            continue;
+        }
+        const ObjRec& a = objs[k];
+        size_t e = k + 1;
+        while (e < n && e - k < kMeshRunMax && brute(e) && objs[e].u1 == a.u1 &&
+               objs[e].u0 == a.u0 + (uint32_t)(e - k) * a.u1 && objs[e].order == a.order + (uint32_t)(e - k))
+            ++e;
+        for (size_t j = k; j < e; ++j) {
+            const uint32_t g = j == k ? (uint32_t)(e - k) : 0u;
+            memcpy(&objs[j].f[7], &g, 4);
+        }
+        k = e;
+    }
 }
 
 // Moves the (moving) spheres of a large scene behind one kObjSphereGroup record

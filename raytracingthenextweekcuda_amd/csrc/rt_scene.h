@@ -49,6 +49,7 @@ struct alignas(16) ObjRec {
 constexpr uint32_t kNoBvh = 0xFFFFFFFFu;
 // Meshes with more triangles than this are traversed through a BVH.
 constexpr uint32_t kBvhMinTris = 64;
+constexpr uint32_t kMeshRunMax = 4;  // brute-force meshes compacted together (rt_kernel.hip mesh_run)
 // Scenes with at least this many (moving) spheres get an object-level BVH.
 constexpr uint32_t kSphereBvhMin = 16;
 // Per-lane LDS traversal stack depth; the builder rejects deeper trees, like
@@ -103,6 +104,7 @@ struct SceneArgs {
     int32_t n_mats;
     bool has_bvh;  // any mesh carries a BVH (selects the kernel variant)
     int32_t stack_cap = kBvhStackDepth;  // traversal stack entries per lane (the scene's BVH depth)
+    bool has_media = false;  // any participating medium in the scan list (selects the kernel variant)
 };
 
 // ----------------------------------------------------------------------------
@@ -155,6 +157,7 @@ struct HostScene {
     // Returns "" on success or an error message.
     std::string flatten();
     std::string group_spheres();
+    void mark_mesh_runs();
     // A mesh BVH: read from `<cache_ply>.bvh` when the cache mode allows and the file is
     // fresh and valid, else built (and written when the mode says so).
     void build_bvh(const std::vector<v3>& vs, const std::vector<uint32_t>& ix, CFBvh& b,

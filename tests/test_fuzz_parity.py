@@ -133,3 +133,68 @@ def test_gpu_random_scene_parity(seed):
     assert float(np.abs(got - want).max()) <= 1e-4
     assert np.array_equal(got, want)
     assert st["segments"] == ost["segments"]
+
+
+def mesh_run_spec(seed):
+    """Runs of equal brute-force meshes for the kernel's mesh_run (rt_scene.cpp
+    mark_mesh_runs): five 12-triangle meshes in a row (a run of 4, then 1), a 3-triangle
+    mesh, a plane, a pair, a BVH mesh and a single one. Meshes 1 and 2 are the SAME
+    triangles with different materials: at equal t the earlier mesh must win
+    (the sequential hit()'s strict <), which the shading makes visible."""
+    rng = np.random.RandomState(seed)
+    mats = [("lambertian", 0, (0.8, 0.3, 0.3)), ("metal", 1, (0.9, 0.9, 0.5), 0.3),
+            ("lambertian", 2, (0.2, 0.7, 0.3)), ("emission", 3, (1.0, 0.9, 0.8), 4.0),
+            ("dielectric", 4, 1.5)]
+
+    def soup(nt, centre):
+        base = np.float32(centre)
+        return (base + rng.uniform(-0.35, 0.35, size=(nt, 3, 3)).astype(np.float32)).reshape(nt, 9)
+
+    objs, slot = [], 0
+
+    def add(o):
+        nonlocal slot
+        objs.append(o)
+        slot += 1
+
+    twin = soup(12, (0.0, 0.0, 0.0))
+    add(("mesh", slot, soup(12, (-0.5, 0.2, 0.1)), 0))
+    add(("mesh", slot, twin, 1))
+    add(("mesh", slot, twin.copy(), 2))
+    add(("mesh", slot, soup(12, (0.4, -0.3, 0.0)), 0))
+    add(("mesh", slot, soup(12, (0.1, 0.5, -0.2)), 4))
+    add(("mesh", slot, soup(3, (-0.3, -0.4, 0.3)), 2))
+    add(("plane", slot, (0.0, -0.8, 0.0), (0.0, 1.0, 0.0), (2.0, 2.0, 2.0), 0, 2, True))
+    add(("mesh", slot, soup(12, (0.6, 0.4, 0.2)), 1))
+    add(("mesh", slot, soup(12, (-0.6, -0.2, -0.3)), 2))
+    add(("mesh", slot, soup(80, (0.2, 0.0, -0.6)), 0))
+    add(("mesh", slot, soup(12, (0.0, -0.5, 0.5)), 3))
+    add(("sphere", slot, (0.0, 1.5, 0.0), 0.6, 3))
+    cam = ((0.2, 0.3, 2.6), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 1.33, 50.0, 0.0, 2.5, 0.0, 1.0)
+    return {"camera": cam, "materials": mats, "objects": objs}
+
+
+def test_mesh_run_specs_build_on_host():
+    import raytracingthenextweekcuda_amd as rtmi
+
+    for seed in range(3):
+        r = rtmi.Renderer(-1)
+        build_product(r, mesh_run_spec(seed))
+        r.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,lanes", [(0, 1), (1, 4), (2, 32)])
+def test_gpu_mesh_runs_parity(seed, lanes):
+    import raytracingthenextweekcuda_amd as rtmi
+
+    spec = mesh_run_spec(seed)
+    w, h, spp, depth = 48, 36, 8, 6
+    r = rtmi.Renderer(0)
+    build_product(r, spec)
+    got = r.render(w, h, spp, depth, lanes_per_pixel=lanes)
+    st = r.stats()
+    r.close()
+    want, ost = build_oracle(spec).render(w, h, spp, depth, lanes_per_pixel=lanes)
+    assert np.array_equal(got, want)
+    assert st["segments"] == ost["segments"]
