@@ -1233,11 +1233,30 @@ __device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, i
     __builtin_amdgcn_wave_barrier();
 }
 
+#ifndef RT_LK
+#define RT_LK 1  // the render loop reads its launch parameters from the kernarg segment at their use
+#endif
+// The render kernel's launch parameters (its FIRST argument: kernarg offset 0) behind an
+// opaque pointer. Each loop trip re-reads the fields it uses with scalar loads at their
+// use, instead of the compiler holding ~40 of them in SGPRs across the persistent loop
+// (SGPRs are the scarce resource: their spills take VGPR lanes, whose spills go to scratch).
+__device__ __forceinline__ const RenderLaunch& launch_args() {
+    const __attribute__((address_space(4))) char* p =
+        (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *reinterpret_cast<const RenderLaunch*>((const char*)p);
+}
+
+__device__ __forceinline__ int global_row_of(const RenderLaunch& L, int lr) {
+    const int lb = (int)udiv((uint32_t)lr, L.row_block_div);
+    return (lb * L.row_world + L.row_rank) * L.row_block + (lr - lb * L.row_block);
+}
+
 template <bool kBvh, bool kQueue, bool kMed = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_waves<kBvh>()))) void render_kernel(
-    const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
+    RenderLaunch L, const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
     const MatRec* __restrict__ mats, const BvhNode* __restrict__ nodes,
-    const uint32_t* __restrict__ tri_orig, int n_objs, const CamRec* __restrict__ cam, RenderLaunch L,
+    const uint32_t* __restrict__ tri_orig, int n_objs, const CamRec* __restrict__ cam,
     float* __restrict__ out, unsigned long long* __restrict__ counters) {
     const SceneArgs S{objs, tris, mats, nodes, tri_orig, n_objs, 0, kBvh, L.stack_depth};
     __shared__ WaveLds lds[kWavesPerBlock];
@@ -1263,11 +1282,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
     int px = L.col0 + blockIdx.x * (2 * tw) + (wave & 1) * tw + (pix % tw);
     int lrow = blockIdx.y * (2 * th) + (wave >> 1) * th + (pix / tw);
     // Row tiling: local row -> global row (y = 0 is the bottom row).
-    auto global_row = [&](int lr) {
-        const int lb = (int)udiv((uint32_t)lr, L.row_block_div);
-        return (lb * L.row_world + L.row_rank) * L.row_block + (lr - lb * L.row_block);
-    };
-    int y = global_row(lrow);
+    int y = global_row_of(L, lrow);
     bool valid = !kQueue && (px - L.col0 < L.cols) && (lrow < L.local_rows) && (y < L.height);
     uint32_t pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
     uint32_t item = 0;
@@ -1290,12 +1305,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
     Ray ray{{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 1.0f}, 0.0f};
     v3 thr{1.0f, 1.0f, 1.0f};
     Rng rng{1u, 0u, 0u, 0u};
-    const float fw = (float)(L.width - 1), fh = (float)(L.height - 1);
 
 #ifdef RT_STAMPS
     uint64_t tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
     for (;;) {
+#if RT_LK
+        const RenderLaunch& L = launch_args();  // this trip's view of the launch parameters
+        const int SP = L.lanes_per_pixel;
+#endif
         RT_STAMP(t_q);
         if (kQueue) {
             // lanes without work take the next items once enough lanes are idle
@@ -1326,10 +1344,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             if (kQueue) {
                 int ic, ilr;
                 queue_item(L, item, ic, px, ilr);
-                y = global_row(ilr);
+                y = global_row_of(L, ilr);
                 pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
             }
-            ray = camera_sample(cam, L, rng, pixel, px, y, s, fw, fh);
+            ray = camera_sample(cam, L, rng, pixel, px, y, s, (float)(L.width - 1), (float)(L.height - 1));
             thr = v3{1.0f, 1.0f, 1.0f};
             depth = 0;
             need_cam = false;
@@ -2241,14 +2259,14 @@ hipError_t launch_render(const SceneArgs& sc, const CamRec* cam, const RenderLau
                                                    (uint32_t)L.queue);
         dim3 grid(blocks, 1);
         if (sc.has_bvh)
-            hipLaunchKernelGGL((render_kernel<true, true>), grid, block, stack_bytes(L), stream, sc.objs, sc.tris, sc.mats,
-                               sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
+            hipLaunchKernelGGL((render_kernel<true, true>), grid, block, stack_bytes(L), stream, L, sc.objs, sc.tris,
+                               sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
         else if (sc.has_media && RT_MED_VARIANT)
-            hipLaunchKernelGGL((render_kernel<false, true, true>), grid, block, 0, stream, sc.objs, sc.tris,
-                               sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
+            hipLaunchKernelGGL((render_kernel<false, true, true>), grid, block, 0, stream, L, sc.objs, sc.tris,
+                               sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
         else
-            hipLaunchKernelGGL((render_kernel<false, true>), grid, block, 0, stream, sc.objs, sc.tris,
-                               sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
+            hipLaunchKernelGGL((render_kernel<false, true>), grid, block, 0, stream, L, sc.objs, sc.tris,
+                               sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
         if (main_done) (void)hipEventRecord(main_done, stream);
         const uint32_t pixels = L.n_items / (uint32_t)L.lanes_per_pixel;
         hipLaunchKernelGGL(combine_kernel, dim3((pixels + 255u) / 256u), dim3(256), 0, stream, L, out);
@@ -2258,14 +2276,14 @@ hipError_t launch_render(const SceneArgs& sc, const CamRec* cam, const RenderLau
               (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
     if (grid.x == 0 || grid.y == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
     if (sc.has_bvh)
-        hipLaunchKernelGGL((render_kernel<true, false>), grid, block, stack_bytes(L), stream, sc.objs, sc.tris, sc.mats,
-                           sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
+        hipLaunchKernelGGL((render_kernel<true, false>), grid, block, stack_bytes(L), stream, L, sc.objs, sc.tris, sc.mats,
+                           sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
     else if (sc.has_media && RT_MED_VARIANT)
-        hipLaunchKernelGGL((render_kernel<false, false, true>), grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
-                           sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
+        hipLaunchKernelGGL((render_kernel<false, false, true>), grid, block, 0, stream, L, sc.objs, sc.tris, sc.mats,
+                           sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
     else
-        hipLaunchKernelGGL((render_kernel<false, false>), grid, block, 0, stream, sc.objs, sc.tris, sc.mats,
-                           sc.nodes, sc.tri_orig, sc.n_objs, cam, L, out, counters);
+        hipLaunchKernelGGL((render_kernel<false, false>), grid, block, 0, stream, L, sc.objs, sc.tris, sc.mats,
+                           sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
     if (main_done) (void)hipEventRecord(main_done, stream);
     return hipGetLastError();
 }
