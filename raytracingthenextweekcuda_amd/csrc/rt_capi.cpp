@@ -700,7 +700,7 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
         if (have) {
             const int waves = p->integrator == RT_INTEGRATOR_PATHTRACE
                                   ? rt::pathtrace_queue_waves()
-                                  : rt::render_queue_waves(!c->scene.nodes.empty());
+                                  : rt::render_queue_waves(!c->scene.nodes.empty(), c->has_media);
             L.queue = rt::queue_blocks(c->n_cu, waves);
             L.n_items = (uint32_t)items;
             L.n_pix = (uint32_t)(items >> L.sp_log2);

@@ -980,14 +980,18 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }  // namespace
 
 // Occupancy per kernel (min waves per SIMD; VGPR budget 512 / waves): the BVH rayColor
-// kernel at 4 (128 VGPRs, spill-free), the linear-scan rayColor kernel at 6 and the
-// pathTrace kernel at 5 (same-box A/B in DESIGN.md §4; profiles/r02/ab_occ.txt).
+// kernel at 4 (128 VGPRs, spill-free), the linear-scan rayColor kernel at 5 (96 VGPRs,
+// spill-free since the launch parameters are read at their use), its media variant at 6
+// and the pathTrace kernel at 5 (same-box A/B in DESIGN.md §4; profiles/r02/ab_occ*.txt).
 // -DRT_WAVES_PER_EU=k forces all to k.
 #ifndef RT_BVH_WAVES
 #define RT_BVH_WAVES 4
 #endif
 #ifndef RT_SCAN_WAVES
-#define RT_SCAN_WAVES 6
+#define RT_SCAN_WAVES 5
+#endif
+#ifndef RT_MED_WAVES
+#define RT_MED_WAVES 6
 #endif
 #ifndef RT_PT_WAVES
 #define RT_PT_WAVES 5
@@ -995,13 +999,15 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #ifdef RT_WAVES_PER_EU
 #undef RT_BVH_WAVES
 #undef RT_SCAN_WAVES
+#undef RT_MED_WAVES
 #undef RT_PT_WAVES
 #define RT_BVH_WAVES RT_WAVES_PER_EU
 #define RT_SCAN_WAVES RT_WAVES_PER_EU
+#define RT_MED_WAVES RT_WAVES_PER_EU
 #define RT_PT_WAVES RT_WAVES_PER_EU
 #endif
-template <bool kBvh>
-constexpr int render_waves() { return kBvh ? RT_BVH_WAVES : RT_SCAN_WAVES; }
+template <bool kBvh, bool kMed = false>
+constexpr int render_waves() { return kBvh ? RT_BVH_WAVES : (kMed ? RT_MED_WAVES : RT_SCAN_WAVES); }
 
 // Canvas::gamma (Canvas.h:198-200) with clamp = fmaxf(a, fminf(f, b)).
 __device__ __forceinline__ uint8_t gamma_u8(float c) {
@@ -1234,9 +1240,9 @@ __device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, i
 }
 
 #ifndef RT_LK
-#define RT_LK 1  // the render loop reads its launch parameters from the kernarg segment at their use
+#define RT_LK 1  // the render loops read their launch parameters from the kernarg segment at their use
 #endif
-// The render kernel's launch parameters (its FIRST argument: kernarg offset 0) behind an
+// The megakernels' launch parameters (their FIRST argument: kernarg offset 0) behind an
 // opaque pointer. Each loop trip re-reads the fields it uses with scalar loads at their
 // use, instead of the compiler holding ~40 of them in SGPRs across the persistent loop
 // (SGPRs are the scarce resource: their spills take VGPR lanes, whose spills go to scratch).
@@ -1253,7 +1259,7 @@ __device__ __forceinline__ int global_row_of(const RenderLaunch& L, int lr) {
 }
 
 template <bool kBvh, bool kQueue, bool kMed = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_waves<kBvh>()))) void render_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_waves<kBvh, kMed>()))) void render_kernel(
     RenderLaunch L, const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
     const MatRec* __restrict__ mats, const BvhNode* __restrict__ nodes,
     const uint32_t* __restrict__ tri_orig, int n_objs, const CamRec* __restrict__ cam,
@@ -1934,8 +1940,8 @@ __device__ __forceinline__ void pt_traverse_coop(const KTri* __restrict__ ktris,
 
 template <bool kQueue>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES))) void pathtrace_kernel(
-    const KTri* __restrict__ ktris, const CFNode* __restrict__ nodes,
-    const int32_t* __restrict__ tri_list, const CamRec* __restrict__ cam, RenderLaunch L, float* __restrict__ out,
+    RenderLaunch L, const KTri* __restrict__ ktris, const CFNode* __restrict__ nodes,
+    const int32_t* __restrict__ tri_list, const CamRec* __restrict__ cam, float* __restrict__ out,
     unsigned long long* __restrict__ counters) {
     extern __shared__ uint32_t dyn_stacks[];  // kWavesPerBlock x L.stack_depth x 64, sized at launch
     __shared__ unsigned long long pt_keys[kWavesPerBlock][64];  // per-ray minima (cooperative traversal)
@@ -1950,11 +1956,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
     const int tw = L.tile_w, th = L.tile_h;
     int px = L.col0 + blockIdx.x * (2 * tw) + (wave & 1) * tw + (pix % tw);
     int lrow = blockIdx.y * (2 * th) + (wave >> 1) * th + (pix / tw);
-    auto global_row = [&](int lr) {
-        const int lb = (int)udiv((uint32_t)lr, L.row_block_div);
-        return (lb * L.row_world + L.row_rank) * L.row_block + (lr - lb * L.row_block);
-    };
-    int y = global_row(lrow);
+    int y = global_row_of(L, lrow);
     const bool valid = !kQueue && (px - L.col0 < L.cols) && (lrow < L.local_rows) && (y < L.height);
     uint32_t pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
     uint32_t item = 0;
@@ -1971,15 +1973,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
     v3 o{0.0f, 0.0f, 0.0f}, d{0.0f, 0.0f, 1.0f};
     v3 mask{1.0f, 1.0f, 1.0f}, accu{0.0f, 0.0f, 0.0f};
     Rng rng{1u, 0u, 0u, 0u};
-    const float fw = (float)(L.width - 1), fh = (float)(L.height - 1);
-    const bool has_mesh = L.pt_has_mesh != 0;
 
     for (;;) {
+#if RT_LK
+        const RenderLaunch& L = launch_args();  // this trip's view of the launch parameters
+        const int SP = L.lanes_per_pixel;
+#endif
+        const bool has_mesh = L.pt_has_mesh != 0;
         if (kQueue) {
             queue_refill(L, lane, alive, exhausted, shard, shards_tried, [&](uint32_t it) {
                 if (!queue_item(L, it, c, px, lrow)) return;  // past the frame edge: ask again
                 item = it;
-                y = global_row(lrow);
+                y = global_row_of(L, lrow);
                 pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
                 s = c;
                 sum = v3{0.0f, 0.0f, 0.0f};
@@ -1991,7 +1996,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
         }
         if (__ballot(alive || (kQueue && !exhausted)) == 0) break;
         if (alive && need_cam) {
-            const Ray r = camera_sample(cam, L, rng, pixel, px, y, s, fw, fh);
+            const Ray r = camera_sample(cam, L, rng, pixel, px, y, s, (float)(L.width - 1), (float)(L.height - 1));
             o = r.o;
             d = r.d;
             mask = v3{1.0f, 1.0f, 1.0f};
@@ -2210,8 +2215,8 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
         const uint32_t waves = (L.n_items + 63u) / 64u;
         const uint32_t blocks = std::min<uint32_t>((waves + kWavesPerBlock - 1) / kWavesPerBlock,
                                                    (uint32_t)L.queue);
-        hipLaunchKernelGGL(pathtrace_kernel<true>, dim3(blocks), block, stack_bytes(L), stream, sc.ktris, sc.nodes,
-                           sc.tri_list, cam, L, out, counters);
+        hipLaunchKernelGGL(pathtrace_kernel<true>, dim3(blocks), block, stack_bytes(L), stream, L, sc.ktris, sc.nodes,
+                           sc.tri_list, cam, out, counters);
         if (main_done) (void)hipEventRecord(main_done, stream);
         const uint32_t pixels = L.n_items / (uint32_t)L.lanes_per_pixel;
         hipLaunchKernelGGL(combine_kernel, dim3((pixels + 255u) / 256u), dim3(256), 0, stream, L, out);
@@ -2220,15 +2225,17 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
     dim3 grid((L.cols + 2 * L.tile_w - 1) / (2 * L.tile_w),
               (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
     if (grid.x == 0 || grid.y == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
-    hipLaunchKernelGGL(pathtrace_kernel<false>, grid, block, stack_bytes(L), stream, sc.ktris, sc.nodes,
-                       sc.tri_list, cam, L, out, counters);
+    hipLaunchKernelGGL(pathtrace_kernel<false>, grid, block, stack_bytes(L), stream, L, sc.ktris, sc.nodes,
+                       sc.tri_list, cam, out, counters);
     if (main_done) (void)hipEventRecord(main_done, stream);
     return hipGetLastError();
 }
 
 // A persistent grid fills the resident waves: waves per SIMD x 4 SIMDs / 4-wave blocks per CU.
 int queue_blocks(int n_cu, int waves_per_simd) { return n_cu * waves_per_simd; }
-int render_queue_waves(bool bvh) { return bvh ? render_waves<true>() : render_waves<false>(); }
+int render_queue_waves(bool bvh, bool media) {
+    return bvh ? render_waves<true>() : (media && RT_MED_VARIANT ? render_waves<false, true>() : render_waves<false>());
+}
 int pathtrace_queue_waves() { return RT_PT_WAVES; }
 
 // rtmi.h RT_BUILD_*: which non-shipped options this translation unit (and, through
@@ -2242,7 +2249,7 @@ uint32_t kernel_build_flags() {
     f |= 2u;  // RT_BUILD_STAMPS
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
-    !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_PT_WAVES != 5 || \
+    !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 5 || RT_MED_WAVES != 6 || RT_PT_WAVES != 5 || \
     defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif

@@ -1,0 +1,38 @@
+"""DESIGN.md §5 table rows from the committed evidence: bench lines (ms/frame, segments),
+profiles/valu_issue.json (SQ_INSTS_VALU per segment) and profiles/pmc_traffic.json (HBM
+bytes per launch).
+  python tools/roofline_table.py <dir with bench_<scene>.log files>
+"""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PEAK_VALU = 256 * 4 * 2.4 / 2  # G wave64 VALU instructions / s (bench.py VALU_GINST_PER_CU x 256 CUs)
+PEAK_HBM = 8000.0  # GB/s
+SCENES = ["cornellbox1", "spheres", "bunny", "media", "materialball", "suzanne"]
+
+
+def main(src):
+    valu = json.load(open(os.path.join(REPO, "profiles", "valu_issue.json")))["workloads"]
+    traffic = json.load(open(os.path.join(REPO, "profiles", "pmc_traffic.json")))
+    print("| workload | ms/frame | kernel ms | G segments/s | VALU inst / segment | VALU issue (frac) | HBM bytes / launch (frac) |")
+    for sc in SCENES:
+        f = os.path.join(src, f"bench_{sc}.log")
+        if not os.path.exists(f):
+            continue
+        line = next(json.loads(s) for s in open(f) if s.startswith("{"))
+        wl = line["config"]["workload"]
+        segs = line["config"]["segments_per_frame"]
+        kms = line["roofline"]["kernel_ms"]
+        v = valu.get(wl, {}).get("valu_insts_per_segment")
+        t = traffic.get(wl, {}).get("hbm_bytes_per_launch")
+        ach = v * segs / (kms * 1e-3) / 1e9 if v else None
+        hbm = t / (kms * 1e-3) / 1e9 if t else None
+        print(f"| {wl} | {line['ms_per_step']:.3f} | {kms:.3f} | {segs / (line['ms_per_step'] * 1e-3) / 1e9:.2f} | "
+              f"{v:.2f} | {ach:.0f} G/s ({ach / PEAK_VALU:.3f}) | "
+              + (f"{t / 1e9:.2f} GB ({hbm / PEAK_HBM:.4f}) |" if t else "— |"))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
