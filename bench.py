@@ -6,7 +6,9 @@ with the HIP megakernel (librtmi.so) straight into an HBM buffer, then the
 tiles are gathered to rank 0 with one RCCL gather over xGMI (N > 1), which
 overlaps the next frame's render (double-buffered tiles); the timed region ends
 after the last frame is assembled on rank 0. The frame work is fixed as N grows
-(strong scaling).
+(strong scaling). Consecutive frames alternate between two renderer contexts on two
+HIP streams, so a frame's launch overlaps the tail of the previous one (--no-overlap:
+one context, one stream, for per-launch measurements).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 N > 1 is launched by torch.distributed.run (one process per GPU).
@@ -70,6 +72,8 @@ def parse():
                     help="rows per round-robin block (2: per-rank shard times within 1.1%% at N=8, tools/shard_balance.py)")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per pixel (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="one context and stream: consecutive frames do not overlap (per-launch roofline)")
     ap.add_argument("--cpu-spp", type=int, default=None)
     a = ap.parse_args()
     _, w, h, spp, depth, _ = SCENES[a.scene]
@@ -239,37 +243,53 @@ def main():
 
     _lib.require_parity_build("bench.py")  # an ablation / timer build would not measure the shipped kernel
     W, H = args.width, args.height
-    r = rtmi.Renderer(device=local)
-    getattr(rtmi, SCENES[args.scene][0])(r, W, H)
+    # Frame overlap (default): two contexts on two streams take alternate frames, so frame
+    # k+1's launch fills the SIMDs that frame k's persistent launch leaves idle while its
+    # last work items drain (tools/overlap_probe.py: CB1 N = 8 shard 1.17 -> 1.00 ms/frame,
+    # N = 1 7.57 -> 7.42). Every frame is still rendered completely.
+    overlap = not args.no_overlap and not rehearsal
+    rs = [rtmi.Renderer(device=local) for _ in range(2 if overlap else 1)]
+    for rr in rs:
+        getattr(rtmi, SCENES[args.scene][0])(rr, W, H)
+    r = rs[0]
     from raytracingthenextweekcuda_amd.distributed import RowShardedFrame
 
     block = args.row_block
     rows = rtmi.owned_rows(H, block, rank, world)
+    streams = [torch.cuda.Stream(device=local) for _ in rs] if overlap else None
     # N > 1: frames are pipelined - frame k's RCCL gather runs on the NCCL stream under
     # frame k+1's render (double-buffered tiles); every frame is complete by the end
     frame = RowShardedFrame(W, H, block,
                             device=torch.device("cpu") if rehearsal else torch.device("cuda", local),
-                            pipeline=world > 1)
+                            pipeline=world > 1, streams=streams)
     integrator = INTEGRATOR.get(args.scene, "rayColor")
     params = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, world, args.lanes, integrator)
     # timed launches add to the device counters (one read after the loop, no
-    # per-frame host sync); the first timed launch resets them
+    # per-frame host sync); each context's first timed launch resets them
     params_keep = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, world, args.lanes, integrator,
                            keep_counters=True)
     stream = torch.cuda.current_stream()
     scratch = torch.empty(frame.tile.shape, dtype=torch.float32, device="cuda") if rehearsal else None
 
-    def render_into(tile, p):
+    def launch_stream(b):
+        return streams[b] if overlap else stream
+
+    def render_into(tile, p, b=0):
         if rehearsal:
             r.render_device(p, scratch.data_ptr(), stream.cuda_stream)
             tile.copy_(scratch.cpu())
         else:
-            r.render_device(p, tile.data_ptr(), stream.cuda_stream)
+            rs[b].render_device(p, tile.data_ptr(), launch_stream(b).cuda_stream)
 
     for _ in range(args.warmup):
-        frame.submit(lambda tile: render_into(tile, params))
+        if overlap:
+            frame.submit(lambda tile, b: render_into(tile, params, b))
+        else:
+            frame.submit(lambda tile: render_into(tile, params))
         frame.drain()
-        r.stats()
+    torch.cuda.synchronize()
+    for rr in rs:
+        rr.stats()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
     if world > 1:
@@ -277,12 +297,12 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        p = params if i == 0 else params_keep
+        p = params if i < len(rs) else params_keep
 
-        def timed_render(tile, p=p, e=ev[i]):
-            e[0].record(stream)  # on the stream the kernel is launched on
-            render_into(tile, p)
-            e[1].record(stream)
+        def timed_render(tile, b=0, p=p, e=ev[i]):
+            e[0].record(launch_stream(b))  # on the stream the kernel is launched on
+            render_into(tile, p, b)
+            e[1].record(launch_stream(b))
 
         frame.submit(timed_render)  # this rank's row tiles; the RCCL gather to rank 0 overlaps the next frame
     frame.drain()  # the last frame's gather and row assembly
@@ -290,7 +310,11 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    st = r.stats()  # counters summed over the timed launches
+    sts = [rr.stats() for rr in rs]  # counters summed over each context's timed launches
+    st = dict(sts[0])
+    for k in ("segments", "tri_tests", "box_tests", "node_visits", "group_sphere_tests",
+              "group_moving_sphere_tests", "launches", "kernel_ms_sum"):
+        st[k] = sum(x[k] for x in sts)
     launch_ms = [a.elapsed_time(b) for a, b in ev]  # render kernel + the work queue's combine pass
     assert st["launches"] == args.steps, st["launches"]
     kern_ms = [st["kernel_ms_sum"] / st["launches"]]  # the megakernel alone (the library's event pairs)
@@ -326,7 +350,7 @@ def main():
                      + box_tests / K / world * BYTES["box"] + nodes / K / world * BYTES["node"]
                      + grp / K / world
                      + rows_tot / world * W * BYTES["pixel"])
-        record_gbs = alg_bytes / (kmean * 1e-3) / 1e9
+        record_gbs = alg_bytes / ((ms_frame if overlap else kmean) * 1e-3) / 1e9
         workload = f"{args.scene}_{W}x{H}_spp{args.spp}_d{args.depth}_n{world}"
         traffic = load_pmc_traffic(workload)
         # Roofline: the megakernel is bound by VALU issue. achieved = VALU
@@ -336,7 +360,10 @@ def main():
         valu_peak = n_cu * VALU_GINST_PER_CU
         vp = load_valu_profile(workload)
         valu_launch = vp["valu_insts_per_segment"] * seg_launch if vp else None
-        valu_achieved = valu_launch / (kmean * 1e-3) / 1e9 if vp else None
+        # with frame overlap a launch's event pair also spans the next frame's launch: the
+        # launch's effective duration is then the frame time (wall / K)
+        t_eff = ms_frame if overlap else kmean
+        valu_achieved = valu_launch / (t_eff * 1e-3) / 1e9 if vp else None
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args, host_threads())
@@ -368,16 +395,23 @@ def main():
                 "unit": "Ginst/s (wave64 VALU instructions)",
                 "frac": round(valu_achieved / valu_peak, 4) if vp else None,
                 "traffic": traffic,
-                "kernel_ms": round(kmean, 4),
+                # the launch duration `achieved` divides by: the event-pair mean, or with frame
+                # overlap the frame time (the pairs then also span the wait behind the other stream)
+                "kernel_ms": round(t_eff, 4),
+                "kernel_ms_event_pairs": round(kmean, 4),
                 "launch_ms": round(float(np.mean(launch_ms)), 4),
                 "valu_insts_per_launch": int(valu_launch) if vp else None,
                 "valu_profile": vp.get("source") if vp else None,
-                "hbm_frac": round(traffic / (kmean * 1e-3) / (HBM_PEAK_GBS * 1e9), 5) if traffic else None,
+                "hbm_frac": round(traffic / (t_eff * 1e-3) / (HBM_PEAK_GBS * 1e9), 5) if traffic else None,
+                "overlap": overlap,
                 "record_bytes_per_launch": int(alg_bytes),
                 "record_gbs": round(record_gbs, 1),
                 "note": ("achieved = SQ_INSTS_VALU per segment (rocprofv3 pass on this workload, "
-                         "profiles/valu_issue.json) x this launch's segments / the megakernel's mean time "
-                         "(library event pairs, combine pass excluded); peak = CUs x 4 SIMDs x 2.4 GHz / 2 "
+                         "profiles/valu_issue.json) x this launch's segments / the launch's effective time: the "
+                         "frame time when consecutive frames overlap on two streams (overlap: true; "
+                         "kernel_ms_event_pairs then also spans the wait behind the other stream's launch), "
+                         "else the megakernel's mean time (library event pairs, combine pass excluded; "
+                         "rocprofv3 kernel traces are taken with --no-overlap); peak = CUs x 4 SIMDs x 2.4 GHz / 2 "
                          "cycles per wave64 VALU op. traffic = HBM-side bytes per launch (FETCH_SIZE x 2 + "
                          "WRITE_SIZE, profiles/pmc_traffic.json), hbm_frac its share of 8 TB/s; "
                          "record_* = SURVEY 8(d)'s cache-served record-byte model"),
@@ -387,7 +421,8 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    r.close()
+    for rr in rs:
+        rr.close()
 
 
 if __name__ == "__main__":

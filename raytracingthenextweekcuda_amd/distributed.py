@@ -41,7 +41,7 @@ class RowShardedFrame:
     """
 
     def __init__(self, width: int, height: int, row_block: int, group=None, device=None,
-                 pipeline: bool = False):
+                 pipeline: bool = False, streams=None):
         import torch
         import torch.distributed as dist
 
@@ -59,11 +59,20 @@ class RowShardedFrame:
         self.src_rows = None
         self.pending = None  # (async gather work, landing block index) of the last submitted frame
         self.n_submitted = 0
+        # Frame overlap (streams = two torch.cuda.Streams): consecutive frames alternate
+        # between two buffers AND two streams, so frame k+1's render runs while frame k's
+        # launch drains its last work items (a persistent launch's tail leaves SIMDs idle);
+        # render_into(tile, b) must then launch on streams[b]. Without streams every frame
+        # runs on the current stream.
+        self.streams = streams
         if self.world == 1:
             # one rank owns every row in order: render straight into the frame
             self.frame = torch.zeros((height, width, 3), dtype=torch.float32, device=self.device)
             self.tile = self.frame
+            self.frames = [self.frame] + ([torch.zeros_like(self.frame)] if streams else [])
             return
+        if streams and not pipeline:
+            raise ValueError("frame overlap (streams) needs pipeline=True")
         self.tile = torch.zeros((self.max_rows, width, 3), dtype=torch.float32, device=self.device)
         # pipelined frames (submit/drain): two tile buffers (and two landing blocks on rank 0),
         # so frame k's gather overlaps frame k+1's render
@@ -71,6 +80,7 @@ class RowShardedFrame:
         self.tiles = [self.tile] + ([torch.zeros_like(self.tile)] if pipeline else [])
         if self.rank == 0:
             self.frame = torch.zeros((height, width, 3), dtype=torch.float32, device=self.device)
+            self.frames = [self.frame] + ([torch.zeros_like(self.frame)] if streams else [])
             # the gather lands in one (world * max_rows) block; frame row y is
             # block row rank(y) * max_rows + (its position in that rank's tile)
             self.gathered = torch.empty((self.world * self.max_rows, width, 3), dtype=torch.float32,
@@ -102,30 +112,49 @@ class RowShardedFrame:
         return self.gather()
 
     # ---- pipelined frames ----
+    def _on(self, b):
+        """Context that makes buffer b's stream current (a no-op without frame overlap)."""
+        import contextlib
+
+        return self.torch.cuda.stream(self.streams[b]) if self.streams else contextlib.nullcontext()
+
     def _finish_pending(self):
         work, b = self.pending
         self.pending = None
-        work.wait()  # the current stream waits for the gather (the host does not, on NCCL)
-        if self.rank == 0:
-            self.torch.index_select(self.landing[b][0], 0, self.src_rows, out=self.frame)
+        with self._on(b):
+            # this stream waits for the gather (the host does not, on NCCL): the assembly and
+            # the next render into tile b come after it
+            work.wait()
+            if self.rank == 0:
+                self.frame = self.frames[b] if self.streams else self.frame
+                self.torch.index_select(self.landing[b][0], 0, self.src_rows, out=self.frame)
 
-    def submit(self, render_into: Callable[["object"], None]):
+    def submit(self, render_into: Callable[..., None]):
         """Render the next frame into the free tile buffer and start its gather without
         waiting for it; the previous frame's gather (which ran under this render) is
-        completed and assembled on rank 0 after this frame's render is enqueued."""
+        completed and assembled on rank 0 after this frame's render is enqueued. With
+        frame overlap, render_into(tile, b) is called and must launch on streams[b]."""
+        b = self.n_submitted % 2
+        self.n_submitted += 1
         if self.world == 1:
-            render_into(self.frame)
+            if self.streams:
+                self.frame = self.frames[b]
+                render_into(self.frame, b)
+            else:
+                render_into(self.frame)
             return
         if not self.pipeline:
             raise RuntimeError("RowShardedFrame(pipeline=True) is required for submit()")
-        b = self.n_submitted % 2
-        self.n_submitted += 1
         tile = self.tiles[b]
-        render_into(tile)  # enqueued before waiting on the previous gather
+        if self.streams:
+            render_into(tile, b)  # on streams[b], which waited for the last gather out of tile b
+        else:
+            render_into(tile)  # enqueued before waiting on the previous gather
         if self.pending is not None:
             self._finish_pending()
-        work = self.dist.gather(tile, self.landing[b][1] if self.rank == 0 else None, dst=0,
-                                group=self.group, async_op=True)
+        with self._on(b):  # the NCCL stream waits for this frame's render stream
+            work = self.dist.gather(tile, self.landing[b][1] if self.rank == 0 else None, dst=0,
+                                    group=self.group, async_op=True)
         self.pending = (work, b)
 
     def drain(self) -> Optional["object"]:

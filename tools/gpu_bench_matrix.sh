@@ -23,16 +23,16 @@ for sc in ${SCENES:-cornellbox1}; do
 done
 for sc in ${TRAFFIC:-}; do
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_${sc}_$c" -o pmc -- python3 bench.py --scene $sc --steps 1 --warmup 1 --no-cpu-baseline > "$O/pmc_${sc}_$c.log" 2>&1
+    timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_${sc}_$c" -o pmc -- python3 bench.py --scene $sc --steps 1 --warmup 1 --no-cpu-baseline --no-overlap > "$O/pmc_${sc}_$c.log" 2>&1
     stop_if_fatal $? pmc_${sc}_$c
   done
 done
 for sc in ${VALU:-}; do
-  timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --output-format csv -d "$O/pmc_valu_$sc" -o pmc -- python3 bench.py --scene $sc --steps 2 --warmup 1 --no-cpu-baseline > "$O/pmc_valu_$sc.log" 2>&1
+  timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --output-format csv -d "$O/pmc_valu_$sc" -o pmc -- python3 bench.py --scene $sc --steps 2 --warmup 1 --no-cpu-baseline --no-overlap > "$O/pmc_valu_$sc.log" 2>&1
   stop_if_fatal $? pmc_valu_$sc
 done
 for sc in ${PROF:-}; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$sc" -o run --output-format csv -- python3 bench.py --scene $sc --steps ${PROF_STEPS:-10} --warmup ${PROF_WARMUP:-2} --no-cpu-baseline > "$O/prof_$sc.log" 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$sc" -o run --output-format csv -- python3 bench.py --scene $sc --steps ${PROF_STEPS:-10} --warmup ${PROF_WARMUP:-2} --no-cpu-baseline --no-overlap > "$O/prof_$sc.log" 2>&1
   stop_if_fatal $? prof_$sc
 done
 if [ "${PROBE:-0}" = "1" ]; then

@@ -25,11 +25,11 @@ if [ "${PROBE:-1}" = "1" ]; then
   done
 fi
 for sc in ${PMC_SCENES:-cornellbox1}; do
-  timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --output-format csv -d "$O/pmc_valu_$sc" -o pmc -- python3 bench.py --scene $sc --steps 2 --warmup 1 --no-cpu-baseline > "$O/pmc_valu_$sc.log" 2>&1
+  timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --output-format csv -d "$O/pmc_valu_$sc" -o pmc -- python3 bench.py --scene $sc --steps 2 --warmup 1 --no-cpu-baseline --no-overlap > "$O/pmc_valu_$sc.log" 2>&1
   stop_if_fatal $? pmc_valu_$sc
 done
 for sc in ${PROF_SCENES:-cornellbox1}; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$sc" -o run --output-format csv -- python3 bench.py --scene $sc --steps ${PROF_STEPS:-20} --warmup 5 --no-cpu-baseline > "$O/bench_${sc}_under_rocprof.log" 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$sc" -o run --output-format csv -- python3 bench.py --scene $sc --steps ${PROF_STEPS:-20} --warmup 5 --no-cpu-baseline --no-overlap > "$O/bench_${sc}_under_rocprof.log" 2>&1
   stop_if_fatal $? prof_$sc
 done
 if [ -x ./examples/multigpu ]; then
