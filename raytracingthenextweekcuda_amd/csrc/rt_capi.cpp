@@ -645,7 +645,8 @@ rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& 
     // static grid maps one pixel's sub-streams onto lanes of one wave (<= 64)
     if (s < 0 || s > (queue ? 128 : 64) || (s & (s - 1)) != 0)
         return fail(c, RT_ERR_INVALID, "lanes_per_pixel must be 0 (auto) or a power of two <= 128 (64 static)");
-    rt::choose_layout(L, s, queue);
+    const bool bvh = p->integrator == RT_INTEGRATOR_PATHTRACE || !c->scene.nodes.empty();
+    rt::choose_layout(L, s, queue, bvh);
     L.accumulate = 0;
     L.accum_scale = 0.0f;
     L.u8 = nullptr;

@@ -78,7 +78,13 @@ struct RenderLaunch {
 // coherent waves (less divergence in BVH traversal and mesh compaction).
 // Work-queue launches (the default) take the largest power of two
 // S <= min(32, spp) with pixels * S <= 2^25 items (the partial-sum buffer stays
-// <= 400 MB); static launches the largest with pixels * S <= 2^24 lanes.
+// <= 400 MB); launches that traverse BVHs (`bvh`: rayColor meshes / sphere groups,
+// or pathTrace) the largest S <= min(128, spp) with pixels * S <= 2^27 (1.6 GB): a
+// whole wave on one pixel keeps the traversal coherent (same box, frame overlap on:
+// random spheres S = 32 / 64 / 128 -> 76.7 / 73.8 / 71.8 ms, bunny 517.0 / 518.6 / 516.5,
+// while CornellBox1 without BVHs is best at 32: 7.39 vs 7.61 at 64;
+// profiles/r02/lanes_sweep.txt). Static launches take the largest S <= min(32, spp)
+// with pixels * S <= 2^24 lanes.
 // `pixels` is the FULL frame (width * height), not this shard's rows: every rank
 // of a row-sharded frame then folds a pixel's samples with the same S, so the
 // assembled frame is bit-identical for any world size (and N > 1 shards do the
@@ -86,13 +92,15 @@ struct RenderLaunch {
 // Measured on one MI355X, ms/frame (static S=1 -> static auto -> queue auto):
 // CornellBox1 11.9 -> 10.7 -> 8.9, random spheres 245 -> 164 -> 113,
 // materialball 34.5 -> 14.5 -> 11.7, bunny 999 -> 950 -> 765, media 1982 -> 2015 -> 1883.
-inline void choose_layout(RenderLaunch& L, int32_t requested, bool queue) {
+inline void choose_layout(RenderLaunch& L, int32_t requested, bool queue, bool bvh) {
     int32_t s = requested;
     if (s <= 0) {
         s = 1;
         const int64_t px = (int64_t)L.height * L.width;
-        const int64_t cap = queue ? (int64_t(1) << 25) : (int64_t(1) << 24);
-        while (2 * s <= 32 && 2 * s <= L.spp && px * 2 * s <= cap) s *= 2;
+        const bool wide = queue && bvh;
+        const int64_t cap = wide ? (int64_t(1) << 27) : queue ? (int64_t(1) << 25) : (int64_t(1) << 24);
+        const int32_t smax = wide ? 128 : 32;
+        while (2 * s <= smax && 2 * s <= L.spp && px * 2 * s <= cap) s *= 2;
     }
     L.lanes_per_pixel = s;
     L.sp_log2 = 0;

@@ -222,6 +222,21 @@ def test_auto_lane_layout(rtmi):
         assert r.stats()["lanes_per_pixel"] == 8  # 4M pixels x 8 = 2^25 work items
 
 
+def test_auto_lane_layout_bvh(rtmi):
+    # launches that traverse BVHs: largest power of two S <= min(128, spp) with
+    # pixels * S <= 2^27 (rt_kernel.h choose_layout)
+    with rtmi.Renderer(0) as r:
+        rtmi.suzanne_cornell_box(r, 64, 64)
+        r.render(64, 64, 256, 3, lanes_per_pixel=0)
+        assert r.stats()["lanes_per_pixel"] == 128
+        r.render(64, 64, 32, 3, lanes_per_pixel=0)
+        assert r.stats()["lanes_per_pixel"] == 32
+    with rtmi.Renderer(0) as r:
+        rtmi.materialball(r, 48, 32)
+        r.render(48, 32, 64, 5, lanes_per_pixel=0, integrator="pathTrace")
+        assert r.stats()["lanes_per_pixel"] == 64
+
+
 def test_auto_layout_within_north_star_tolerance_of_sequential_sum(rtmi):
     # the bench's auto layout sums samples in S sub-streams: bit-exact against the
     # oracle with the same S, and within 1e-4 of the reference's sequential sum
