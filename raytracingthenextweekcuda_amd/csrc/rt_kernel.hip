@@ -776,15 +776,22 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
     const v3 c{f[0], f[1], f[2]}, e{f[3], f[4], f[5]};
     const v3 pos[6] = {{c.x - e.x, c.y, c.z}, {c.x + e.x, c.y, c.z}, {c.x, c.y + e.y, c.z},
                        {c.x, c.y - e.y, c.z}, {c.x, c.y, c.z + e.z}, {c.x, c.y, c.z - e.z}};
-    const v3 nrm[6] = {{-1.0f, 0.0f, 0.0f}, {1.0f, 0.0f, 0.0f}, {0.0f, 1.0f, 0.0f},
-                       {0.0f, -1.0f, 0.0f}, {0.0f, 0.0f, 1.0f}, {0.0f, 0.0f, -1.0f}};
     float tf[6];
     bool ok[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
         const v3 p = pos[k];
-        const float den = dot(nrm[k], d);
-        const float t = fdiv(dot(sub(p, o), nrm[k]), den);
+        // Plane::hit with the face's unit normal +-e_a (a = k / 2): dot(n, d) is +-d_a and
+        // dot(p - o, n) is +-(p_a - o_a) - the zero terms only decide the sign of a zero,
+        // which no test below can see (the faces count only when |d_a| > tMin; ray origins
+        // and directions are finite, or all NaN) - and (-x) / (-y) = x / y, so
+        // t = (p_a - o_a) / d_a is the restatement's quotient bit for bit.
+        const int a = k >> 1;
+        const float da = a == 0 ? d.x : (a == 1 ? d.y : d.z);
+        const float pa = a == 0 ? p.x : (a == 1 ? p.y : p.z);
+        const float oa = a == 0 ? o.x : (a == 1 ? o.y : o.z);
+        const float den = da;
+        const float t = fdiv(pa - oa, da);
         const v3 q = add(o, scale(d, t));
         bool in;
         if (k < 2)  // YZ faces
