@@ -188,6 +188,26 @@ struct Hit {
             }
         }
     }
+    // merge() for candidates that arrive in increasing scan order (the linear-scan kernel:
+    // no sphere groups, so objects, mesh runs and media merge in slot order): an equal t of
+    // a later object never lowers mi, so only the strict-less update and a later sphere at
+    // the same t remain. Same result as merge() for such sequences.
+    template <bool kOrdered>
+    __device__ __forceinline__ void merge_seq(float tc, uint32_t order, bool sphere, int32_t o, int32_t tr) {
+        if constexpr (!kOrdered) {
+            merge(tc, order, sphere, o, tr);
+        } else if (tc < t) {
+            t = tc;
+            mi = order;
+            obj = o;
+            tri = tr;
+            ms_obj = sphere ? o : -1;
+            ms = order;
+        } else if (sphere && tc == t) {
+            ms_obj = o;
+            ms = order;
+        }
+    }
     __device__ __forceinline__ void finish() {
         if (ms_obj >= 0 && ms > mi) {
             obj = ms_obj;
@@ -625,6 +645,7 @@ __device__ __forceinline__ ObjRec load_obj(const ObjRec* __restrict__ objs, int 
 // consecutive meshes are consecutive in `tris` (their bases rise with scan order), so
 // the per-lane minimum of (t, global triangle index) over the run is the candidate the
 // sequential hit() keeps: smallest t, then the earliest mesh, then its lowest triangle.
+template <bool kOrdered>
 __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
                                          int i0, uint32_t g, uint32_t m, uint32_t magic, bool live, v3 o, v3 d,
                                          v3 inv, Hit& h, Counters& cnt, WaveLds& W, int lane) {
@@ -690,7 +711,8 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
             const uint32_t tri = (uint32_t)(key & 0xFFFFFFFFu);
             const uint32_t base0 = objs[i0].u0;  // wave-uniform
             const uint32_t j = m > 1u ? __umulhi(tri - base0, magic) : tri - base0;  // the mesh in the run
-            h.merge(__uint_as_float((uint32_t)(key >> 32)), objs[i0].order + j, false, i0 + (int)j, (int32_t)tri);
+            h.merge_seq<kOrdered>(__uint_as_float((uint32_t)(key >> 32)), objs[i0].order + j, false, i0 + (int)j,
+                                  (int32_t)tri);
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -839,6 +861,9 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
 // wave active; `live` masks lanes without a path. Records are fetched one
 // object ahead (scalar loads overlap the current object's VALU work), and the
 // per-object tests are branch-free candidates merged with Hit's tie rule.
+#ifndef RT_ORDERED_MERGE
+#define RT_ORDERED_MERGE 1  // linear-scan kernels merge candidates with Hit::merge_seq<true> (0: A/B)
+#endif
 #ifndef RT_MED_MERGE1
 #define RT_MED_MERGE1 1  // the media variant merges once per object (0: per branch, A/B)
 #endif
@@ -864,6 +889,8 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
 #define RT_OBJ_PREFETCH 1
 #endif
     constexpr bool kPf = RT_OBJ_PREFETCH && !kMed;
+    // no sphere groups: merges come in scan order (the media variant measured slower with it)
+    constexpr bool kOrd = RT_ORDERED_MERGE && !kBvh && !kMed;
     ObjRec cur = load_obj(S.objs, 0);
     for (int i = 0; i < n; ++i) {
         const ObjRec ob = kPf ? cur : load_obj(S.objs, i);
@@ -876,7 +903,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 tc = t;
                 tsph = sphere;
             } else {
-                h.merge(t, ob.order, sphere, i, -1);
+                h.merge_seq<kOrd>(t, ob.order, sphere, i, -1);
             }
         };
         if (ob.type == kObjPlane) {
@@ -912,7 +939,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 const uint32_t g = __float_as_uint(ob.f[7]);  // run length (0: inside a run)
                 RT_STAMP(t_m0);
                 if (g != 0u)
-                    mesh_run(S.objs, S.tris, i, g, ob.u1, __float_as_uint(ob.f[6]), live, o, d, inv, h, cnt, W,
+                    mesh_run<kOrd>(S.objs, S.tris, i, g, ob.u1, __float_as_uint(ob.f[6]), live, o, d, inv, h, cnt, W,
                              lane);
                 RT_STAMP(t_m1);
                 RT_ACC(3, t_m0, t_m1);
@@ -943,7 +970,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
         } else if (kBvh) {  // kObjSphereGroup
             sphere_group(S.objs, S.nodes, ob.u2, live, ray, inv, h, stack, cnt, S.stack_cap);
         }
-        if constexpr (kMed && RT_MED_MERGE1) h.merge(tc, ob.order, tsph, i, -1);  // NaN: no candidate
+        if constexpr (kMed && RT_MED_MERGE1) h.merge_seq<kOrd>(tc, ob.order, tsph, i, -1);  // NaN: no candidate
     }
     h.finish();
     return h;
@@ -2257,7 +2284,7 @@ uint32_t kernel_build_flags() {
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
     !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 5 || RT_MED_WAVES != 6 || RT_PT_WAVES != 5 || \
-    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN
+    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;
