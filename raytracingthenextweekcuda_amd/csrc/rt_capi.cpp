@@ -580,8 +580,12 @@ static rt_status rt_commit_impl(rt_ctx* c) {
     c->n_objs = S.n_scan;
     c->n_mats = (int)S.mats.size();
     c->has_media = false;
-    for (int32_t i = 0; i < S.n_scan && i < (int32_t)S.objs.size(); ++i)
-        if (S.objs[(size_t)i].type == rt::kObjMedium) c->has_media = true;
+    c->has_spheres = false;
+    for (int32_t i = 0; i < S.n_scan && i < (int32_t)S.objs.size(); ++i) {
+        const uint32_t t = S.objs[(size_t)i].type;
+        if (t == rt::kObjMedium) c->has_media = true;
+        if (t == rt::kObjSphere || t == rt::kObjMovingSphere) c->has_spheres = true;
+    }
     c->committed = true;
     return RT_OK;
 }
@@ -701,7 +705,7 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
         if (have) {
             const int waves = p->integrator == RT_INTEGRATOR_PATHTRACE
                                   ? rt::pathtrace_queue_waves()
-                                  : rt::render_queue_waves(!c->scene.nodes.empty(), c->has_media);
+                                  : rt::render_queue_waves(!c->scene.nodes.empty(), c->has_media, c->has_spheres);
             L.queue = rt::queue_blocks(c->n_cu, waves);
             L.n_items = (uint32_t)items;
             L.n_pix = (uint32_t)(items >> L.sp_log2);
@@ -760,6 +764,7 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
         rt::SceneArgs sc{c->d_objs,   c->d_tris,  c->d_mats,  c->d_nodes,
                          c->d_tri_orig, c->n_objs, c->n_mats, !c->scene.nodes.empty()};
         sc.has_media = c->has_media;
+        sc.has_spheres = c->has_spheres;
         RT_HIP(c, rt::launch_render(sc, c->d_cam, L, out, c->d_counters, st, k1));
     }
     RT_HIP(c, hipEventRecord(c->ev1, st));

@@ -31,6 +31,7 @@ struct rt_ctx {
     uint32_t* d_tri_orig = nullptr;
     int n_objs = 0;
     bool has_media = false;   // the committed scan list holds a participating medium (kernel variant)
+    bool has_spheres = true;  // the committed scan list holds a (moving) sphere (kernel variant)
     int n_mats = 0;
     unsigned long long* d_counters = nullptr;
     rt::CamRec* d_cam = nullptr;  // device copy of scene.camera read by the kernels

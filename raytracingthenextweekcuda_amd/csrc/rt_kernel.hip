@@ -867,6 +867,9 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
 #ifndef RT_MED_MERGE1
 #define RT_MED_MERGE1 1  // the media variant merges once per object (0: per branch, A/B)
 #endif
+#ifndef RT_NOSPH_VARIANT
+#define RT_NOSPH_VARIANT 1  // sphere-free scenes without BVHs or media take render_kernel<false, *, false, false>
+#endif
 #ifndef RT_MED_VARIANT
 #define RT_MED_VARIANT 1  // media scenes without BVHs take render_kernel<false, *, true> (0: A/B)
 #endif
@@ -874,7 +877,7 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
 // no record prefetch (the medium test is long and the next record's 16 SGPRs stay live
 // across it) and one merge per object (the type branches yield a candidate instead of
 // each updating the Hit state). Both were measured slower on the other scenes.
-template <bool kBvh, bool kMed = false>
+template <bool kBvh, bool kMed = false, bool kSph = true>
 __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v3 inv, bool live,
                                            Rng& rng, WaveLds& W, uint32_t* stack, int lane,
                                            Counters& cnt
@@ -928,7 +931,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             const bool in = (pa > f[6]) & (pa < f[7]) & (pb > f[8]) & (pb < f[9]);
             const bool ok = proceed & (t >= kTMin) & in;
             cand(ok ? t : __builtin_nanf(""), false);
-        } else if (ob.type == kObjSphere || ob.type == kObjMovingSphere) {
+        } else if ((kSph || kBvh || kMed) && (ob.type == kObjSphere || ob.type == kObjMovingSphere)) {
             cand(sphere_candidate(ob, o, d, ray.time), true);
         } else if (ob.type == kObjMesh) {
             // TriangleMesh::hit (TriangleMesh.cu:34-117): the AABB early-out
@@ -965,7 +968,9 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                          S.stack_cap);
 #endif
             }
-        } else if (ob.type == kObjMedium) {
+        } else if ((kMed || kBvh || !RT_MED_VARIANT) && ob.type == kObjMedium) {
+            // (the general linear-scan kernel never sees a medium: launch_render sends scenes with
+            // media to the kMed variant, so its register allocation need not cover this test)
             cand(live ? medium_candidate(ob, o, d, rng) : __builtin_nanf(""), false);
         } else if (kBvh) {  // kObjSphereGroup
             sphere_group(S.objs, S.nodes, ob.u2, live, ray, inv, h, stack, cnt, S.stack_cap);
@@ -1014,18 +1019,22 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }  // namespace
 
 // Occupancy per kernel (min waves per SIMD; VGPR budget 512 / waves): the BVH rayColor
-// kernel at 4 (128 VGPRs, spill-free), the linear-scan rayColor kernel at 5 (96 VGPRs,
-// spill-free since the launch parameters are read at their use), its media variant at 6
-// and the pathTrace kernel at 5 (same-box A/B in DESIGN.md §4; profiles/r02/ab_occ*.txt).
+// kernel at 4 (128 VGPRs, spill-free), the linear-scan rayColor kernel at 6 (89 VGPRs at 5
+// since it no longer carries the medium test; 9 spilled at 6 and still faster), its
+// sphere-free variant at 7, its media variant at 6 and the pathTrace kernel at 5 (same-box
+// A/B in DESIGN.md §4; profiles/r02/ab_occ*.txt, ab_no_medium.txt, ab_no_spheres.txt).
 // -DRT_WAVES_PER_EU=k forces all to k.
 #ifndef RT_BVH_WAVES
 #define RT_BVH_WAVES 4
 #endif
 #ifndef RT_SCAN_WAVES
-#define RT_SCAN_WAVES 5
+#define RT_SCAN_WAVES 6
 #endif
 #ifndef RT_MED_WAVES
 #define RT_MED_WAVES 6
+#endif
+#ifndef RT_NOSPH_WAVES
+#define RT_NOSPH_WAVES 7
 #endif
 #ifndef RT_PT_WAVES
 #define RT_PT_WAVES 5
@@ -1034,14 +1043,18 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #undef RT_BVH_WAVES
 #undef RT_SCAN_WAVES
 #undef RT_MED_WAVES
+#undef RT_NOSPH_WAVES
 #undef RT_PT_WAVES
 #define RT_BVH_WAVES RT_WAVES_PER_EU
 #define RT_SCAN_WAVES RT_WAVES_PER_EU
 #define RT_MED_WAVES RT_WAVES_PER_EU
+#define RT_NOSPH_WAVES RT_WAVES_PER_EU
 #define RT_PT_WAVES RT_WAVES_PER_EU
 #endif
-template <bool kBvh, bool kMed = false>
-constexpr int render_waves() { return kBvh ? RT_BVH_WAVES : (kMed ? RT_MED_WAVES : RT_SCAN_WAVES); }
+template <bool kBvh, bool kMed = false, bool kSph = true>
+constexpr int render_waves() {
+    return kBvh ? RT_BVH_WAVES : (kMed ? RT_MED_WAVES : (kSph ? RT_SCAN_WAVES : RT_NOSPH_WAVES));
+}
 
 // Canvas::gamma (Canvas.h:198-200) with clamp = fmaxf(a, fminf(f, b)).
 __device__ __forceinline__ uint8_t gamma_u8(float c) {
@@ -1292,8 +1305,10 @@ __device__ __forceinline__ int global_row_of(const RenderLaunch& L, int lr) {
     return (lb * L.row_world + L.row_rank) * L.row_block + (lr - lb * L.row_block);
 }
 
-template <bool kBvh, bool kQueue, bool kMed = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_waves<kBvh, kMed>()))) void render_kernel(
+// kSph = false: the linear-scan variant for scenes without spheres (CornellBox1): neither the
+// sphere test nor the sphere normals are compiled in (rt_capi.cpp picks it).
+template <bool kBvh, bool kQueue, bool kMed = false, bool kSph = true>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_waves<kBvh, kMed, kSph>()))) void render_kernel(
     RenderLaunch L, const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
     const MatRec* __restrict__ mats, const BvhNode* __restrict__ nodes,
     const uint32_t* __restrict__ tri_orig, int n_objs, const CamRec* __restrict__ cam,
@@ -1405,7 +1420,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
 #endif
 
         const v3 inv = rcp(ray.d);
-        const Hit h = closest_hit<kBvh, kMed>(S, ray, inv, live, rng, W, stack, lane, cnt
+        const Hit h = closest_hit<kBvh, kMed, kSph>(S, ray, inv, live, rng, W, stack, lane, cnt
 #ifdef RT_STAMPS
                                         , tm
 #endif
@@ -1427,13 +1442,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             const float* f = ob.f;
             v3 p = add(ray.o, scale(ray.d, h.t));  // ray.at(t)
             v3 outward;
-            if (ob.type == kObjMedium) {
+            constexpr bool kAnySph = kSph || kBvh || kMed;
+            if ((kMed || kBvh || !RT_MED_VARIANT) && ob.type == kObjMedium) {
                 outward = v3{1.0f, 0.0f, 0.0f};  // arbitrary; isotropic scatter ignores it
             } else if (ob.type == kObjPlane) {
                 outward = v3{f[3], f[4], f[5]};
-            } else if (ob.type == kObjSphere) {
+            } else if (kAnySph && ob.type == kObjSphere) {
                 outward = divs(sub(p, v3{f[0], f[1], f[2]}), f[3]);
-            } else if (ob.type == kObjMovingSphere) {
+            } else if (kAnySph && ob.type == kObjMovingSphere) {
                 outward = divs(sub(p, moving_center(f, ray.time)), f[8]);
             } else {
                 const TriRec& tr = S.tris[h.tri];
@@ -2267,8 +2283,11 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
 
 // A persistent grid fills the resident waves: waves per SIMD x 4 SIMDs / 4-wave blocks per CU.
 int queue_blocks(int n_cu, int waves_per_simd) { return n_cu * waves_per_simd; }
-int render_queue_waves(bool bvh, bool media) {
-    return bvh ? render_waves<true>() : (media && RT_MED_VARIANT ? render_waves<false, true>() : render_waves<false>());
+int render_queue_waves(bool bvh, bool media, bool spheres) {
+    if (bvh) return render_waves<true>();
+    if (media && RT_MED_VARIANT) return render_waves<false, true>();
+    if (!spheres && RT_NOSPH_VARIANT) return render_waves<false, false, false>();
+    return render_waves<false>();
 }
 int pathtrace_queue_waves() { return RT_PT_WAVES; }
 
@@ -2283,8 +2302,8 @@ uint32_t kernel_build_flags() {
     f |= 2u;  // RT_BUILD_STAMPS
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
-    !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 5 || RT_MED_WAVES != 6 || RT_PT_WAVES != 5 || \
-    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE
+    !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_PT_WAVES != 5 || \
+    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE || !RT_NOSPH_VARIANT
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;
@@ -2305,6 +2324,9 @@ hipError_t launch_render(const SceneArgs& sc, const CamRec* cam, const RenderLau
         else if (sc.has_media && RT_MED_VARIANT)
             hipLaunchKernelGGL((render_kernel<false, true, true>), grid, block, 0, stream, L, sc.objs, sc.tris,
                                sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
+        else if (!sc.has_spheres && RT_NOSPH_VARIANT)
+            hipLaunchKernelGGL((render_kernel<false, true, false, false>), grid, block, 0, stream, L, sc.objs,
+                               sc.tris, sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
         else
             hipLaunchKernelGGL((render_kernel<false, true>), grid, block, 0, stream, L, sc.objs, sc.tris,
                                sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
@@ -2322,6 +2344,9 @@ hipError_t launch_render(const SceneArgs& sc, const CamRec* cam, const RenderLau
     else if (sc.has_media && RT_MED_VARIANT)
         hipLaunchKernelGGL((render_kernel<false, false, true>), grid, block, 0, stream, L, sc.objs, sc.tris, sc.mats,
                            sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
+    else if (!sc.has_spheres && RT_NOSPH_VARIANT)
+        hipLaunchKernelGGL((render_kernel<false, false, false, false>), grid, block, 0, stream, L, sc.objs, sc.tris,
+                           sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
     else
         hipLaunchKernelGGL((render_kernel<false, false>), grid, block, 0, stream, L, sc.objs, sc.tris, sc.mats,
                            sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
