@@ -580,11 +580,18 @@ static rt_status rt_commit_impl(rt_ctx* c) {
     c->n_objs = S.n_scan;
     c->n_mats = (int)S.mats.size();
     c->has_media = false;
-    c->has_spheres = false;
+    c->full_scan = false;
+    c->bvh_parts = 0;
     for (int32_t i = 0; i < S.n_scan && i < (int32_t)S.objs.size(); ++i) {
         const uint32_t t = S.objs[(size_t)i].type;
         if (t == rt::kObjMedium) c->has_media = true;
-        if (t == rt::kObjSphere || t == rt::kObjMovingSphere) c->has_spheres = true;
+        if (t == rt::kObjSphere || t == rt::kObjMovingSphere) c->full_scan = true;
+        if (t == rt::kObjMesh && S.objs[(size_t)i].u2 != rt::kNoBvh) c->bvh_parts |= 1;
+        if (t == rt::kObjSphereGroup) c->bvh_parts |= 2;
+        // the simple-scene kernel variant shades Lambertian (0) and emissive (3) materials only
+        const uint32_t mi = S.objs[(size_t)i].material;
+        const uint32_t mt = mi < S.mats.size() ? S.mats[mi].type : 0xFFFFFFFFu;
+        if (mt != 0u && mt != 3u) c->full_scan = true;
     }
     c->committed = true;
     return RT_OK;
@@ -705,7 +712,7 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
         if (have) {
             const int waves = p->integrator == RT_INTEGRATOR_PATHTRACE
                                   ? rt::pathtrace_queue_waves()
-                                  : rt::render_queue_waves(!c->scene.nodes.empty(), c->has_media, c->has_spheres);
+                                  : rt::render_queue_waves(!c->scene.nodes.empty(), c->has_media, c->full_scan, c->bvh_parts);
             L.queue = rt::queue_blocks(c->n_cu, waves);
             L.n_items = (uint32_t)items;
             L.n_pix = (uint32_t)(items >> L.sp_log2);
@@ -764,7 +771,8 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
         rt::SceneArgs sc{c->d_objs,   c->d_tris,  c->d_mats,  c->d_nodes,
                          c->d_tri_orig, c->n_objs, c->n_mats, !c->scene.nodes.empty()};
         sc.has_media = c->has_media;
-        sc.has_spheres = c->has_spheres;
+        sc.full_scan = c->full_scan;
+        sc.bvh_parts = c->bvh_parts;
         RT_HIP(c, rt::launch_render(sc, c->d_cam, L, out, c->d_counters, st, k1));
     }
     RT_HIP(c, hipEventRecord(c->ev1, st));

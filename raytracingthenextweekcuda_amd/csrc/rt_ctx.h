@@ -31,7 +31,8 @@ struct rt_ctx {
     uint32_t* d_tri_orig = nullptr;
     int n_objs = 0;
     bool has_media = false;   // the committed scan list holds a participating medium (kernel variant)
-    bool has_spheres = true;  // the committed scan list holds a (moving) sphere (kernel variant)
+    int bvh_parts = 3;        // 1: mesh BVHs, 2: sphere groups in the committed scan list (kernel variant)
+    bool full_scan = true;  // the committed scan list needs the general kernel (spheres, metal, glass, isotropic)
     int n_mats = 0;
     unsigned long long* d_counters = nullptr;
     rt::CamRec* d_cam = nullptr;  // device copy of scene.camera read by the kernels

@@ -138,7 +138,7 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
 // Workgroups of the persistent work-queue grid (n_cu x resident 4-wave blocks per CU),
 // and the occupancy each kernel is compiled for (waves per SIMD).
 int queue_blocks(int n_cu, int waves_per_simd);
-int render_queue_waves(bool bvh, bool media, bool spheres);
+int render_queue_waves(bool bvh, bool media, bool full, int bvh_parts);
 int pathtrace_queue_waves();
 
 hipError_t launch_render(const SceneArgs& sc, const CamRec* cam, const RenderLaunch& L,

@@ -867,6 +867,9 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
 #ifndef RT_MED_MERGE1
 #define RT_MED_MERGE1 1  // the media variant merges once per object (0: per branch, A/B)
 #endif
+#ifndef RT_BVH_PARTS_VARIANT
+#define RT_BVH_PARTS_VARIANT 1  // BVH scenes with only mesh BVHs / only sphere groups take the kParts 1 / 2 kernels
+#endif
 #ifndef RT_NOSPH_VARIANT
 #define RT_NOSPH_VARIANT 1  // sphere-free scenes without BVHs or media take render_kernel<false, *, false, false>
 #endif
@@ -877,7 +880,9 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
 // no record prefetch (the medium test is long and the next record's 16 SGPRs stay live
 // across it) and one merge per object (the type branches yield a candidate instead of
 // each updating the Hit state). Both were measured slower on the other scenes.
-template <bool kBvh, bool kMed = false, bool kSph = true>
+// kParts (BVH kernels): 1 = the scene has BVH meshes, 2 = sphere groups; the other traversal is
+// not compiled in (rt_capi.cpp picks the variant from the committed scene).
+template <bool kBvh, bool kMed = false, bool kSph = true, int kParts = 3>
 __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v3 inv, bool live,
                                            Rng& rng, WaveLds& W, uint32_t* stack, int lane,
                                            Counters& cnt
@@ -947,6 +952,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 RT_STAMP(t_m1);
                 RT_ACC(3, t_m0, t_m1);
             } else {
+                if constexpr ((kParts & 1) != 0) {
                 const bool want = live && box_hit(f, o, inv);
                 cnt.box_tests += (uint32_t)__popcll(__ballot(live));
 #else
@@ -967,12 +973,15 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 mesh_bvh(S.tris, S.tri_orig, S.nodes, root, want, o, d, inv, h, i, ob.order, stack, cnt,
                          S.stack_cap);
 #endif
+#if RT_MESH_RUN
+                }
+#endif
             }
         } else if ((kMed || kBvh || !RT_MED_VARIANT) && ob.type == kObjMedium) {
             // (the general linear-scan kernel never sees a medium: launch_render sends scenes with
             // media to the kMed variant, so its register allocation need not cover this test)
             cand(live ? medium_candidate(ob, o, d, rng) : __builtin_nanf(""), false);
-        } else if (kBvh) {  // kObjSphereGroup
+        } else if (kBvh && (kParts & 2) != 0) {  // kObjSphereGroup
             sphere_group(S.objs, S.nodes, ob.u2, live, ray, inv, h, stack, cnt, S.stack_cap);
         }
         if constexpr (kMed && RT_MED_MERGE1) h.merge_seq<kOrd>(tc, ob.order, tsph, i, -1);  // NaN: no candidate
@@ -1019,7 +1028,8 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }  // namespace
 
 // Occupancy per kernel (min waves per SIMD; VGPR budget 512 / waves): the BVH rayColor
-// kernel at 4 (128 VGPRs, spill-free), the linear-scan rayColor kernel at 6 (89 VGPRs at 5
+// kernel at 4 (128 VGPRs, spill-free; its sphere-group-only variant at 5), the linear-scan
+// rayColor kernel at 6 (89 VGPRs at 5
 // since it no longer carries the medium test; 9 spilled at 6 and still faster), its
 // sphere-free variant at 7, its media variant at 6 and the pathTrace kernel at 5 (same-box
 // A/B in DESIGN.md §4; profiles/r02/ab_occ*.txt, ab_no_medium.txt, ab_no_spheres.txt).
@@ -1036,6 +1046,9 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #ifndef RT_NOSPH_WAVES
 #define RT_NOSPH_WAVES 7
 #endif
+#ifndef RT_GROUP_WAVES
+#define RT_GROUP_WAVES 5
+#endif
 #ifndef RT_PT_WAVES
 #define RT_PT_WAVES 5
 #endif
@@ -1044,16 +1057,19 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #undef RT_SCAN_WAVES
 #undef RT_MED_WAVES
 #undef RT_NOSPH_WAVES
+#undef RT_GROUP_WAVES
 #undef RT_PT_WAVES
 #define RT_BVH_WAVES RT_WAVES_PER_EU
 #define RT_SCAN_WAVES RT_WAVES_PER_EU
 #define RT_MED_WAVES RT_WAVES_PER_EU
 #define RT_NOSPH_WAVES RT_WAVES_PER_EU
+#define RT_GROUP_WAVES RT_WAVES_PER_EU
 #define RT_PT_WAVES RT_WAVES_PER_EU
 #endif
-template <bool kBvh, bool kMed = false, bool kSph = true>
+template <bool kBvh, bool kMed = false, bool kSph = true, int kParts = 3>
 constexpr int render_waves() {
-    return kBvh ? RT_BVH_WAVES : (kMed ? RT_MED_WAVES : (kSph ? RT_SCAN_WAVES : RT_NOSPH_WAVES));
+    return kBvh ? (kParts == 2 ? RT_GROUP_WAVES : RT_BVH_WAVES)
+                : (kMed ? RT_MED_WAVES : (kSph ? RT_SCAN_WAVES : RT_NOSPH_WAVES));
 }
 
 // Canvas::gamma (Canvas.h:198-200) with clamp = fmaxf(a, fminf(f, b)).
@@ -1305,10 +1321,11 @@ __device__ __forceinline__ int global_row_of(const RenderLaunch& L, int lr) {
     return (lb * L.row_world + L.row_rank) * L.row_block + (lr - lb * L.row_block);
 }
 
-// kSph = false: the linear-scan variant for scenes without spheres (CornellBox1): neither the
-// sphere test nor the sphere normals are compiled in (rt_capi.cpp picks it).
-template <bool kBvh, bool kQueue, bool kMed = false, bool kSph = true>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_waves<kBvh, kMed, kSph>()))) void render_kernel(
+// kSph = false: the linear-scan variant for simple scenes (CornellBox1): planes and brute-force
+// meshes with Lambertian and emissive materials only - neither the sphere test, the sphere
+// normals nor the metal / dielectric / isotropic scatter is compiled in (rt_capi.cpp picks it).
+template <bool kBvh, bool kQueue, bool kMed = false, bool kSph = true, int kParts = 3>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_waves<kBvh, kMed, kSph, kParts>()))) void render_kernel(
     RenderLaunch L, const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
     const MatRec* __restrict__ mats, const BvhNode* __restrict__ nodes,
     const uint32_t* __restrict__ tri_orig, int n_objs, const CamRec* __restrict__ cam,
@@ -1420,7 +1437,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
 #endif
 
         const v3 inv = rcp(ray.d);
-        const Hit h = closest_hit<kBvh, kMed, kSph>(S, ray, inv, live, rng, W, stack, lane, cnt
+        const Hit h = closest_hit<kBvh, kMed, kSph, kParts>(S, ray, inv, live, rng, W, stack, lane, cnt
 #ifdef RT_STAMPS
                                         , tm
 #endif
@@ -1470,13 +1487,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                 nd = normalize(sd);
                 att = v3{m.a0, m.a1, m.a2};
                 scattered = true;
-            } else if (m.type == 1u) {
+            } else if (kSph && m.type == 1u) {
                 // Metal::scatter (Material.h:45-51).
                 v3 refl = reflect(normalize(ray.d), n);
                 nd = add(refl, scale(random_in_unit_sphere(rng), m.p0));
                 scattered = dot(nd, n) > 0.0f;
                 att = scale(v3{m.a0, m.a1, m.a2}, scattered ? 1.0f : 0.0f);
-            } else if (m.type == 2u) {
+            } else if (kSph && m.type == 2u) {
                 // Dieletric::scatter + reflectance (Material.h:65-109).
                 att = v3{1.0f, 1.0f, 1.0f};
                 const float ratio = front ? (1.0f / m.p0) : m.p0;
@@ -1495,7 +1512,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                 v3 dir = refl ? reflect(ud, n) : refract(ud, n, ratio);
                 nd = normalize(dir);
                 scattered = true;
-            } else if (m.type == 4u) {
+            } else if (kSph && m.type == 4u) {
                 // isotropic::scatter: Ray(p, randomInUnitSphere(), time), attenuation = albedo.
                 nd = random_in_unit_sphere(rng);
                 att = v3{m.a0, m.a1, m.a2};
@@ -2283,10 +2300,10 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
 
 // A persistent grid fills the resident waves: waves per SIMD x 4 SIMDs / 4-wave blocks per CU.
 int queue_blocks(int n_cu, int waves_per_simd) { return n_cu * waves_per_simd; }
-int render_queue_waves(bool bvh, bool media, bool spheres) {
-    if (bvh) return render_waves<true>();
+int render_queue_waves(bool bvh, bool media, bool full, int bvh_parts) {
+    if (bvh) return bvh_parts == 2 && RT_BVH_PARTS_VARIANT ? render_waves<true, false, true, 2>() : render_waves<true>();
     if (media && RT_MED_VARIANT) return render_waves<false, true>();
-    if (!spheres && RT_NOSPH_VARIANT) return render_waves<false, false, false>();
+    if (!full && RT_NOSPH_VARIANT) return render_waves<false, false, false>();
     return render_waves<false>();
 }
 int pathtrace_queue_waves() { return RT_PT_WAVES; }
@@ -2302,8 +2319,8 @@ uint32_t kernel_build_flags() {
     f |= 2u;  // RT_BUILD_STAMPS
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
-    !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_PT_WAVES != 5 || \
-    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE || !RT_NOSPH_VARIANT
+    !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_PT_WAVES != 5 || \
+    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE || !RT_NOSPH_VARIANT || !RT_BVH_PARTS_VARIANT
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;
@@ -2318,13 +2335,19 @@ hipError_t launch_render(const SceneArgs& sc, const CamRec* cam, const RenderLau
         const uint32_t blocks = std::min<uint32_t>((lanes_needed + kWavesPerBlock - 1) / kWavesPerBlock,
                                                    (uint32_t)L.queue);
         dim3 grid(blocks, 1);
-        if (sc.has_bvh)
+        if (sc.has_bvh && sc.bvh_parts == 1 && RT_BVH_PARTS_VARIANT)
+            hipLaunchKernelGGL((render_kernel<true, true, false, true, 1>), grid, block, stack_bytes(L), stream, L,
+                               sc.objs, sc.tris, sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
+        else if (sc.has_bvh && sc.bvh_parts == 2 && RT_BVH_PARTS_VARIANT)
+            hipLaunchKernelGGL((render_kernel<true, true, false, true, 2>), grid, block, stack_bytes(L), stream, L,
+                               sc.objs, sc.tris, sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
+        else if (sc.has_bvh)
             hipLaunchKernelGGL((render_kernel<true, true>), grid, block, stack_bytes(L), stream, L, sc.objs, sc.tris,
                                sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
         else if (sc.has_media && RT_MED_VARIANT)
             hipLaunchKernelGGL((render_kernel<false, true, true>), grid, block, 0, stream, L, sc.objs, sc.tris,
                                sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
-        else if (!sc.has_spheres && RT_NOSPH_VARIANT)
+        else if (!sc.full_scan && RT_NOSPH_VARIANT)
             hipLaunchKernelGGL((render_kernel<false, true, false, false>), grid, block, 0, stream, L, sc.objs,
                                sc.tris, sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
         else
@@ -2344,7 +2367,7 @@ hipError_t launch_render(const SceneArgs& sc, const CamRec* cam, const RenderLau
     else if (sc.has_media && RT_MED_VARIANT)
         hipLaunchKernelGGL((render_kernel<false, false, true>), grid, block, 0, stream, L, sc.objs, sc.tris, sc.mats,
                            sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
-    else if (!sc.has_spheres && RT_NOSPH_VARIANT)
+    else if (!sc.full_scan && RT_NOSPH_VARIANT)
         hipLaunchKernelGGL((render_kernel<false, false, false, false>), grid, block, 0, stream, L, sc.objs, sc.tris,
                            sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
     else

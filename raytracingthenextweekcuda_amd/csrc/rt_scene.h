@@ -105,7 +105,8 @@ struct SceneArgs {
     bool has_bvh;  // any mesh carries a BVH (selects the kernel variant)
     int32_t stack_cap = kBvhStackDepth;  // traversal stack entries per lane (the scene's BVH depth)
     bool has_media = false;  // any participating medium in the scan list (selects the kernel variant)
-    bool has_spheres = true;  // any (moving) sphere in the scan list (false selects the sphere-free variant)
+    int32_t bvh_parts = 3;   // BVH scenes: 1 = mesh BVHs only, 2 = sphere groups only, 3 = both
+    bool full_scan = true;  // spheres or non-Lambertian/emissive materials in the scan list (false: the simple-scene variant)
 };
 
 // ----------------------------------------------------------------------------
