@@ -936,7 +936,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             const bool in = (pa > f[6]) & (pa < f[7]) & (pb > f[8]) & (pb < f[9]);
             const bool ok = proceed & (t >= kTMin) & in;
             cand(ok ? t : __builtin_nanf(""), false);
-        } else if ((kSph || kBvh || kMed) && (ob.type == kObjSphere || ob.type == kObjMovingSphere)) {
+        } else if ((kSph || kMed) && (ob.type == kObjSphere || ob.type == kObjMovingSphere)) {
             cand(sphere_candidate(ob, o, d, ray.time), true);
         } else if (ob.type == kObjMesh) {
             // TriangleMesh::hit (TriangleMesh.cu:34-117): the AABB early-out
@@ -977,7 +977,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 }
 #endif
             }
-        } else if ((kMed || kBvh || !RT_MED_VARIANT) && ob.type == kObjMedium) {
+        } else if ((kMed || (kBvh && kSph) || !RT_MED_VARIANT) && ob.type == kObjMedium) {
             // (the general linear-scan kernel never sees a medium: launch_render sends scenes with
             // media to the kMed variant, so its register allocation need not cover this test)
             cand(live ? medium_candidate(ob, o, d, rng) : __builtin_nanf(""), false);
@@ -1028,7 +1028,7 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }  // namespace
 
 // Occupancy per kernel (min waves per SIMD; VGPR budget 512 / waves): the BVH rayColor
-// kernel at 4 (128 VGPRs, spill-free; its sphere-group-only variant at 5), the linear-scan
+// kernel at 4 (128 VGPRs, spill-free; its sphere-group-only and simple-scene mesh variants at 5), the linear-scan
 // rayColor kernel at 6 (89 VGPRs at 5
 // since it no longer carries the medium test; 9 spilled at 6 and still faster), its
 // sphere-free variant at 7, its media variant at 6 and the pathTrace kernel at 5 (same-box
@@ -1049,6 +1049,9 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #ifndef RT_GROUP_WAVES
 #define RT_GROUP_WAVES 5
 #endif
+#ifndef RT_BVH_SIMPLE_WAVES
+#define RT_BVH_SIMPLE_WAVES 5
+#endif
 #ifndef RT_PT_WAVES
 #define RT_PT_WAVES 5
 #endif
@@ -1058,17 +1061,19 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #undef RT_MED_WAVES
 #undef RT_NOSPH_WAVES
 #undef RT_GROUP_WAVES
+#undef RT_BVH_SIMPLE_WAVES
 #undef RT_PT_WAVES
 #define RT_BVH_WAVES RT_WAVES_PER_EU
 #define RT_SCAN_WAVES RT_WAVES_PER_EU
 #define RT_MED_WAVES RT_WAVES_PER_EU
 #define RT_NOSPH_WAVES RT_WAVES_PER_EU
 #define RT_GROUP_WAVES RT_WAVES_PER_EU
+#define RT_BVH_SIMPLE_WAVES RT_WAVES_PER_EU
 #define RT_PT_WAVES RT_WAVES_PER_EU
 #endif
 template <bool kBvh, bool kMed = false, bool kSph = true, int kParts = 3>
 constexpr int render_waves() {
-    return kBvh ? (kParts == 2 ? RT_GROUP_WAVES : RT_BVH_WAVES)
+    return kBvh ? (kParts == 2 ? RT_GROUP_WAVES : (kSph ? RT_BVH_WAVES : RT_BVH_SIMPLE_WAVES))
                 : (kMed ? RT_MED_WAVES : (kSph ? RT_SCAN_WAVES : RT_NOSPH_WAVES));
 }
 
@@ -1321,9 +1326,10 @@ __device__ __forceinline__ int global_row_of(const RenderLaunch& L, int lr) {
     return (lb * L.row_world + L.row_rank) * L.row_block + (lr - lb * L.row_block);
 }
 
-// kSph = false: the linear-scan variant for simple scenes (CornellBox1): planes and brute-force
+// kSph = false: the variant for simple scenes (CornellBox1; with kBvh the bunny box): planes and
 // meshes with Lambertian and emissive materials only - neither the sphere test, the sphere
-// normals nor the metal / dielectric / isotropic scatter is compiled in (rt_capi.cpp picks it).
+// normals, media nor the metal / dielectric / isotropic scatter is compiled in (rt_capi.cpp
+// picks it).
 template <bool kBvh, bool kQueue, bool kMed = false, bool kSph = true, int kParts = 3>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_waves<kBvh, kMed, kSph, kParts>()))) void render_kernel(
     RenderLaunch L, const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
@@ -1459,8 +1465,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             const float* f = ob.f;
             v3 p = add(ray.o, scale(ray.d, h.t));  // ray.at(t)
             v3 outward;
-            constexpr bool kAnySph = kSph || kBvh || kMed;
-            if ((kMed || kBvh || !RT_MED_VARIANT) && ob.type == kObjMedium) {
+            constexpr bool kAnySph = kSph || kMed;
+            if ((kMed || (kBvh && kSph) || !RT_MED_VARIANT) && ob.type == kObjMedium) {
                 outward = v3{1.0f, 0.0f, 0.0f};  // arbitrary; isotropic scatter ignores it
             } else if (ob.type == kObjPlane) {
                 outward = v3{f[3], f[4], f[5]};
@@ -2301,6 +2307,8 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
 // A persistent grid fills the resident waves: waves per SIMD x 4 SIMDs / 4-wave blocks per CU.
 int queue_blocks(int n_cu, int waves_per_simd) { return n_cu * waves_per_simd; }
 int render_queue_waves(bool bvh, bool media, bool full, int bvh_parts) {
+    if (bvh && bvh_parts == 1 && !full && !media && RT_BVH_PARTS_VARIANT && RT_NOSPH_VARIANT)
+        return render_waves<true, false, false, 1>();
     if (bvh) return bvh_parts == 2 && RT_BVH_PARTS_VARIANT ? render_waves<true, false, true, 2>() : render_waves<true>();
     if (media && RT_MED_VARIANT) return render_waves<false, true>();
     if (!full && RT_NOSPH_VARIANT) return render_waves<false, false, false>();
@@ -2319,7 +2327,7 @@ uint32_t kernel_build_flags() {
     f |= 2u;  // RT_BUILD_STAMPS
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
-    !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_PT_WAVES != 5 || \
+    !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || RT_PT_WAVES != 5 || \
     defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE || !RT_NOSPH_VARIANT || !RT_BVH_PARTS_VARIANT
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
@@ -2335,7 +2343,11 @@ hipError_t launch_render(const SceneArgs& sc, const CamRec* cam, const RenderLau
         const uint32_t blocks = std::min<uint32_t>((lanes_needed + kWavesPerBlock - 1) / kWavesPerBlock,
                                                    (uint32_t)L.queue);
         dim3 grid(blocks, 1);
-        if (sc.has_bvh && sc.bvh_parts == 1 && RT_BVH_PARTS_VARIANT)
+        if (sc.has_bvh && sc.bvh_parts == 1 && !sc.full_scan && !sc.has_media && RT_BVH_PARTS_VARIANT &&
+            RT_NOSPH_VARIANT)
+            hipLaunchKernelGGL((render_kernel<true, true, false, false, 1>), grid, block, stack_bytes(L), stream, L,
+                               sc.objs, sc.tris, sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
+        else if (sc.has_bvh && sc.bvh_parts == 1 && RT_BVH_PARTS_VARIANT)
             hipLaunchKernelGGL((render_kernel<true, true, false, true, 1>), grid, block, stack_bytes(L), stream, L,
                                sc.objs, sc.tris, sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
         else if (sc.has_bvh && sc.bvh_parts == 2 && RT_BVH_PARTS_VARIANT)
