@@ -384,7 +384,8 @@ def main():
                 "workload": workload,
                 "scene": SCENES[args.scene][5],
                 "width": W, "height": H, "spp": args.spp, "depth": args.depth,
-                "row_block": block, "lanes_per_pixel": int(st["lanes_per_pixel"]), "parallelism": f"row-tiles x{world} + RCCL gather" if world > 1 else "single GPU",
+                "row_block": block, "lanes_per_pixel": int(st["lanes_per_pixel"]),
+                "refill": int(st["refill"]), "queue_blocks": int(st["queue_blocks"]), "parallelism": f"row-tiles x{world} + RCCL gather" if world > 1 else "single GPU",
                 "segments_per_frame": int(segs / K),
                 "msamples_per_s": round(W * H * args.spp / (dt / K) / 1e6, 3),
             },

@@ -60,6 +60,8 @@ def test_bench_line_with_and_without_overlap():
     assert a["roofline"]["overlap"] is True and b["roofline"]["overlap"] is False
     assert a["config"]["segments_per_frame"] == b["config"]["segments_per_frame"]
     assert a["value"] > 0 and b["value"] > 0 and a["steps"] == 3
+    # the work-queue schedule the line was measured with (rt_render_stats.refill / queue_blocks)
+    assert a["config"]["refill"] in (4, 8) and a["config"]["queue_blocks"] > 0
 
 
 def test_row_sharded_frame_overlap_two_ranks_rank0(monkeypatch):
