@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RTMI_ABI_VERSION 8
+#define RTMI_ABI_VERSION 9
 
 typedef int32_t rt_status;
 enum {
@@ -71,7 +71,7 @@ typedef struct rt_render_params {
     int32_t row_rank;       /* this shard's rank */
     int32_t row_world;      /* number of shards (>= 1) */
     int32_t lanes_per_pixel;/* sub-streams that split one pixel's samples: 0 = auto,
-                               or a power of two <= 128 (<= 64 with RTMI_QUEUE=0).
+                               or a power of two <= 128 (<= 64 on the static grid).
                                Partial sums are combined in a fixed order, so
                                results are deterministic for a given value; 1 (and
                                spp) = the reference's sequential sum. */
@@ -85,8 +85,39 @@ typedef struct rt_render_params {
      * those of the full frame (camera and RNG keyed by the frame position). */
     int32_t col_begin;
     int32_t col_count;
+    /* Launch schedule: RT_SCHEDULE_AUTO (0) = the persistent work queue, or the static grid
+     * when the frame's partial sums do not fit (more than 2^32 items or 16 GB);
+     * RT_SCHEDULE_STATIC (1) = the static grid (one lane per (pixel, sub-stream), the
+     * reference's launch shape). Both compute the same partial sums: the image is
+     * bit-identical. rt_render_stats.variant reports the kernel that ran. */
+    int32_t schedule;
 } rt_render_params;
 enum { RT_RENDER_KEEP_COUNTERS = 1 };
+enum { RT_SCHEDULE_AUTO = 0, RT_SCHEDULE_STATIC = 1 };
+
+/* The megakernel instantiation a launch ran (rt_render_stats.variant). renderKernel
+ * (main.cu:160-206) is one kernel with virtual calls; this library compiles one
+ * instantiation per scene content (BVH traversal parts, media, spheres / non-Lambertian
+ * materials) and schedule, each with its own register budget. rt_kernel_variant_name
+ * gives the template tuple as rocprofv3 prints the symbol. */
+enum {
+    RT_VARIANT_NONE = 0,
+    RT_VARIANT_SCAN_QUEUE = 1,             /* render_kernel<false, true, false, true, 3>: linear scan */
+    RT_VARIANT_SCAN_MEDIA_QUEUE = 2,       /* render_kernel<false, true, true, true, 3>: + media */
+    RT_VARIANT_SCAN_SIMPLE_QUEUE = 3,      /* render_kernel<false, true, false, false, 3>: planes/meshes,
+                                              Lambertian + emission only (CornellBox1) */
+    RT_VARIANT_BVH_QUEUE = 4,              /* render_kernel<true, true, false, true, 3>: mesh BVHs + sphere groups */
+    RT_VARIANT_BVH_MESH_QUEUE = 5,         /* render_kernel<true, true, false, true, 1>: mesh BVHs */
+    RT_VARIANT_BVH_MESH_SIMPLE_QUEUE = 6,  /* render_kernel<true, true, false, false, 1>: mesh BVHs, simple scene */
+    RT_VARIANT_BVH_GROUP_QUEUE = 7,        /* render_kernel<true, true, false, true, 2>: sphere groups */
+    RT_VARIANT_SCAN_STATIC = 8,            /* render_kernel<false, false, false, true, 3> */
+    RT_VARIANT_SCAN_MEDIA_STATIC = 9,      /* render_kernel<false, false, true, true, 3> */
+    RT_VARIANT_SCAN_SIMPLE_STATIC = 10,    /* render_kernel<false, false, false, false, 3> */
+    RT_VARIANT_BVH_STATIC = 11,            /* render_kernel<true, false, false, true, 3> */
+    RT_VARIANT_PATHTRACE_QUEUE = 12,       /* pathtrace_kernel<true> */
+    RT_VARIANT_PATHTRACE_STATIC = 13,      /* pathtrace_kernel<false> */
+    RT_VARIANT_COUNT = 14
+};
 
 typedef struct rt_render_stats {
     uint64_t segments;      /* closest-hit queries traced (camera ray = 1, +1 per scatter) */
@@ -106,6 +137,8 @@ typedef struct rt_render_stats {
     uint32_t gather;        /* rt_render_multi*: RT_GATHER_RCCL or RT_GATHER_COPY (first context only) */
     uint32_t launches;      /* launches summed in these counters (RT_RENDER_KEEP_COUNTERS chains; else 1) */
     double kernel_ms_sum;   /* render-kernel time summed over those launches (one event pair each) */
+    uint32_t variant;       /* RT_VARIANT_* of the last launch */
+    uint32_t reserved;
 } rt_render_stats;
 
 #define RT_GATHER_RCCL 1 /* one ncclGather over the contexts' devices */
@@ -123,6 +156,9 @@ int32_t rt_abi_version(void);
 #define RT_BUILD_STAMPS 2u
 #define RT_BUILD_AB 4u
 uint32_t rt_build_flags(void);
+/* The symbol of RT_VARIANT_* `variant` as rocprofv3 prints it, e.g.
+ * "render_kernel<false, true, false, false, 3>"; NULL for an unknown id. */
+const char* rt_kernel_variant_name(uint32_t variant);
 /* device >= 0: HIP ordinal. device = -1: scene-building only (no GPU calls). */
 rt_status rt_create(int32_t device, rt_ctx** out);
 void rt_destroy(rt_ctx* ctx);
@@ -215,7 +251,9 @@ rt_status rt_ply_bvh_image_gpu(int32_t device, const char* path, const float off
  * newer than it (the reference's `plyFileTime > bvhFileTime` rebuild rule), for the
  * pathTrace scene (the last rt_load_object path, as main.cu:435 passes sceneFile)
  * and for rt_mesh_ply meshes (read at rt_commit). RT_BVH_CACHE_WRITE: after a build,
- * write `<ply>.bvh` (BVH.cpp:535-541). READ | WRITE is the reference's behaviour.
+ * write `<ply>.bvh` (BVH.cpp:535-541) - the pathTrace scene only, as in the reference
+ * (rt_mesh_ply meshes may be placed differently, so they read caches but never write them).
+ * READ | WRITE is the reference's behaviour.
  * Cache files are untrusted input: the header counts must match the file size and
  * the triangle count, every node index and leaf range must be in bounds, children
  * must follow their parent (DFS order), the leaves must partition the triangle list

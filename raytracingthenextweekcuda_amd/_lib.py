@@ -27,7 +27,7 @@ BVH_CACHE_OFF, BVH_CACHE_READ, BVH_CACHE_WRITE = 0, 1, 2
 GATHER_RCCL, GATHER_COPY = 1, 2
 
 # Every symbol include/rtmi.h declares (checked by tests/test_abi.py).
-ABI_VERSION = 8  # include/rtmi.h RTMI_ABI_VERSION
+ABI_VERSION = 9  # include/rtmi.h RTMI_ABI_VERSION
 
 EXPORTS = [
     "rt_abi_version", "rt_create", "rt_destroy", "rt_last_error", "rt_clear_scene",
@@ -42,8 +42,16 @@ EXPORTS = [
     "rt_render_u8", "rt_accumulate", "rt_render_multi", "rt_gamma_u8",
     "rt_build_flags", "rt_set_bvh_cache", "rt_bvh_cache_stats",
     "rt_owned_rows", "rt_max_tile_rows", "rt_render_multi_device", "rt_comm_unique_id", "rt_comm_init",
-    "rt_comm_destroy", "rt_gather_rows", "rt_assemble_rows",
+    "rt_comm_destroy", "rt_gather_rows", "rt_assemble_rows", "rt_kernel_variant_name",
 ]
+
+# rtmi.h RT_SCHEDULE_* and RT_VARIANT_* (rt_render_stats.variant)
+SCHEDULES = {"auto": 0, "static": 1}
+VARIANTS = {
+    1: "SCAN_QUEUE", 2: "SCAN_MEDIA_QUEUE", 3: "SCAN_SIMPLE_QUEUE", 4: "BVH_QUEUE", 5: "BVH_MESH_QUEUE",
+    6: "BVH_MESH_SIMPLE_QUEUE", 7: "BVH_GROUP_QUEUE", 8: "SCAN_STATIC", 9: "SCAN_MEDIA_STATIC",
+    10: "SCAN_SIMPLE_STATIC", 11: "BVH_STATIC", 12: "PATHTRACE_QUEUE", 13: "PATHTRACE_STATIC",
+}
 
 
 class RTError(RuntimeError):
@@ -58,7 +66,7 @@ class RenderParams(C.Structure):
         ("max_depth", C.c_int32), ("seed", C.c_uint32), ("sample_offset", C.c_uint32),
         ("row_block", C.c_int32), ("row_rank", C.c_int32), ("row_world", C.c_int32),
         ("lanes_per_pixel", C.c_int32), ("integrator", C.c_int32), ("flags", C.c_uint32),
-        ("col_begin", C.c_int32), ("col_count", C.c_int32),
+        ("col_begin", C.c_int32), ("col_count", C.c_int32), ("schedule", C.c_int32),
     ]
 
 
@@ -70,7 +78,7 @@ class RenderStats(C.Structure):
         ("group_sphere_tests", C.c_uint64), ("group_moving_sphere_tests", C.c_uint64),
         ("debug", C.c_uint64 * 8),
         ("refill", C.c_uint32), ("queue_blocks", C.c_uint32), ("gather", C.c_uint32), ("launches", C.c_uint32),
-        ("kernel_ms_sum", C.c_double),
+        ("kernel_ms_sum", C.c_double), ("variant", C.c_uint32), ("reserved", C.c_uint32),
     ]
 
 
@@ -146,6 +154,8 @@ def lib():
     L.rt_gamma_u8.argtypes = [fp, C.c_int64, C.POINTER(C.c_uint8)]
     L.rt_build_flags.restype = C.c_uint32
     L.rt_build_flags.argtypes = []
+    L.rt_kernel_variant_name.argtypes = [C.c_uint32]
+    L.rt_kernel_variant_name.restype = C.c_char_p
     L.rt_set_bvh_cache.argtypes = [vp, i32]
     L.rt_bvh_cache_stats.argtypes = [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]
     L.rt_owned_rows.argtypes = [i32, i32, i32, i32]
@@ -165,6 +175,12 @@ def lib():
 def build_flags() -> int:
     """rt_build_flags() of the loaded library (0 = the shipped parity build)."""
     return int(lib().rt_build_flags())
+
+
+def variant_name(variant: int) -> str | None:
+    """rt_kernel_variant_name: the kernel symbol of an RT_VARIANT_* id as rocprofv3 prints it."""
+    n = lib().rt_kernel_variant_name(int(variant))
+    return n.decode() if n else None
 
 
 def require_parity_build(what: str) -> None:

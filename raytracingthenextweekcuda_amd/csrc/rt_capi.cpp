@@ -505,6 +505,12 @@ static rt_status rt_process_triangle_data_impl(rt_ctx* c, const float offset[3],
                 c->pt_cache_writes = 1;
         }
         c->pt_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        // the traversal keeps one pending subtree per level in LDS; the reference's builder
+        // refuses trees as deep as its BVH_STACK_SIZE (BVH.cpp:469-496), and so does this one
+        // (a `.bvh` cache file is untrusted input: its depth is checked here, not assumed)
+        if (b.max_depth >= rt::kBvhStackDepth)
+            return fail(c, RT_ERR_INVALID, "pathTrace BVH depth " + std::to_string(b.max_depth) +
+                                               " exceeds the traversal stack (" + std::to_string(rt::kBvhStackDepth) + ")");
     }
     if (out_info) {
         out_info[0] = (int32_t)kt.size();
@@ -650,8 +656,9 @@ rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& 
     L.col0 = p->col_begin;
     L.cols = p->col_count ? p->col_count : p->width;
     const int32_t s = p->lanes_per_pixel;
-    const char* qenv = getenv("RTMI_QUEUE");
-    const bool queue = !(qenv && qenv[0] == '0');  // RTMI_QUEUE=0: static grid (A/B only)
+    if (p->schedule != RT_SCHEDULE_AUTO && p->schedule != RT_SCHEDULE_STATIC)
+        return fail(c, RT_ERR_INVALID, "unknown schedule");
+    const bool queue = p->schedule == RT_SCHEDULE_AUTO;
     // work-queue launches split a pixel into up to 128 sub-streams (items); the
     // static grid maps one pixel's sub-streams onto lanes of one wave (<= 64)
     if (s < 0 || s > (queue ? 128 : 64) || (s & (s - 1)) != 0)
@@ -688,10 +695,11 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
     c->launched = true;
     rt::RenderLaunch L = L0;
     // Work-queue mode (rt_kernel.h): persistent grid + partial sums, bit-identical
-    // to the static layout with the same lanes_per_pixel. RTMI_QUEUE=0 selects the
-    // static grid (A/B measurements only).
-    const char* qenv = getenv("RTMI_QUEUE");
-    if (!(qenv && qenv[0] == '0') && L.local_rows > 0) {
+    // to the static layout with the same lanes_per_pixel. RT_SCHEDULE_STATIC selects the
+    // static grid.
+    const bool pathtrace = p->integrator == RT_INTEGRATOR_PATHTRACE;
+    const bool bvh = !c->scene.nodes.empty();
+    if (p->schedule == RT_SCHEDULE_AUTO && L.local_rows > 0) {
         const uint64_t tiles = (uint64_t)L.tiles_x * (uint64_t)((L.local_rows + 7) / 8);
         const uint64_t items = tiles * 64u * (uint64_t)L.lanes_per_pixel;
         const size_t bytes = (size_t)items * 3 * sizeof(float);
@@ -710,9 +718,8 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
             }
         }
         if (have) {
-            const int waves = p->integrator == RT_INTEGRATOR_PATHTRACE
-                                  ? rt::pathtrace_queue_waves()
-                                  : rt::render_queue_waves(!c->scene.nodes.empty(), c->has_media, c->full_scan, c->bvh_parts);
+            const int waves =
+                rt::variant_waves(rt::select_variant(pathtrace, true, bvh, c->has_media, c->full_scan, c->bvh_parts));
             L.queue = rt::queue_blocks(c->n_cu, waves);
             L.n_items = (uint32_t)items;
             L.n_pix = (uint32_t)(items >> L.sp_log2);
@@ -728,6 +735,7 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
             RT_HIP(c, hipMemsetAsync(c->d_queue, 0, rt::kQueueHeadWords * sizeof(uint32_t), st));
         }
     }
+    const uint32_t variant = rt::select_variant(pathtrace, L.queue != 0, bvh, c->has_media, c->full_scan, c->bvh_parts);
     if (L.queue == 0 && L.lanes_per_pixel > 64)  // the static grid keeps a pixel's sub-streams in one wave
         return fail(c, RT_ERR_INVALID, "lanes_per_pixel > 64 needs the work queue, which this frame does not fit");
     const bool keep = (p->flags & RT_RENDER_KEEP_COUNTERS) != 0;
@@ -773,7 +781,7 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
         sc.has_media = c->has_media;
         sc.full_scan = c->full_scan;
         sc.bvh_parts = c->bvh_parts;
-        RT_HIP(c, rt::launch_render(sc, c->d_cam, L, out, c->d_counters, st, k1));
+        RT_HIP(c, rt::launch_render(variant, sc, c->d_cam, L, out, c->d_counters, st, k1));
     }
     RT_HIP(c, hipEventRecord(c->ev1, st));
     const uint64_t prev_samples = keep ? c->last.samples : 0;
@@ -782,6 +790,7 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
     c->last.lanes_per_pixel = (uint32_t)L.lanes_per_pixel;
     c->last.refill = L.queue ? (uint32_t)L.refill : 0u;
     c->last.queue_blocks = (uint32_t)L.queue;
+    c->last.variant = variant;
     c->stats_pending = true;
     return RT_OK;
 }

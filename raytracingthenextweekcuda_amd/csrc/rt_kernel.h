@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "../../include/rtmi.h"
 #include "rt_scene.h"
 
 namespace rt {
@@ -135,13 +136,17 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
                             float* out, unsigned long long* counters, hipStream_t stream,
                             hipEvent_t main_done);
 
-// Workgroups of the persistent work-queue grid (n_cu x resident 4-wave blocks per CU),
-// and the occupancy each kernel is compiled for (waves per SIMD).
+// Workgroups of the persistent work-queue grid (n_cu x resident 4-wave blocks per CU).
 int queue_blocks(int n_cu, int waves_per_simd);
-int render_queue_waves(bool bvh, bool media, bool full, int bvh_parts);
-int pathtrace_queue_waves();
+// The kernel instantiation of a launch (rtmi.h RT_VARIANT_*) from the integrator, the
+// schedule and the committed scene's content; the occupancy it is compiled for (waves per
+// SIMD); its symbol as rocprofv3 prints it (nullptr for an unknown id).
+uint32_t select_variant(bool pathtrace, bool queue, bool bvh, bool media, bool full, int bvh_parts);
+int variant_waves(uint32_t variant);
+const char* variant_name(uint32_t variant);
 
-hipError_t launch_render(const SceneArgs& sc, const CamRec* cam, const RenderLaunch& L,
+// `variant` = select_variant(false, L.queue != 0, ...) of the committed scene.
+hipError_t launch_render(uint32_t variant, const SceneArgs& sc, const CamRec* cam, const RenderLaunch& L,
                          float* out, unsigned long long* counters, hipStream_t stream, hipEvent_t main_done);
 
 // Frame assembly on the gather root (rt_rows.hip): staging = world tiles of

@@ -46,7 +46,6 @@ namespace {
 
 constexpr float kInf = __builtin_huge_valf();
 constexpr int kWavesPerBlock = 4;
-constexpr int kStackDepth = kBvhStackDepth;
 
 struct Ray {
     v3 o, d;
@@ -301,7 +300,7 @@ __device__ __forceinline__ int lane_rank(uint64_t mask) {
 // lanes of the wave (uniform control flow); `want` = this lane's ray hit the
 // mesh box. The result equals the reference's sequential scan: the smallest t
 // below the caller's closestSoFar, ties resolved to the lowest triangle index.
-__device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, uint32_t base,
+[[maybe_unused]] __device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, uint32_t base,
                                              uint32_t m, uint32_t mesh_magic, bool want, v3 o, v3 d, Hit& h, int32_t obj,
                                              uint32_t order, WaveLds& W, int lane) {
     const uint64_t mask = __ballot(want);
@@ -1171,12 +1170,13 @@ __device__ __forceinline__ uint32_t queue_take(const RenderLaunch& L, int sh, ui
 // Refill of a wave's idle lanes (wave-uniform: called by all 64 lanes). A lane
 // that wants work and gets an item calls start(item); `exhausted` is set once
 // every shard ran dry.
-template <typename Start>
+template <typename Start, typename Flush>
 __device__ __forceinline__ void queue_refill(const RenderLaunch& L, int lane, bool alive, bool& exhausted,
-                                             int& shard, int& tried, Start&& start) {
+                                             int& shard, int& tried, Start&& start, Flush&& flush) {
     const bool want = !alive && !exhausted;
     const uint64_t need = __ballot(want);
     if (need && (__popcll(need) >= RT_REFILL_AT(L) || __ballot(alive) == 0)) {
+        flush();
         const uint32_t it = queue_take(L, shard, need, lane);
         if (__ballot(want && it == ~0u)) {  // this shard ran dry: move on
             ++tried;
@@ -1409,6 +1409,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                 // a sub-stream with no samples (S > spp) still owns its partial-sum slot
                 if (!alive) store_partial(L, item, sum);
                 need_cam = true;
+            }, [&]() {
+                // the wave-uniform event counts are 32-bit: at a dequeue, flush them to the 64-bit
+                // device counters before they can wrap (a brute-force mesh adds up to 64 x its
+                // triangles per trip)
+                if ((cnt.segs | cnt.box_tests | cnt.tri_wave) >= 0x40000000u) {
+                    if (lane == 0) {
+                        atomicAdd(&counters[0], (unsigned long long)cnt.segs);
+                        atomicAdd(&counters[1], (unsigned long long)cnt.tri_wave);
+                        atomicAdd(&counters[2], (unsigned long long)cnt.box_tests);
+                    }
+                    cnt.segs = cnt.box_tests = cnt.tri_wave = 0;
+                }
             });
         }
 #if RT_TAIL_STEAL
@@ -2065,7 +2077,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
                 // a sub-stream with no samples (S > spp) still owns its partial-sum slot
                 if (!alive) store_partial(L, item, sum);
                 need_cam = true;
-            });
+            }, []() {});
         }
         if (__ballot(alive || (kQueue && !exhausted)) == 0) break;
         if (alive && need_cam) {
@@ -2306,15 +2318,63 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
 
 // A persistent grid fills the resident waves: waves per SIMD x 4 SIMDs / 4-wave blocks per CU.
 int queue_blocks(int n_cu, int waves_per_simd) { return n_cu * waves_per_simd; }
-int render_queue_waves(bool bvh, bool media, bool full, int bvh_parts) {
+
+// The instantiation a launch runs (rtmi.h RT_VARIANT_*). This is the only place that maps
+// scene content + schedule to a kernel: launch_render / launch_pathtrace dispatch on the id,
+// the queue grid is sized with variant_waves(id), and rt_render_stats.variant reports it.
+uint32_t select_variant(bool pathtrace, bool queue, bool bvh, bool media, bool full, int bvh_parts) {
+    if (pathtrace) return queue ? RT_VARIANT_PATHTRACE_QUEUE : RT_VARIANT_PATHTRACE_STATIC;
+    if (!queue) {
+        if (bvh) return RT_VARIANT_BVH_STATIC;
+        if (media && RT_MED_VARIANT) return RT_VARIANT_SCAN_MEDIA_STATIC;
+        if (!full && RT_NOSPH_VARIANT) return RT_VARIANT_SCAN_SIMPLE_STATIC;
+        return RT_VARIANT_SCAN_STATIC;
+    }
     if (bvh && bvh_parts == 1 && !full && !media && RT_BVH_PARTS_VARIANT && RT_NOSPH_VARIANT)
-        return render_waves<true, false, false, 1>();
-    if (bvh) return bvh_parts == 2 && RT_BVH_PARTS_VARIANT ? render_waves<true, false, true, 2>() : render_waves<true>();
-    if (media && RT_MED_VARIANT) return render_waves<false, true>();
-    if (!full && RT_NOSPH_VARIANT) return render_waves<false, false, false>();
-    return render_waves<false>();
+        return RT_VARIANT_BVH_MESH_SIMPLE_QUEUE;
+    if (bvh && bvh_parts == 1 && RT_BVH_PARTS_VARIANT) return RT_VARIANT_BVH_MESH_QUEUE;
+    if (bvh && bvh_parts == 2 && RT_BVH_PARTS_VARIANT) return RT_VARIANT_BVH_GROUP_QUEUE;
+    if (bvh) return RT_VARIANT_BVH_QUEUE;
+    if (media && RT_MED_VARIANT) return RT_VARIANT_SCAN_MEDIA_QUEUE;
+    if (!full && RT_NOSPH_VARIANT) return RT_VARIANT_SCAN_SIMPLE_QUEUE;
+    return RT_VARIANT_SCAN_QUEUE;
 }
-int pathtrace_queue_waves() { return RT_PT_WAVES; }
+
+// Occupancy each instantiation is compiled for (waves per SIMD).
+int variant_waves(uint32_t v) {
+    switch (v) {
+        case RT_VARIANT_SCAN_QUEUE: case RT_VARIANT_SCAN_STATIC: return render_waves<false>();
+        case RT_VARIANT_SCAN_MEDIA_QUEUE: case RT_VARIANT_SCAN_MEDIA_STATIC: return render_waves<false, true>();
+        case RT_VARIANT_SCAN_SIMPLE_QUEUE: case RT_VARIANT_SCAN_SIMPLE_STATIC: return render_waves<false, false, false>();
+        case RT_VARIANT_BVH_QUEUE: case RT_VARIANT_BVH_STATIC: return render_waves<true>();
+        case RT_VARIANT_BVH_MESH_QUEUE: return render_waves<true, false, true, 1>();
+        case RT_VARIANT_BVH_MESH_SIMPLE_QUEUE: return render_waves<true, false, false, 1>();
+        case RT_VARIANT_BVH_GROUP_QUEUE: return render_waves<true, false, true, 2>();
+        case RT_VARIANT_PATHTRACE_QUEUE: case RT_VARIANT_PATHTRACE_STATIC: return RT_PT_WAVES;
+        default: return 4;
+    }
+}
+
+// The instantiation's symbol as rocprofv3 prints it (template arguments spelled out, the
+// defaults included), so a profile can be matched to the variant a launch reported.
+const char* variant_name(uint32_t v) {
+    switch (v) {
+        case RT_VARIANT_SCAN_QUEUE: return "render_kernel<false, true, false, true, 3>";
+        case RT_VARIANT_SCAN_MEDIA_QUEUE: return "render_kernel<false, true, true, true, 3>";
+        case RT_VARIANT_SCAN_SIMPLE_QUEUE: return "render_kernel<false, true, false, false, 3>";
+        case RT_VARIANT_BVH_QUEUE: return "render_kernel<true, true, false, true, 3>";
+        case RT_VARIANT_BVH_MESH_QUEUE: return "render_kernel<true, true, false, true, 1>";
+        case RT_VARIANT_BVH_MESH_SIMPLE_QUEUE: return "render_kernel<true, true, false, false, 1>";
+        case RT_VARIANT_BVH_GROUP_QUEUE: return "render_kernel<true, true, false, true, 2>";
+        case RT_VARIANT_SCAN_STATIC: return "render_kernel<false, false, false, true, 3>";
+        case RT_VARIANT_SCAN_MEDIA_STATIC: return "render_kernel<false, false, true, true, 3>";
+        case RT_VARIANT_SCAN_SIMPLE_STATIC: return "render_kernel<false, false, false, false, 3>";
+        case RT_VARIANT_BVH_STATIC: return "render_kernel<true, false, false, true, 3>";
+        case RT_VARIANT_PATHTRACE_QUEUE: return "pathtrace_kernel<true>";
+        case RT_VARIANT_PATHTRACE_STATIC: return "pathtrace_kernel<false>";
+        default: return nullptr;
+    }
+}
 
 // rtmi.h RT_BUILD_*: which non-shipped options this translation unit (and, through
 // the shared EXTRA flags, the whole library) was compiled with.
@@ -2334,58 +2394,61 @@ uint32_t kernel_build_flags() {
     return f;
 }
 
-hipError_t launch_render(const SceneArgs& sc, const CamRec* cam, const RenderLaunch& L, float* out,
+namespace {
+template <bool kBvh, bool kQueue, bool kMed = false, bool kSph = true, int kParts = 3>
+void launch_rk(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const RenderLaunch& L, const SceneArgs& sc,
+               const CamRec* cam, float* out, unsigned long long* counters) {
+    hipLaunchKernelGGL((render_kernel<kBvh, kQueue, kMed, kSph, kParts>), grid, block, kBvh ? lds : 0, stream, L,
+                       sc.objs, sc.tris, sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
+}
+}  // namespace
+
+hipError_t launch_render(uint32_t variant, const SceneArgs& sc, const CamRec* cam, const RenderLaunch& L, float* out,
                          unsigned long long* counters, hipStream_t stream, hipEvent_t main_done) {
-    dim3 block(64 * kWavesPerBlock);
+    const dim3 block(64 * kWavesPerBlock);
+    const size_t lds = stack_bytes(L);
+    dim3 grid;
     if (L.queue) {
         if (L.n_items == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
-        const uint32_t lanes_needed = (L.n_items + 63u) / 64u;  // waves
-        const uint32_t blocks = std::min<uint32_t>((lanes_needed + kWavesPerBlock - 1) / kWavesPerBlock,
-                                                   (uint32_t)L.queue);
-        dim3 grid(blocks, 1);
-        if (sc.has_bvh && sc.bvh_parts == 1 && !sc.full_scan && !sc.has_media && RT_BVH_PARTS_VARIANT &&
-            RT_NOSPH_VARIANT)
-            hipLaunchKernelGGL((render_kernel<true, true, false, false, 1>), grid, block, stack_bytes(L), stream, L,
-                               sc.objs, sc.tris, sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
-        else if (sc.has_bvh && sc.bvh_parts == 1 && RT_BVH_PARTS_VARIANT)
-            hipLaunchKernelGGL((render_kernel<true, true, false, true, 1>), grid, block, stack_bytes(L), stream, L,
-                               sc.objs, sc.tris, sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
-        else if (sc.has_bvh && sc.bvh_parts == 2 && RT_BVH_PARTS_VARIANT)
-            hipLaunchKernelGGL((render_kernel<true, true, false, true, 2>), grid, block, stack_bytes(L), stream, L,
-                               sc.objs, sc.tris, sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
-        else if (sc.has_bvh)
-            hipLaunchKernelGGL((render_kernel<true, true>), grid, block, stack_bytes(L), stream, L, sc.objs, sc.tris,
-                               sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
-        else if (sc.has_media && RT_MED_VARIANT)
-            hipLaunchKernelGGL((render_kernel<false, true, true>), grid, block, 0, stream, L, sc.objs, sc.tris,
-                               sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
-        else if (!sc.full_scan && RT_NOSPH_VARIANT)
-            hipLaunchKernelGGL((render_kernel<false, true, false, false>), grid, block, 0, stream, L, sc.objs,
-                               sc.tris, sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
-        else
-            hipLaunchKernelGGL((render_kernel<false, true>), grid, block, 0, stream, L, sc.objs, sc.tris,
-                               sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
-        if (main_done) (void)hipEventRecord(main_done, stream);
+        const uint32_t waves_needed = (L.n_items + 63u) / 64u;
+        grid = dim3(std::min<uint32_t>((waves_needed + kWavesPerBlock - 1) / kWavesPerBlock, (uint32_t)L.queue), 1);
+    } else {
+        grid = dim3((L.cols + 2 * L.tile_w - 1) / (2 * L.tile_w), (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
+        if (grid.x == 0 || grid.y == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
+    }
+    switch (variant) {
+        case RT_VARIANT_BVH_MESH_SIMPLE_QUEUE:
+            launch_rk<true, true, false, false, 1>(grid, block, lds, stream, L, sc, cam, out, counters);
+            break;
+        case RT_VARIANT_BVH_MESH_QUEUE:
+            launch_rk<true, true, false, true, 1>(grid, block, lds, stream, L, sc, cam, out, counters);
+            break;
+        case RT_VARIANT_BVH_GROUP_QUEUE:
+            launch_rk<true, true, false, true, 2>(grid, block, lds, stream, L, sc, cam, out, counters);
+            break;
+        case RT_VARIANT_BVH_QUEUE: launch_rk<true, true>(grid, block, lds, stream, L, sc, cam, out, counters); break;
+        case RT_VARIANT_SCAN_MEDIA_QUEUE:
+            launch_rk<false, true, true>(grid, block, lds, stream, L, sc, cam, out, counters);
+            break;
+        case RT_VARIANT_SCAN_SIMPLE_QUEUE:
+            launch_rk<false, true, false, false>(grid, block, lds, stream, L, sc, cam, out, counters);
+            break;
+        case RT_VARIANT_SCAN_QUEUE: launch_rk<false, true>(grid, block, lds, stream, L, sc, cam, out, counters); break;
+        case RT_VARIANT_BVH_STATIC: launch_rk<true, false>(grid, block, lds, stream, L, sc, cam, out, counters); break;
+        case RT_VARIANT_SCAN_MEDIA_STATIC:
+            launch_rk<false, false, true>(grid, block, lds, stream, L, sc, cam, out, counters);
+            break;
+        case RT_VARIANT_SCAN_SIMPLE_STATIC:
+            launch_rk<false, false, false, false>(grid, block, lds, stream, L, sc, cam, out, counters);
+            break;
+        case RT_VARIANT_SCAN_STATIC: launch_rk<false, false>(grid, block, lds, stream, L, sc, cam, out, counters); break;
+        default: return hipErrorInvalidValue;
+    }
+    if (main_done) (void)hipEventRecord(main_done, stream);
+    if (L.queue) {
         const uint32_t pixels = L.n_items / (uint32_t)L.lanes_per_pixel;
         hipLaunchKernelGGL(combine_kernel, dim3((pixels + 255u) / 256u), dim3(256), 0, stream, L, out);
-        return hipGetLastError();
     }
-    dim3 grid((L.cols + 2 * L.tile_w - 1) / (2 * L.tile_w),
-              (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
-    if (grid.x == 0 || grid.y == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
-    if (sc.has_bvh)
-        hipLaunchKernelGGL((render_kernel<true, false>), grid, block, stack_bytes(L), stream, L, sc.objs, sc.tris, sc.mats,
-                           sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
-    else if (sc.has_media && RT_MED_VARIANT)
-        hipLaunchKernelGGL((render_kernel<false, false, true>), grid, block, 0, stream, L, sc.objs, sc.tris, sc.mats,
-                           sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
-    else if (!sc.full_scan && RT_NOSPH_VARIANT)
-        hipLaunchKernelGGL((render_kernel<false, false, false, false>), grid, block, 0, stream, L, sc.objs, sc.tris,
-                           sc.mats, sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
-    else
-        hipLaunchKernelGGL((render_kernel<false, false>), grid, block, 0, stream, L, sc.objs, sc.tris, sc.mats,
-                           sc.nodes, sc.tri_orig, sc.n_objs, cam, out, counters);
-    if (main_done) (void)hipEventRecord(main_done, stream);
     return hipGetLastError();
 }
 

@@ -297,5 +297,6 @@ rt_status rt_assemble_rows(rt_ctx* c, const rt_render_params* p, int32_t world, 
 }
 
 uint32_t rt_build_flags(void) { return rt::kernel_build_flags(); }
+const char* rt_kernel_variant_name(uint32_t variant) { return rt::variant_name(variant); }
 
 }  // extern "C"

@@ -256,7 +256,11 @@ void HostScene::build_bvh(const std::vector<v3>& vs, const std::vector<uint32_t>
     if (got <= 0) {
         if (bvh_gpu && gpu_build_cf_bvh(bvh_device, vs, ix, b, 4, nullptr).empty()) ++bvh_gpu_builds;
         else build_cf_bvh(vs, ix, b);
-        if (!cache_ply.empty() && (bvh_cache_mode & 2) && write_bvh_cache(cache_ply, b)) ++cache_writes;
+        // rt_mesh_ply meshes read caches but never write them: a mesh placed with another
+        // offset / maxCoord than the pathTrace scene's would overwrite that scene's cache (and
+        // the two would keep rebuilding and replacing each other's file). The reference writes
+        // `<ply>.bvh` from UpdateBoundingVolumeHierarchy only, i.e. the pathTrace scene
+        // (rt_process_triangle_data).
     }
     bvh_build_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }

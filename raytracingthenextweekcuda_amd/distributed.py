@@ -158,9 +158,16 @@ class RowShardedFrame:
         self.pending = (work, b)
 
     def drain(self) -> Optional["object"]:
-        """Complete the last submitted frame; returns it on rank 0 (None elsewhere)."""
+        """Complete the last submitted frame; returns it on rank 0 (None elsewhere).
+
+        With frame overlap the frame was rendered (world 1) or assembled (rank 0) on
+        streams[b]: the caller's current stream is made to wait for that stream, so work the
+        caller enqueues on it reads the finished frame. The frame buffer is reused by the
+        second-next submit()."""
         if self.pending is not None:
             self._finish_pending()
+        if self.streams and self.n_submitted:
+            self.torch.cuda.current_stream().wait_stream(self.streams[(self.n_submitted - 1) % 2])
         return self.frame if self.rank == 0 else None
 
 

@@ -22,7 +22,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import RT_OK, RenderParams, RenderStats, RTError, lib
+from ._lib import RT_OK, SCHEDULES, RenderParams, RenderStats, RTError, lib, variant_name
 
 _f3 = C.c_float * 3
 
@@ -256,14 +256,17 @@ class Renderer:
     @staticmethod
     def params(width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,
                row_rank=0, row_world=1, lanes_per_pixel=1, integrator="rayColor",
-               keep_counters=False, col_begin=0, col_count=0) -> RenderParams:
+               keep_counters=False, col_begin=0, col_count=0, schedule="auto") -> RenderParams:
+        """rt_render_params; schedule "auto" = the persistent work queue (the static grid when
+        the frame's partial sums do not fit), "static" = the static grid (same image)."""
         return RenderParams(width, height, spp, max_depth, seed, sample_offset, row_block,
                             row_rank, row_world, lanes_per_pixel, _integrator(integrator),
-                            KEEP_COUNTERS if keep_counters else 0, col_begin, col_count)
+                            KEEP_COUNTERS if keep_counters else 0, col_begin, col_count,
+                            SCHEDULES[schedule])
 
     def render(self, width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,
                row_rank=0, row_world=1, lanes_per_pixel=1, integrator="rayColor",
-               col_begin=0, col_count=0) -> np.ndarray:
+               col_begin=0, col_count=0, schedule="auto") -> np.ndarray:
         """Mean radiance of the owned rows, shape (rows, width, 3), y = 0 bottom.
         lanes_per_pixel=1 keeps the reference's sequential per-pixel sample sum;
         0 lets the library pick a lane layout that fills the GPU. integrator
@@ -272,7 +275,7 @@ class Renderer:
         col_count > 0 renders only columns [col_begin, col_begin + col_count) of the
         frame's rows (shape (rows, col_count, 3)); the pixels are the full frame's."""
         p = self.params(width, height, spp, max_depth, seed, sample_offset, row_block, row_rank,
-                        row_world, lanes_per_pixel, integrator, False, col_begin, col_count)
+                        row_world, lanes_per_pixel, integrator, False, col_begin, col_count, schedule)
         rows = owned_rows(height, row_block, row_rank, row_world)
         out = np.zeros((rows, col_count or width, 3), np.float32)
         self._check(self.L.rt_render(self.ctx, C.byref(p), out.ctypes.data_as(C.POINTER(C.c_float))))
@@ -314,8 +317,9 @@ class Renderer:
     def stats(self) -> dict:
         s = RenderStats()
         self._check(self.L.rt_sync_stats(self.ctx, C.byref(s)))
-        d = {k: getattr(s, k) for k, _ in RenderStats._fields_}
+        d = {k: getattr(s, k) for k, _ in RenderStats._fields_ if k != "reserved"}
         d["debug"] = list(s.debug)
+        d["variant_name"] = variant_name(s.variant)  # the kernel symbol, as rocprofv3 prints it
         return d
 
 

@@ -167,3 +167,45 @@ def test_gpu_frames_equal_with_and_without_the_cache(tmp_path):
             frames.append(r.render(64, 64, 4, 5, integrator="pathTrace", lanes_per_pixel=0))
             assert r.bvh_cache_stats()["reads"] == (1 if mode else 0)
     assert np.array_equal(frames[0], frames[1])
+
+
+def _chain_bvh(n_tris):
+    """A structurally valid `.bvh` image whose tree is a chain: inner node k has a one-triangle
+    leaf on the left and the rest of the chain on the right, so its depth is n_tris - 1."""
+    big = 1e30
+    box = struct.pack("<6f", -big, -big, -big, big, big, big)
+    nodes = []
+    for k in range(n_tris - 1):
+        me = 2 * k
+        nodes.append(box + struct.pack("<II", me + 1, me + 2))  # inner: left leaf, right chain
+        nodes.append(box + struct.pack("<II", 0x80000001, k))    # leaf: triangle list entry k
+    nodes.append(box + struct.pack("<II", 0x80000001, n_tris - 1))
+    return struct.pack("<II", len(nodes), n_tris) + b"".join(nodes) + struct.pack(f"<{n_tris}i", *range(n_tris))
+
+
+@pytest.mark.parametrize("n_tris,ok", [(32, True), (33, False), (40, False)])
+def test_deep_cache_is_refused_not_launched(tmp_path, n_tris, ok):
+    # the traversal keeps one pending subtree per tree level (LDS stacks sized by the depth):
+    # like the reference's builder (BVH.cpp:469-496), a tree at least BVH_STACK_SIZE (32) deep is
+    # refused with a clear error at process_triangle_data, here for a deep but valid cache file
+    ply = tmp_path / "chain.ply"
+    lines = ["ply", "format ascii 1.0", f"element vertex {3 * n_tris}", "property float x",
+             "property float y", "property float z", f"element face {n_tris}",
+             "property list uchar int vertex_indices", "end_header"]
+    lines += [f"{k * 0.1} {y} 0" for k in range(n_tris) for y in (0.0, 1.0, 2.0)]
+    lines += [f"3 {3 * k} {3 * k + 1} {3 * k + 2}" for k in range(n_tris)]
+    ply.write_text("\n".join(lines) + "\n")
+    cache = str(ply) + ".bvh"
+    with open(cache, "wb") as fh:
+        fh.write(_chain_bvh(n_tris))
+    t = os.stat(ply).st_mtime
+    os.utime(cache, (t + 10, t + 10))
+    r = rtmi.Renderer(-1)
+    r.set_bvh_cache(rtmi.BVH_CACHE_READ)
+    r.load_object(str(ply), "DIFFUSE")
+    if ok:
+        info = r.process_triangle_data()
+        assert info["depth"] == n_tris - 1 and r.bvh_cache_stats()["reads"] == 1
+    else:
+        with pytest.raises(rtmi.RTError, match="exceeds the traversal stack"):
+            r.process_triangle_data()

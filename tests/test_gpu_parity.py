@@ -352,22 +352,21 @@ def test_realtime_accumulation_matches_per_frame_sums():
 @pytest.mark.parametrize("scene", ["cornellbox1", "random_spheres", "materialball"])
 def test_work_queue_and_static_grid_agree(rtmi, scene):
     # the persistent work-queue launch (default) and the static grid
-    # (RTMI_QUEUE=0) compute the same partial sums per (pixel, sub-stream)
+    # (RT_SCHEDULE_STATIC) compute the same partial sums per (pixel, sub-stream)
     w, h, spp, lanes = 40, 24, 8, 4
-    imgs = []
-    for mode in ("1", "0"):
-        os.environ["RTMI_QUEUE"] = mode
-        try:
-            with rtmi.Renderer(0) as r:
-                if scene == "materialball":
-                    rtmi.materialball(r, w, h)
-                    imgs.append(r.render(w, h, spp, 5, lanes_per_pixel=lanes, integrator="pathTrace"))
-                else:
-                    getattr(rtmi, scene if scene != "cornellbox1" else "cornell_box1")(r, w, h)
-                    imgs.append(r.render(w, h, spp, 6, lanes_per_pixel=lanes, row_block=4, row_rank=1,
-                                         row_world=3))
-        finally:
-            del os.environ["RTMI_QUEUE"]
+    imgs, variants = [], []
+    for schedule in ("auto", "static"):
+        with rtmi.Renderer(0) as r:
+            if scene == "materialball":
+                rtmi.materialball(r, w, h)
+                imgs.append(r.render(w, h, spp, 5, lanes_per_pixel=lanes, integrator="pathTrace",
+                                     schedule=schedule))
+            else:
+                getattr(rtmi, scene if scene != "cornellbox1" else "cornell_box1")(r, w, h)
+                imgs.append(r.render(w, h, spp, 6, lanes_per_pixel=lanes, row_block=4, row_rank=1,
+                                     row_world=3, schedule=schedule))
+            variants.append(r.stats()["variant_name"])
+    assert "<" in variants[0] and variants[0] != variants[1], variants
     assert np.array_equal(imgs[0], imgs[1])
 
 
@@ -427,26 +426,26 @@ def test_tail_stealing_keeps_the_fold_order(rtmi, spp, lanes, row_world):
     assert st["samples"] == len(rows) * w * spp
 
 
-@pytest.mark.parametrize("queue", ["1", "0"])
-def test_column_window_equals_full_frame_pixels(monkeypatch, queue):
+@pytest.mark.parametrize("schedule", ["auto", "static"])
+def test_column_window_equals_full_frame_pixels(schedule):
     """rt_render_params.col_begin / col_count: a window of the owned rows, bit-identical to
     the full frame's pixels (work queue and static grid; rayColor with a BVH mesh scene and
     pathTrace), with the samples counted for the window only."""
     import raytracingthenextweekcuda_amd as rtmi
 
-    monkeypatch.setenv("RTMI_QUEUE", queue)
     W, H = 70, 33
     with rtmi.Renderer(0) as r:
         rtmi.bunny_cornell_box(r, W, H)
-        full = r.render(W, H, 4, 6, lanes_per_pixel=4)
+        full = r.render(W, H, 4, 6, lanes_per_pixel=4, schedule=schedule)
         win = r.render(W, H, 4, 6, lanes_per_pixel=4, row_block=3, row_rank=1, row_world=2,
-                       col_begin=9, col_count=45)
+                       col_begin=9, col_count=45, schedule=schedule)
         assert r.stats()["samples"] == rtmi.owned_rows(H, 3, 1, 2) * 45 * 4
         assert np.array_equal(win, full[rtmi.owned_row_ids(H, 3, 1, 2), 9:54])
     with rtmi.Renderer(0) as r:
         rtmi.materialball(r, W, H)
-        full = r.render(W, H, 2, 5, lanes_per_pixel=2, integrator="pathTrace")
-        win = r.render(W, H, 2, 5, lanes_per_pixel=2, integrator="pathTrace", col_begin=61, col_count=9)
+        full = r.render(W, H, 2, 5, lanes_per_pixel=2, integrator="pathTrace", schedule=schedule)
+        win = r.render(W, H, 2, 5, lanes_per_pixel=2, integrator="pathTrace", col_begin=61, col_count=9,
+                       schedule=schedule)
         assert np.array_equal(win, full[:, 61:70])
         with pytest.raises(rtmi.RTError):
             r.render(W, H, 2, 5, col_begin=62, col_count=9)  # past the right edge
