@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true",
                     help="one context and stream: consecutive frames do not overlap (per-launch roofline)")
     ap.add_argument("--cpu-spp", type=int, default=None)
+    ap.add_argument("--line-selftest", action="store_true",
+                    help="CPU only: synthetic per-rank numbers through the N > 1 collectives and the JSON line")
     a = ap.parse_args()
     _, w, h, spp, depth, _ = SCENES[a.scene]
     a.width = a.width or w
@@ -205,38 +207,52 @@ def load_valu_profile(workload: str):
 
 
 def load_pmc_traffic(workload: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any (the entry)."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     with open(path) as fh:
         d = json.load(fh)
-    ent = d.get(workload)
-    return None if ent is None else float(ent["hbm_bytes_per_launch"])
+    return d.get(workload)
 
 
-def main():
-    args = parse()
+KERNEL_SOURCES = ("rt_kernel.hip", "rt_kernel.h", "rt_math.h", "rt_scene.h", "rt_bvh.h")
+
+
+def kernel_source_sha() -> str:
+    """sha256 of the megakernel's sources (csrc/): a VALU or traffic profile recorded with
+    the same digest (tools/valu_summary.py, tools/pmc_summary.py) was taken of this code."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(REPO, "raytracingthenextweekcuda_amd", "csrc", f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
+def profile_check(ent, variant_name: str, sha: str):
+    """None if a committed profile entry was taken of the timed kernel (same symbol and the
+    same kernel sources), else the reason it was not."""
+    if ent is None:
+        return "no profile for this workload"
+    k = ent.get("kernel") or ""
+    if variant_name and variant_name not in k:
+        return f"profiled kernel {k!r} is not the launched {variant_name!r}"
+    if ent.get("kernel_source_sha") != sha:
+        return f"profiled kernel sources {ent.get('kernel_source_sha')} != this tree's {sha}"
+    return None
+
+
+N_ISOLATED = 3
+
+
+def measure(args, world, rank, local, rehearsal):
+    """One rank's timed frames on its GPU, then N_ISOLATED isolated frames (one launch at a
+    time, no overlap: kernel latency, gather time, frame latency). Returns per-rank numbers."""
     import numpy as np
     import torch
     import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    # RTMI_REHEARSAL=1 (testing only): N ranks share GPU 0 and gather over gloo
-    # through host memory, to exercise the N > 1 code path on a one-GPU box.
-    rehearsal = os.environ.get("RTMI_REHEARSAL") == "1"
-    if rehearsal:
-        local = 0
-    torch.cuda.set_device(local)
-    if world > 1:
-        if rehearsal:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import raytracingthenextweekcuda_amd as rtmi
     from raytracingthenextweekcuda_amd import _lib
@@ -317,113 +333,255 @@ def main():
         st[k] = sum(x[k] for x in sts)
     launch_ms = [a.elapsed_time(b) for a, b in ev]  # render kernel + the work queue's combine pass
     assert st["launches"] == args.steps, st["launches"]
-    kern_ms = [st["kernel_ms_sum"] / st["launches"]]  # the megakernel alone (the library's event pairs)
-    segs, tri_tests, box_tests, nodes = st["segments"], st["tri_tests"], st["box_tests"], st["node_visits"]
-    grp = st["group_sphere_tests"] * BYTES["sphere"] + st["group_moving_sphere_tests"] * BYTES["moving_sphere"]
 
-    # max time over ranks, totals over ranks
-    agg = torch.tensor([dt, float(segs), float(tri_tests), float(box_tests), float(np.mean(kern_ms)),
-                        float(rows), float(nodes), float(grp)], dtype=torch.float64, device="cpu" if rehearsal else "cuda")
-    if world > 1:
-        tmax = agg[:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tot = agg[1:].clone()
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        dt = float(tmax.item())
-        segs, tri_tests, box_tests = (float(x) for x in tot[:3].tolist())
-        kmean_sum, rows_tot, nodes = float(tot[3].item()), float(tot[4].item()), float(tot[5].item())
-        grp = float(tot[6].item())
-        kmean = kmean_sum / world
-    else:
-        kmean, rows_tot = float(np.mean(kern_ms)), float(rows)
-
-    if rank == 0:
-        K = args.steps
-        ms_frame = dt * 1e3 / K
-        mrays = segs / dt / 1e6
-        # Record-byte model of SURVEY §8(d), kept as a side figure: these records are
-        # served by the scalar cache, L1 and L2 (the scene is cache-resident), not HBM.
-        seg_launch = segs / K / world
-        pt = integrator == "pathTrace"
-        alg_bytes = (seg_launch * (6 * BYTES["sphere"] if pt else object_bytes_per_segment(r))
-                     + tri_tests / K / world * BYTES["ktri" if pt else "tri"]
-                     + box_tests / K / world * BYTES["box"] + nodes / K / world * BYTES["node"]
-                     + grp / K / world
-                     + rows_tot / world * W * BYTES["pixel"])
-        record_gbs = alg_bytes / ((ms_frame if overlap else kmean) * 1e-3) / 1e9
-        workload = f"{args.scene}_{W}x{H}_spp{args.spp}_d{args.depth}_n{world}"
-        traffic = load_pmc_traffic(workload)
-        # Roofline: the megakernel is bound by VALU issue. achieved = VALU
-        # wave-instructions per launch (SQ_INSTS_VALU per traced segment, profiled, x this
-        # launch's segments) / the megakernel's mean time; peak = the chip's issue rate.
-        n_cu = torch.cuda.get_device_properties(local).multi_processor_count
-        valu_peak = n_cu * VALU_GINST_PER_CU
-        vp = load_valu_profile(workload)
-        valu_launch = vp["valu_insts_per_segment"] * seg_launch if vp else None
-        # with frame overlap a launch's event pair also spans the next frame's launch: the
-        # launch's effective duration is then the frame time (wall / K)
-        t_eff = ms_frame if overlap else kmean
-        valu_achieved = valu_launch / (t_eff * 1e-3) / 1e9 if vp else None
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(args, host_threads())
-        line = {
-            "metric": METRIC,
-            "value": round(mrays, 3),
-            "unit": "Mrays/s",
-            "n_gpus": world,
-            "steps": K,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_frame, 4),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": f"synthetic (deterministic {args.scene} scene from assets/scenes; counter-based RNG seed 1984)",
-            "config": {
-                "workload": workload,
-                "scene": SCENES[args.scene][5],
-                "width": W, "height": H, "spp": args.spp, "depth": args.depth,
-                "row_block": block, "lanes_per_pixel": int(st["lanes_per_pixel"]),
-                "refill": int(st["refill"]), "queue_blocks": int(st["queue_blocks"]), "parallelism": f"row-tiles x{world} + RCCL gather" if world > 1 else "single GPU",
-                "segments_per_frame": int(segs / K),
-                "msamples_per_s": round(W * H * args.spp / (dt / K) / 1e6, 3),
-            },
-            "roofline": {
-                "bound": "valu",
-                "achieved": round(valu_achieved, 2) if vp else None,
-                "peak": round(valu_peak, 1),
-                "unit": "Ginst/s (wave64 VALU instructions)",
-                "frac": round(valu_achieved / valu_peak, 4) if vp else None,
-                "traffic": traffic,
-                # the launch duration `achieved` divides by: the event-pair mean, or with frame
-                # overlap the frame time (the pairs then also span the wait behind the other stream)
-                "kernel_ms": round(t_eff, 4),
-                "kernel_ms_event_pairs": round(kmean, 4),
-                "launch_ms": round(float(np.mean(launch_ms)), 4),
-                "valu_insts_per_launch": int(valu_launch) if vp else None,
-                "valu_profile": vp.get("source") if vp else None,
-                "hbm_frac": round(traffic / (t_eff * 1e-3) / (HBM_PEAK_GBS * 1e9), 5) if traffic else None,
-                "overlap": overlap,
-                "record_bytes_per_launch": int(alg_bytes),
-                "record_gbs": round(record_gbs, 1),
-                "note": ("achieved = SQ_INSTS_VALU per segment (rocprofv3 pass on this workload, "
-                         "profiles/valu_issue.json) x this launch's segments / the launch's effective time: the "
-                         "frame time when consecutive frames overlap on two streams (overlap: true; "
-                         "kernel_ms_event_pairs then also spans the wait behind the other stream's launch), "
-                         "else the megakernel's mean time (library event pairs, combine pass excluded; "
-                         "rocprofv3 kernel traces are taken with --no-overlap); peak = CUs x 4 SIMDs x 2.4 GHz / 2 "
-                         "cycles per wave64 VALU op. traffic = HBM-side bytes per launch (FETCH_SIZE x 2 + "
-                         "WRITE_SIZE, profiles/pmc_traffic.json), hbm_frac its share of 8 TB/s; "
-                         "record_* = SURVEY 8(d)'s cache-served record-byte model"),
-            },
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    # Isolated frames (outside the timed region): one launch at a time on one context, so the
+    # library's event pair is the megakernel's own latency (the roofline's time base), and at
+    # N > 1 the gather's own time (events on the stream the collective is ordered on) and one
+    # whole frame's latency (render + gather + row assembly, barrier to barrier).
+    iso_kernel, iso_gather, iso_frame = [], [], []
+    cur = torch.cuda.current_stream()
+    for _ in range(N_ISOLATED):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if rehearsal:
+            render_into(frame.tile, params)
+        else:
+            r.render_device(params, frame.tile.data_ptr(), cur.cuda_stream)
+        torch.cuda.synchronize()
+        iso_kernel.append(r.stats()["kernel_ms"])
+        if world > 1:
+            if rehearsal:  # gloo on host tensors: no device events
+                g0 = time.perf_counter()
+                frame.gather()
+                iso_gather.append((time.perf_counter() - g0) * 1e3)
+            else:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                frame.gather(events=(e0, e1))
+                torch.cuda.synchronize()
+                iso_gather.append(e0.elapsed_time(e1))
+            dist.barrier()
+        torch.cuda.synchronize()
+        iso_frame.append((time.perf_counter() - t1) * 1e3)
+    n_cu = torch.cuda.get_device_properties(local).multi_processor_count
+    out = {
+        "dt": dt, "segs": float(st["segments"]), "tri_tests": float(st["tri_tests"]),
+        "box_tests": float(st["box_tests"]), "nodes": float(st["node_visits"]),
+        "grp_bytes": float(st["group_sphere_tests"] * BYTES["sphere"]
+                           + st["group_moving_sphere_tests"] * BYTES["moving_sphere"]),
+        "rows": float(rows),
+        "kernel_ms": st["kernel_ms_sum"] / st["launches"],  # the megakernel alone (library event pairs)
+        "kernel_ms_isolated": float(np.mean(iso_kernel)),
+        "gather_ms": float(np.mean(iso_gather)) if iso_gather else 0.0,
+        "frame_ms_isolated": float(np.mean(iso_frame)),
+        "launch_ms": float(np.mean(launch_ms)),
+        "lanes_per_pixel": int(st["lanes_per_pixel"]), "refill": int(st["refill"]),
+        "queue_blocks": int(st["queue_blocks"]), "variant": st["variant_name"],
+        "object_bytes_per_segment": object_bytes_per_segment(r) if integrator != "pathTrace" else 0,
+        "n_cu": n_cu, "overlap": overlap,
+    }
     for rr in rs:
         rr.close()
+    return out
+
+
+def selftest_measure(args, world, rank):
+    """--line-selftest (CPU only, tests/test_bench_line.py): deterministic per-rank numbers in
+    place of the GPU measurement, so the collectives and the JSON line run end to end under
+    torch.distributed.run with gloo."""
+    return {
+        "dt": 0.010 * (1.0 + 0.1 * rank), "segs": 1.0e6 * (rank + 1), "tri_tests": 2.0e6, "box_tests": 1.0e5,
+        "nodes": 0.0, "grp_bytes": 0.0, "rows": float(args.height // world),
+        "kernel_ms": 5.0 + rank, "kernel_ms_isolated": 4.0 + rank, "gather_ms": 0.05 * (rank + 1),
+        "frame_ms_isolated": 6.0 + 0.5 * rank, "launch_ms": 5.5 + rank, "lanes_per_pixel": 32, "refill": 8,
+        "queue_blocks": 1536, "variant": "render_kernel<false, true, false, false, 3>",
+        "object_bytes_per_segment": 240, "n_cu": 256, "overlap": False,
+    }
+
+
+# per-rank numbers combined over ranks: SUM (work), MAX (time of the slowest rank), and
+# MIN / MAX of the per-rank kernel times (the shard balance the scaling curve depends on)
+SUM_KEYS = ("segs", "tri_tests", "box_tests", "nodes", "grp_bytes", "rows")
+
+
+def aggregate(m: dict, world: int, device):
+    """Combines the ranks' numbers (one all_gather of a small vector over the job's group)."""
+    import torch
+    import torch.distributed as dist
+
+    keys = ("dt",) + SUM_KEYS + ("kernel_ms", "kernel_ms_isolated", "gather_ms", "frame_ms_isolated", "launch_ms")
+    v = torch.tensor([float(m[k]) for k in keys], dtype=torch.float64, device=device)
+    if world > 1:
+        parts = [torch.zeros_like(v) for _ in range(world)]
+        dist.all_gather(parts, v)
+        per_rank = torch.stack(parts).cpu().numpy()
+        comm_world = dist.get_world_size()
+    else:
+        per_rank = v.cpu().numpy()[None, :]
+        comm_world = 1
+    col = {k: per_rank[:, i] for i, k in enumerate(keys)}
+    agg = dict(m)
+    agg["dt"] = float(col["dt"].max())
+    for k in SUM_KEYS:
+        agg[k] = float(col[k].sum())
+    for k in ("kernel_ms", "kernel_ms_isolated", "launch_ms"):
+        agg[k] = float(col[k].mean())
+        agg[k + "_min"] = float(col[k].min())
+        agg[k + "_max"] = float(col[k].max())
+    agg["gather_ms"] = float(col["gather_ms"].max())
+    agg["frame_ms_isolated"] = float(col["frame_ms_isolated"].max())
+    agg["world_size_comm"] = comm_world
+    return agg
+
+
+def build_line(args, agg: dict, world: int, cpu=None) -> dict:
+    """The bench's JSON line (rank 0)."""
+    W, H, K = args.width, args.height, args.steps
+    dt, segs = agg["dt"], agg["segs"]
+    overlap = agg["overlap"]
+    ms_frame = dt * 1e3 / K
+    mrays = segs / dt / 1e6
+    # Record-byte model of SURVEY §8(d), kept as a side figure: these records are
+    # served by the scalar cache, L1 and L2 (the scene is cache-resident), not HBM.
+    seg_launch = segs / K / world
+    pt = INTEGRATOR.get(args.scene) == "pathTrace"
+    alg_bytes = (seg_launch * (6 * BYTES["sphere"] if pt else agg["object_bytes_per_segment"])
+                 + agg["tri_tests"] / K / world * BYTES["ktri" if pt else "tri"]
+                 + agg["box_tests"] / K / world * BYTES["box"] + agg["nodes"] / K / world * BYTES["node"]
+                 + agg["grp_bytes"] / K / world
+                 + agg["rows"] / world * W * BYTES["pixel"])
+    t_iso = agg["kernel_ms_isolated"]
+    workload = f"{args.scene}_{W}x{H}_spp{args.spp}_d{args.depth}_n{world}"
+    sha = kernel_source_sha()
+    # Roofline: the megakernel is bound by VALU issue (DESIGN §5). achieved = VALU
+    # wave-instructions per launch (SQ_INSTS_VALU per traced segment, profiled of this very
+    # kernel, x this launch's segments) / the isolated megakernel time; peak = the chip's issue rate.
+    valu_peak = agg["n_cu"] * VALU_GINST_PER_CU
+    vp = load_valu_profile(workload)
+    vp_bad = profile_check(vp, agg["variant"], sha)
+    valu_launch = vp["valu_insts_per_segment"] * seg_launch if vp else None
+    achieved = valu_launch / (t_iso * 1e-3) / 1e9 if vp and not vp_bad else None
+    achieved_ovl = valu_launch / (ms_frame * 1e-3) / 1e9 if vp and not vp_bad else None
+    tp = load_pmc_traffic(workload)
+    tp_bad = profile_check(tp, agg["variant"], sha)
+    traffic = float(tp["hbm_bytes_per_launch"]) if tp and not tp_bad else None
+    line = {
+        "metric": METRIC,
+        "value": round(mrays, 3),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_frame, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic (deterministic {args.scene} scene from assets/scenes; counter-based RNG seed 1984)",
+        "config": {
+            "workload": workload,
+            "scene": SCENES[args.scene][5],
+            "width": W, "height": H, "spp": args.spp, "depth": args.depth,
+            "row_block": args.row_block, "lanes_per_pixel": agg["lanes_per_pixel"],
+            "variant": agg["variant"], "queue": agg["queue_blocks"] > 0,
+            "refill": agg["refill"], "queue_blocks": agg["queue_blocks"],
+            "kernel_source_sha": sha,
+            "parallelism": f"row-tiles x{world} + RCCL gather" if world > 1 else "single GPU",
+            "segments_per_frame": int(segs / K),
+            "msamples_per_s": round(W * H * args.spp / (dt / K) / 1e6, 3),
+        },
+        # one frame at a time, outside the timed region (N_ISOLATED frames, max over ranks):
+        # what a single frame costs without frame overlap or pipelining
+        "frame_latency": {
+            "frame_ms_isolated": round(agg["frame_ms_isolated"], 4),
+            "kernel_ms_isolated": round(t_iso, 4),
+            "gather_ms": round(agg["gather_ms"], 4),
+        },
+        "roofline": {
+            "bound": "valu",
+            "achieved": round(achieved, 2) if achieved else None,
+            "peak": round(valu_peak, 1),
+            "unit": "Ginst/s (wave64 VALU instructions)",
+            "frac": round(achieved / valu_peak, 4) if achieved else None,
+            "traffic": traffic,
+            # the isolated launch's megakernel time (library event pair, combine pass excluded)
+            "kernel_ms": round(t_iso, 4),
+            "frac_overlapped": round(achieved_ovl / valu_peak, 4) if achieved_ovl else None,
+            "kernel_ms_timed_event_pairs": round(agg["kernel_ms"], 4),
+            "launch_ms": round(agg["launch_ms"], 4),
+            "valu_insts_per_launch": int(valu_launch) if valu_launch else None,
+            "valu_profile": vp.get("source") if vp else None,
+            "profile_mismatch": vp_bad,
+            "traffic_profile_mismatch": tp_bad,
+            "hbm_frac": round(traffic / (t_iso * 1e-3) / (HBM_PEAK_GBS * 1e9), 5) if traffic else None,
+            "overlap": overlap,
+            "record_bytes_per_launch": int(alg_bytes),
+            "record_gbs": round(alg_bytes / (t_iso * 1e-3) / 1e9, 1),
+            "note": ("achieved = SQ_INSTS_VALU per segment (rocprofv3 pass of this kernel symbol and these kernel "
+                     "sources, profiles/valu_issue.json) x this launch's segments / the isolated megakernel time "
+                     "(kernel_ms: one launch at a time after the timed loop, library event pair, combine pass "
+                     "excluded - what rocprofv3's kernel trace measures); frac_overlapped divides by the timed "
+                     "frame time instead (two launches in flight); peak = CUs x 4 SIMDs x 2.4 GHz / 2 cycles per "
+                     "wave64 VALU op. traffic = HBM-side bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, "
+                     "profiles/pmc_traffic.json), hbm_frac its share of 8 TB/s; a profile of another kernel "
+                     "symbol or other kernel sources is not used (profile_mismatch); record_* = SURVEY 8(d)'s "
+                     "cache-served record-byte model"),
+        },
+        "cpu_baseline": cpu,
+    }
+    if world > 1:
+        # what the scaling curve needs to explain itself: the shard balance over ranks and the
+        # exchange's own cost
+        line["scale"] = {
+            "world_size_comm": agg["world_size_comm"],
+            "kernel_ms_timed_min": round(agg["kernel_ms_min"], 4),
+            "kernel_ms_timed_max": round(agg["kernel_ms_max"], 4),
+            "kernel_ms_isolated_min": round(agg["kernel_ms_isolated_min"], 4),
+            "kernel_ms_isolated_max": round(agg["kernel_ms_isolated_max"], 4),
+            "gather_ms": round(agg["gather_ms"], 4),
+            "frame_ms_isolated": round(agg["frame_ms_isolated"], 4),
+        }
+    return line
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    if args.line_selftest:  # CPU: the N > 1 collectives and line building, without a GPU
+        if world > 1:
+            dist.init_process_group("gloo")
+        agg = aggregate(selftest_measure(args, world, rank), world, "cpu")
+        if rank == 0:
+            print(json.dumps(build_line(args, agg, world)), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    # RTMI_REHEARSAL=1 (testing only): N ranks share GPU 0 and gather over gloo
+    # through host memory, to exercise the N > 1 code path on a one-GPU box.
+    rehearsal = os.environ.get("RTMI_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
+    torch.cuda.set_device(local)
+    if world > 1:
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    m = measure(args, world, rank, local, rehearsal)
+    agg = aggregate(m, world, "cpu" if rehearsal else torch.device("cuda", local))
+    if rank == 0:
+        cpu = cpu_baseline(args, host_threads()) if not args.no_cpu_baseline and world == 1 else None
+        print(json.dumps(build_line(args, agg, world, cpu)), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -96,12 +96,18 @@ class RowShardedFrame:
                     src[int(y)] = k * self.max_rows + j
             self.src_rows = torch.as_tensor(src, dtype=torch.long, device=self.device)
 
-    def gather(self) -> Optional["object"]:
-        """One gather of every rank's tile to rank 0, then one row permutation."""
+    def gather(self, events=None) -> Optional["object"]:
+        """One gather of every rank's tile to rank 0, then one row permutation. `events`
+        (start, end) torch.cuda.Events are recorded on the current stream around the
+        collective alone (the stream is ordered after the gather once it returns)."""
         if self.world == 1:
             return self.frame
+        if events:
+            events[0].record()
         self.dist.gather(self.tile, self.gather_list if self.rank == 0 else None, dst=0,
                          group=self.group)
+        if events:
+            events[1].record()
         if self.rank != 0:
             return None
         self.torch.index_select(self.gathered, 0, self.src_rows, out=self.frame)

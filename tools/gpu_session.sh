@@ -1,0 +1,50 @@
+#!/bin/bash
+# One GPU session on a gpurun box, from the repository root; everything lands in gpurun_out/$TAG/.
+#   TESTS=1   pytest -m gpu + smoke()
+#   BENCH=1   the default bench line (config 2, frame overlap, CPU baseline)
+#   SCENES    bench lines of these workloads (no CPU baseline)
+#   VALU      SQ_INSTS_VALU passes of these workloads (--no-overlap), for profiles/valu_issue.json
+#   TRAFFIC   FETCH_SIZE and WRITE_SIZE passes (separate runs), for profiles/pmc_traffic.json
+#   PROF      rocprofv3 --kernel-trace --stats of these workloads (--no-overlap)
+#   MULTI=1   examples/multigpu (RCCL through the C ABI, N = 1 on this box)
+# Every GPU step has its own time limit; a fault, abort or time-out ends the session there.
+#   TAG=r03c TESTS=1 BENCH=1 VALU="cornellbox1 bunny" bash tools/gpu_session.sh
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/${TAG:-session}
+mkdir -p "$O"
+stop_if_fatal() { rc=$1; name=$2; echo "$name rc=$rc"; if [ "$rc" -ne 0 ]; then echo "fatal in $name"; exit "$rc"; fi; }
+export TMPDIR=/tmp
+if [ "${TESTS:-0}" = "1" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread > "$O/pytest_gpu.log" 2>&1
+  stop_if_fatal $? pytest
+  timeout -k 10 240 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
+  stop_if_fatal $? smoke
+fi
+if [ "${BENCH:-0}" = "1" ]; then
+  timeout -k 10 300 python bench.py > "$O/bench.log" 2>&1
+  stop_if_fatal $? bench
+fi
+for sc in ${SCENES:-}; do
+  timeout -k 10 300 python bench.py --scene $sc --no-cpu-baseline ${BENCH_ARGS:-} > "$O/bench_$sc.log" 2>&1
+  stop_if_fatal $? bench_$sc
+done
+for sc in ${VALU:-}; do
+  timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --output-format csv -d "$O/pmc_valu_$sc" -o pmc -- python3 bench.py --scene $sc --steps 2 --warmup 1 --no-cpu-baseline --no-overlap > "$O/pmc_valu_$sc.log" 2>&1
+  stop_if_fatal $? pmc_valu_$sc
+done
+for sc in ${TRAFFIC:-}; do
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_${sc}_$c" -o pmc -- python3 bench.py --scene $sc --steps 1 --warmup 1 --no-cpu-baseline --no-overlap > "$O/pmc_${sc}_$c.log" 2>&1
+    stop_if_fatal $? pmc_${sc}_$c
+  done
+done
+for sc in ${PROF:-}; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$sc" -o run --output-format csv -- python3 bench.py --scene $sc --steps ${PROF_STEPS:-10} --warmup ${PROF_WARMUP:-2} --no-cpu-baseline --no-overlap > "$O/prof_$sc.log" 2>&1
+  stop_if_fatal $? prof_$sc
+done
+if [ "${MULTI:-0}" = "1" ] && [ -x ./examples/multigpu ]; then
+  timeout -k 10 120 ./examples/multigpu 128 96 8 1 > "$O/multigpu.log" 2>&1
+  stop_if_fatal $? multigpu
+fi
+echo done

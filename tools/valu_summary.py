@@ -55,7 +55,11 @@ def workload(pmc_dir, bench_log, out_json):
     line = next(json.loads(s) for s in open(bench_log) if s.startswith("{"))
     wl = line["config"]["workload"]
     segs = line["config"]["segments_per_frame"]
-    ds = dispatches(pmc_dir, ["render_kernel", "pathtrace_kernel"])
+    # only the launched variant's dispatches (bench.py's line names it; rt_kernel_variant_name)
+    variant = line["config"].get("variant")
+    ds = dispatches(pmc_dir, [variant] if variant else ["render_kernel", "pathtrace_kernel"])
+    if not ds:
+        raise SystemExit(f"{pmc_dir}: no dispatch of {variant!r}")
     insts = [v["counters"]["SQ_INSTS_VALU"] for v in ds.values()]
     # every dispatch of the pass renders the same frame (warm-up + timed): take their mean
     per_launch = sum(insts) / len(insts)
@@ -64,7 +68,9 @@ def workload(pmc_dir, bench_log, out_json):
            "valu_insts_per_launch": per_launch, "spread": (max(insts) - min(insts)) / per_launch,
            "segments_per_launch": segs, "valu_insts_per_segment": per_launch / segs,
            "effective_clock_ghz": sum(clk) / len(clk) if clk else None,
-           "dispatches": len(insts), "source": os.path.relpath(pmc_dir, REPO)}
+           "dispatches": len(insts), "source": os.path.relpath(pmc_dir, REPO),
+           # what bench.py checks before using the entry: the launched symbol and the kernel sources
+           "variant": variant, "kernel_source_sha": line["config"].get("kernel_source_sha")}
     d = json.load(open(out_json)) if os.path.exists(out_json) else {}
     d.setdefault("note", "SQ_INSTS_VALU (whole chip, wave64 instructions; calibrated in profiles/r02/valu_probe.json) "
                          "of the bench workload's render kernel per traced segment; bench.py multiplies it by the "
