@@ -6,8 +6,10 @@
 //   ./main_driver SCENE.yaml [--width W] [--height H] [--spp S] [--depth D]
 //       [--frames F] [--realtime] [--camera] [--move-at K] [--device G] [--out FILE.ppm]
 // --camera sets an explicit camera (the `camera` global) over the scene's; --move-at K
-// moves it before frame K, which clears the accumulation (camera->isDirty()).
+// moves it before frame K (walk + yaw, Camera.h:40-67), which clears the accumulation
+// (camera->isDirty(), main.cu:877-881).
 // --device -1 runs initialize()/cleanup() only (scene build, no GPU).
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -59,12 +61,17 @@ int main(int argc, char** argv) {
             return 0;
         }
         for (int f = 0; f < frames; ++f) {
-            if (f == moveAt) cam.eye = rtmi::Vector3Df(0.1f, 0.05f, 1.2f);
+            if (f == moveAt) {
+                H::camera->walk(-0.05f);
+                H::camera->yaw(0.03f);
+            }
             const auto t0 = std::chrono::steady_clock::now();
             H::pathTracing();
             H::frameTime = std::chrono::duration<float>(std::chrono::steady_clock::now() - t0).count();
         }
-        std::printf("frames %d samples %u\n", frames, H::sampleCount);
+        std::printf("frames %d samples %u\n", frames,
+                    H::realtime ? H::canvas->getSampleCount() * (uint32_t)H::samplesPerFrame
+                                : (uint32_t)H::samplesPerFrame);
         FILE* fp = std::fopen(out.c_str(), "wb");
         if (!fp) return 1;
         std::fprintf(fp, "P6\n%d %d\n255\n", w, h);  // top row first (Canvas::writeToPPM)

@@ -66,6 +66,7 @@ int main(int argc, char** argv) {
         rtmi::Canvas canvas(width, height);
         rt_render_params p{width, height, spp, depth, seed, 0, 1, 0, 1, lanes, RT_INTEGRATOR_RAYCOLOR, 0};
         ctx.check(rt_render(ctx.raw(), &p, canvas.data()));
+        canvas.gammaFromRadiance();  // writePixel's gamma (Canvas.h:63-67)
         rt_render_stats st;
         ctx.check(rt_sync_stats(ctx.raw(), &st));
         if (png) canvas.writeToPNG(out);

@@ -288,6 +288,69 @@ rt_status rt_camera(rt_ctx* ctx, const float eye[3], const float center[3], cons
                     float aspect_ratio, float fov, float aperture, float focus_distance,
                     float time0, float time1);
 
+/* ---- the reference's Camera object (Camera.h:12-196) ----
+ * rt_camera_state holds Camera's fields; the rt_camera_* functions below restate its methods
+ * with the reference's float operations, so a realtime frontend's camera moves
+ * (OpenGLFrontend.cpp:393-407 mouse, 586-611 keys, 189-197 sliders) land on the reference's
+ * floats. The state is the caller's (plain memory, no context needed). Like the reference, a
+ * move changes eye / center / forward / right but not the view that getRay reads
+ * (origin, lower_left, horizontal, vertical, right, true_up, lens_radius) until
+ * rt_camera_update_view_matrix runs while the state is dirty. */
+typedef struct rt_camera_state {
+    float eye[3], center[3], up[3];
+    float forward[3], right[3], true_up[3];
+    float origin[3], horizontal[3], vertical[3], lower_left[3];
+    float aspect_ratio, fov, scale, viewport_height, viewport_width;
+    float moving_speed; /* 1.5 after initialize (Camera.h:28); the frontend's "Camera Speed" slider */
+    float aperture, focus_distance, lens_radius, time0, time1;
+    int32_t dirty;      /* bIsDirty */
+} rt_camera_state;
+/* Camera::initialize (Camera.h:19-34): fields, movingSpeed 1.5, dirty, updateViewMatrix. */
+rt_status rt_camera_initialize(rt_camera_state* cam, const float eye[3], const float center[3], const float up[3],
+                               float aspect_ratio, float fov, float aperture, float focus_distance, float time0,
+                               float time1);
+/* Camera::updateViewMatrix (Camera.h:86-103): recomputes the view while dirty and leaves the
+ * state dirty (updateLensRadius, Camera.h:110-113, sets the flag); the caller clears it
+ * (resetDiryFlag: cam->dirty = 0), as pathTracing does (main.cu:877-881). */
+rt_status rt_camera_update_view_matrix(rt_camera_state* cam);
+/* walk / strafe / raise (Camera.h:40-56): eye and center += axis * movingSpeed * delta along
+ * forward / right / up. yaw (58-67): forward and right rotateY by delta radians, center =
+ * eye + forward. pitch (69-76): forward rotated about right. orbit (78-84): eye turned 0.01 rad
+ * about the vertical through `target`. setAperture (105-108). All set the dirty flag. */
+rt_status rt_camera_walk(rt_camera_state* cam, float delta);
+rt_status rt_camera_strafe(rt_camera_state* cam, float delta);
+rt_status rt_camera_raise(rt_camera_state* cam, float delta);
+rt_status rt_camera_yaw(rt_camera_state* cam, float delta);
+rt_status rt_camera_pitch(rt_camera_state* cam, float delta);
+rt_status rt_camera_orbit(rt_camera_state* cam, const float target[3]);
+rt_status rt_camera_set_aperture(rt_camera_state* cam, float aperture);
+/* The context renders with the state's current view (what renderKernel's getRay reads from
+ * the managed Camera); rt_camera() is rt_camera_initialize + rt_camera_apply. */
+rt_status rt_camera_apply(rt_ctx* ctx, const rt_camera_state* cam);
+/* The Camera object of the context's current camera (set by rt_camera, rt_camera_apply or a
+ * scene file): the `camera` a frontend drives after initialize(). RT_ERR_STATE if none. */
+rt_status rt_get_camera(const rt_ctx* ctx, rt_camera_state* out);
+
+/* ---- the reference's Canvas buffers (Canvas.h:20-200) on the device ----
+ * An accumulation buffer (float RGB) and a pixel buffer (uint8 RGB, Canvas::gamma) of
+ * width x height in the context's device memory, row 0 = the bottom row. Destroy canvases
+ * before their context. The sample / rendering-time counters are host state of the
+ * caller's Canvas (the C++ facade keeps them). */
+typedef struct rt_canvas rt_canvas;
+rt_status rt_canvas_create(rt_ctx* ctx, int32_t width, int32_t height, rt_canvas** out);
+void rt_canvas_destroy(rt_canvas* canvas);
+/* clearAccumulationBuffer (Canvas.h:162-164) - to zero: the reference's cudaMemset(..., 1,
+ * ...) leaves 2.4e-38 per float, a bug with no visible effect after gamma. */
+rt_status rt_canvas_clear_accumulation(rt_canvas* canvas);
+/* One GPU_REALTIME frame (renderKernel -> accumulatePixel, main.cu:195-196, Canvas.h:82-98)
+ * into the canvas: rt_accumulate on the full frame with `sample_count` = the samples per
+ * pixel accumulated after this frame (the reference: incrementSampleCount() before the
+ * launch, 1 sample per frame); synchronous, like pathTracing's cudaDeviceSynchronize. */
+rt_status rt_canvas_accumulate(rt_canvas* canvas, const rt_render_params* params, uint32_t sample_count);
+/* getPixelBuffer (Canvas.h:105-107): width x height x 3 uint8; the accumulation buffer. */
+rt_status rt_canvas_read_pixels(const rt_canvas* canvas, uint8_t* out_host);
+rt_status rt_canvas_read_accumulation(const rt_canvas* canvas, float* out_host);
+
 /* Builds the device scene tables and uploads them (replaces the device-side
  * `new` factories + cudaMemcpyToSymbol, main.cu:850-851). */
 rt_status rt_commit(rt_ctx* ctx);

@@ -9,6 +9,7 @@
 //   createLambertianMaterial(materials, 0, Vector3Df(1, 0, 0));        // kernels.h:54
 //   createSphere(spheres, 0, {-1, 0, -1}, 0.5f, materials[0]);        // kernels.h:103
 //   Camera camera(eye, center, up, float(w) / h, 60.0f, 0.0f, 2.0f, 0.0f, 1.0f);
+//   camera.walk(0.1f); camera.updateViewMatrix();              // Camera.h:40-44, 86-103
 //   ctx.setCamera(camera);
 //   Canvas canvas(w, h);
 //   ctx.pathTracing(canvas, spp, bounces);                  // main.cu:875-898
@@ -64,42 +65,115 @@ struct Handle {
 using Material = Handle;
 using Hitable = Handle;
 
-// Camera (Camera.h:14-34): parameters only; the view basis is derived by the
-// library exactly like Camera::updateViewMatrix.
-struct Camera {
-    Vector3Df eye, center, up;
-    float aspectRatio = 1.0f, fov = 90.0f, aperture = 2.0f, focusDistance = 1.0f;
-    float time0 = 0.0f, time1 = 0.0f;
+// Camera (Camera.h:12-196): the reference's fields (rt_camera_state) and methods, restated
+// by the library with the reference's float operations (rtmi.h rt_camera_*), so a frontend's
+// moves - walk/strafe/raise/yaw/pitch from OpenGLFrontend.cpp:393-407 and 586-611, the
+// aperture/FOV/speed sliders of 189-197 - give the reference's floats. Context::setCamera
+// hands the current view (what getRay reads) to the renderer.
+class Camera {
+public:
     Camera() = default;
     Camera(const Vector3Df& e, const Vector3Df& c, const Vector3Df& u, float aspect, float fov_ = 90.0f,
            float aperture_ = 2.0f, float focus = 1.0f, float t0 = 0.0f, float t1 = 0.0f) {
         initialize(e, c, u, aspect, fov_, aperture_, focus, t0, t1);
     }
+    explicit Camera(const rt_camera_state& s) : s_(s) {}
     void initialize(const Vector3Df& e, const Vector3Df& c, const Vector3Df& u, float aspect,
                     float fov_ = 90.0f, float aperture_ = 2.0f, float focus = 1.0f, float t0 = 0.0f,
                     float t1 = 0.0f) {
-        eye = e; center = c; up = u; aspectRatio = aspect; fov = fov_; aperture = aperture_;
-        focusDistance = focus; time0 = t0; time1 = t1;
+        check(rt_camera_initialize(&s_, e.data(), c.data(), u.data(), aspect, fov_, aperture_, focus, t0, t1));
     }
+    void walk(float delta) { check(rt_camera_walk(&s_, delta)); }
+    void strafe(float delta) { check(rt_camera_strafe(&s_, delta)); }
+    void raise(float delta) { check(rt_camera_raise(&s_, delta)); }
+    void yaw(float delta) { check(rt_camera_yaw(&s_, delta)); }
+    void pitch(float delta) { check(rt_camera_pitch(&s_, delta)); }
+    void orbit(const Vector3Df& target) { check(rt_camera_orbit(&s_, target.data())); }
+    void updateViewMatrix() { check(rt_camera_update_view_matrix(&s_)); }
+    void setAperture(float a) { check(rt_camera_set_aperture(&s_, a)); }
+    void updateLensRadius() { check(rt_camera_set_aperture(&s_, s_.aperture)); }
+    // Camera.h:115-137: references, so an ImGui::SliderFloat can write through them
+    // (followed by setDirty(), OpenGLFrontend.cpp:189-197)
+    float& getAperture() { return s_.aperture; }
+    const float& getAperture() const { return s_.aperture; }
+    float& getFOV() { return s_.fov; }
+    const float& getFOV() const { return s_.fov; }
+    float& getMovingSpeed() { return s_.moving_speed; }
+    const float& getMovingSpeed() const { return s_.moving_speed; }
+    void setDirty() { s_.dirty = 1; }
+    bool isDirty() const { return s_.dirty != 0; }
+    void resetDiryFlag() { s_.dirty = 0; }  // the reference's spelling (Camera.h:147)
+    Vector3Df getEye() const { return {s_.eye[0], s_.eye[1], s_.eye[2]}; }
+    Vector3Df getCenter() const { return {s_.center[0], s_.center[1], s_.center[2]}; }
+    const rt_camera_state& state() const { return s_; }
+
+private:
+    static void check(rt_status st) {
+        if (st != RT_OK) throw Error(st, "camera: invalid argument");
+    }
+    rt_camera_state s_{};
 };
 
-// Canvas (Canvas.h): float mean radiance (row 0 = bottom) + gamma'd 8-bit output.
+// Canvas (Canvas.h:20-200): float radiance of the last offline frame (row 0 = bottom), the
+// gamma'd 8-bit pixel buffer, and the realtime accumulation on the device (a librtmi
+// rt_canvas, created by the first Context::accumulate). Counters as Canvas.h:162-189.
 class Canvas {
 public:
-    Canvas(int32_t w, int32_t h) : width(w), height(h), radiance((size_t)w * h * 3, 0.0f) {}
+    Canvas(int32_t w, int32_t h) { initialize(w, h); }
+    ~Canvas() { rt_canvas_destroy(device_); }
+    Canvas(const Canvas&) = delete;
+    Canvas& operator=(const Canvas&) = delete;
+    // Canvas::initialize (Canvas.h:27-40)
+    void initialize(int32_t w, int32_t h) {
+        rt_canvas_destroy(device_);
+        device_ = nullptr;
+        width = w;
+        height = h;
+        radiance.assign((size_t)w * h * 3, 0.0f);
+        pixelBuffer.assign((size_t)w * h * 3, 0);
+        sampleCount = 0;
+        scale = 0.0f;
+        renderingTime = 0.0f;
+    }
     int32_t getWidth() const { return width; }
     int32_t getHeight() const { return height; }
     float* data() { return radiance.data(); }
     const float* data() const { return radiance.data(); }
-    std::vector<uint8_t> pixels() const {
-        std::vector<uint8_t> px(radiance.size());
-        rt_status s = rt_gamma_u8(radiance.data(), (int64_t)radiance.size(), px.data());
+    // getPixelBuffer (Canvas.h:105-107): the last frame written or accumulated
+    uint8_t* getPixelBuffer() { return pixelBuffer.data(); }
+    std::vector<uint8_t> pixels() const { return pixelBuffer; }
+    // clearAccumulationBuffer (Canvas.h:162-164), to zero (the reference's memset(1) is a bug)
+    void clearAccumulationBuffer() {
+        std::fill(radiance.begin(), radiance.end(), 0.0f);
+        if (device_ && rt_canvas_clear_accumulation(device_) != RT_OK)
+            throw Error(RT_ERR_HIP, "clearAccumulationBuffer failed");
+    }
+    // Canvas.h:166-189
+    void incrementSampleCount() {
+        sampleCount++;
+        scale = 1.0f / sampleCount;
+    }
+    void resetSampleCount() { sampleCount = 0; }
+    void resetRenderingTime() { renderingTime = 0.0f; }
+    uint32_t getSampleCount() const { return sampleCount; }
+    float getRenderingTime() const { return renderingTime; }
+    void incrementRenderingTime(float amount = 16.0f) { renderingTime += amount; }
+
+    // the offline frame's radiance -> pixel buffer (writePixel's gamma, Canvas.h:63-67)
+    void gammaFromRadiance() {
+        rt_status s = rt_gamma_u8(radiance.data(), (int64_t)radiance.size(), pixelBuffer.data());
         if (s != RT_OK) throw Error(s, "rt_gamma_u8");
-        return px;
+    }
+    rt_canvas* device(rt_ctx* ctx) {
+        if (!device_) {
+            rt_status s = rt_canvas_create(ctx, width, height, &device_);
+            if (s != RT_OK) throw Error(s, rt_last_error(ctx));
+        }
+        return device_;
     }
     // writeToPPM (Canvas.h:116-139): top row first.
     void writeToPPM(const std::string& path) const {
-        std::vector<uint8_t> px = pixels();
+        const std::vector<uint8_t>& px = pixelBuffer;
         FILE* f = std::fopen(path.c_str(), "wb");
         if (!f) throw Error(RT_ERR_IO, "cannot write " + path);
         std::fprintf(f, "P6\n%d %d\n255\n", width, height);
@@ -109,7 +183,7 @@ public:
     // writeToPNG (Canvas.h:141-154, stbi_write_png with the rows flipped): RGB8, top row
     // first, zlib stream of stored (uncompressed) deflate blocks - no codec dependency.
     void writeToPNG(const std::string& path) const {
-        std::vector<uint8_t> px = pixels();
+        const std::vector<uint8_t>& px = pixelBuffer;
         std::vector<uint8_t> raw;  // filter byte 0 + one top-down row
         raw.reserve((size_t)height * ((size_t)width * 3 + 1));
         for (int32_t y = height - 1; y >= 0; --y) {
@@ -169,8 +243,13 @@ public:
     }
 
 private:
-    int32_t width, height;
+    int32_t width = 0, height = 0;
     std::vector<float> radiance;
+    std::vector<uint8_t> pixelBuffer;
+    uint32_t sampleCount = 0;
+    float scale = 0.0f;
+    float renderingTime = 0.0f;
+    rt_canvas* device_ = nullptr;
 };
 
 class Context {
@@ -201,9 +280,13 @@ public:
         return table(obj_slots_, obj_ptrs_, n, false);
     }
 
-    void setCamera(const Camera& c) {
-        check(rt_camera(ctx_, c.eye.data(), c.center.data(), c.up.data(), c.aspectRatio, c.fov,
-                        c.aperture, c.focusDistance, c.time0, c.time1));
+    // the renderer reads the camera's current view, as renderKernel reads the managed Camera
+    void setCamera(const Camera& c) { check(rt_camera_apply(ctx_, &c.state())); }
+    // the context's Camera object (a scene file's camera after loadYAMLScene)
+    Camera getCamera() const {
+        rt_camera_state s{};
+        check(rt_get_camera(ctx_, &s));
+        return Camera(s);
     }
     void commit() { check(rt_commit(ctx_)); }
     // initialize() for SCENE == 1 (main.cu:623-786): camera, pre-seeded materials
@@ -237,6 +320,23 @@ public:
         rt_render_params p{canvas.getWidth(), canvas.getHeight(), spp, bounces, seed, sampleOffset,
                            1, 0, 1, 0, RT_INTEGRATOR_RAYCOLOR, 0};
         check(rt_render(ctx_, &p, canvas.data()));
+        canvas.gammaFromRadiance();
+    }
+
+    // One GPU_REALTIME frame (main.cu:876-888 after incrementSampleCount): `spp` fresh samples
+    // per pixel (the reference: 1) added to the canvas's device accumulation, its pixel buffer
+    // = gamma(acc * (1 / samples so far)). The canvas's sample count is the frame count, as the
+    // reference's (one incrementSampleCount per frame).
+    void accumulate(Canvas& canvas, int32_t spp, int32_t bounces, uint32_t seed = 1984,
+                    int32_t integrator = RT_INTEGRATOR_RAYCOLOR) {
+        if (canvas.getSampleCount() == 0) throw Error(RT_ERR_STATE, "accumulate: call incrementSampleCount first");
+        if (integrator == RT_INTEGRATOR_RAYCOLOR) commit();
+        const uint32_t frames = canvas.getSampleCount();
+        rt_render_params p{canvas.getWidth(), canvas.getHeight(), spp, bounces, seed, (frames - 1) * (uint32_t)spp,
+                           1, 0, 1, 0, integrator, 0};
+        rt_canvas* d = canvas.device(ctx_);
+        check(rt_canvas_accumulate(d, &p, frames * (uint32_t)spp));
+        check(rt_canvas_read_pixels(d, canvas.getPixelBuffer()));
     }
 
     // prepareCUDAscene (main.cu:404-553): loadObject(...) per PLY, then
@@ -253,6 +353,7 @@ public:
         rt_render_params p{canvas.getWidth(), canvas.getHeight(), spp, bounces, seed, sampleOffset,
                            1, 0, 1, 0, RT_INTEGRATOR_PATHTRACE, 0};
         check(rt_render(ctx_, &p, canvas.data()));
+        canvas.gammaFromRadiance();
     }
 
     // called by the factories below
@@ -295,6 +396,7 @@ inline void pathTracingMulti(const std::vector<Context*>& contexts, Canvas& canv
     rt_render_params p{canvas.getWidth(), canvas.getHeight(), spp, bounces, seed, 0,
                        rowBlock, 0, 1, 0, RT_INTEGRATOR_RAYCOLOR, 0};
     contexts[0]->check(rt_render_multi(raw.data(), (int32_t)raw.size(), &p, canvas.data()));
+    canvas.gammaFromRadiance();
 }
 
 namespace detail {

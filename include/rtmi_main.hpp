@@ -1,38 +1,33 @@
-// rtmi_main.hpp — the reference's host driver shape (main.h:9-35, main.cu:555-936)
-// over the C++ facade: globals `imageData`, `camera`, `canvas`, `width`, `height`,
-// `frameTime` and the four entry points initialize / clearBackBuffers / pathTracing /
-// cleanup, so a frontend written against main.h (OpenGLFrontend.cpp's loop) links
-// against librtmi.so unchanged apart from the namespace.
+// rtmi_main.hpp — the reference's host driver shape (main.h:9-35, main.cu:555-936) over the
+// C++ facade: globals `imageData`, `camera`, `canvas`, `width`, `height`, `frameTime` and the
+// four entry points initialize / clearBackBuffers / pathTracing / cleanup, so a frontend
+// written against main.h - OpenGLFrontend.cpp's loop, which calls camera->walk / strafe /
+// raise / yaw / pitch / updateViewMatrix, writes through camera->getAperture() / getFOV() /
+// getMovingSpeed() and reads canvas->getSampleCount() / getRenderingTime() - compiles against
+// these names (namespace rtmi::host) and links against librtmi.so alone (no HIP headers).
 //
-// Two modes, as the reference's GPU_REALTIME switch (main.cu:867-897):
+// Two modes, as the reference's GPU_REALTIME switch (main.cu:875-898):
 //  - offline (default): pathTracing() renders one frame of `samplesPerFrame` samples
-//    (renderKernel's sequential-sum-equivalent output) into `canvas`; imageData->data
-//    points at its gamma'd RGB8 (top row last, like Canvas's pixel buffer).
-//  - realtime (`realtime = true` before initialize(); needs librtmi's rt_accumulate and
-//    HIP for the device buffers, so build with -DRTMI_REALTIME and link amdhip64):
-//    every pathTracing() adds `samplesPerFrame` fresh samples per pixel to a device
-//    accumulation buffer (Canvas::accumulatePixel, Canvas.h:73-98) and refreshes
-//    imageData->data; a camera change clears the buffers first (camera->isDirty(),
-//    main.cu:869-873), detected by comparing `*camera` with the one last applied.
+//    (renderKernel's offline output) into `canvas`; imageData->data points at its gamma'd
+//    RGB8 pixel buffer (row 0 = the bottom row, like Canvas's pixel buffer).
+//  - realtime (`realtime = true`): pathTracing() follows main.cu:876-888 - if the camera is
+//    dirty: clearBackBuffers(), camera->updateViewMatrix(), camera->resetDiryFlag(); then
+//    canvas->incrementSampleCount(), canvas->incrementRenderingTime(frameTime * 1000), and one
+//    frame of `samplesPerFrame` fresh samples (the reference: 1) accumulated on the device
+//    (Canvas::accumulatePixel, Canvas.h:82-98); imageData->data = canvas->getPixelBuffer().
 //
 // The scene: initialize() loads `sceneFile` (initialize()'s SCENE == 1 YAML path,
-// main.cu:623-786) when set, otherwise it calls `buildScene(context, width, height)`
-// (the create* factories of the compiled-in scenes, main.cu:243-402).
+// main.cu:623-786) when set, otherwise it calls `buildScene(context, width, height)` (the
+// create* factories of the compiled-in scenes, main.cu:243-402). `camera` is the scene's
+// camera after initialize() unless the frontend set its own before.
 #pragma once
 
-#include <chrono>
 #include <cstdint>
-#include <cstring>
 #include <functional>
 #include <memory>
 #include <string>
-#include <vector>
 
 #include "rtmi.hpp"
-
-#ifdef RTMI_REALTIME
-#include <hip/hip_runtime_api.h>
-#endif
 
 namespace rtmi {
 namespace host {
@@ -48,14 +43,14 @@ struct ImageData {
 
 // main.h:22-30 globals (C++17 inline variables: one definition across translation units)
 inline std::shared_ptr<ImageData> imageData;
-inline Camera* camera = nullptr;  // optional: when set, applied at initialize and watched in realtime mode
+inline Camera* camera = nullptr;  // the scene's camera after initialize(), unless set before it
 inline Canvas* canvas = nullptr;
 inline int32_t width = 512;
 inline int32_t height = 512;
 inline float frameTime = 0.0f;  // seconds of the last frame, as the frontend's loop measures it
 
-// Driver settings that the reference fixes at compile time (SCENE, SAMPLES_PER_PIXEL,
-// MAX_DEPTH in main.cu / Constants.h).
+// Driver settings that the reference fixes at compile time (SCENE, samplesPerPixel,
+// BOUNCES in main.cu / Constants.h).
 inline int32_t device = 0;
 inline std::string sceneFile;  // scene YAML; empty = buildScene
 inline std::string modelsDir = "assets/models";
@@ -66,58 +61,19 @@ inline uint32_t seed = 1984;
 inline int32_t integrator = RT_INTEGRATOR_RAYCOLOR;
 inline bool realtime = false;
 
-// Canvas counters (Canvas.h incrementSampleCount / incrementRenderingTime)
-inline uint32_t sampleCount = 0;
-inline float renderingTime = 0.0f;  // ms
-
 inline Context* context = nullptr;
 
 namespace detail {
-inline std::vector<uint8_t>& hostPixels() {
-    static std::vector<uint8_t> px;
-    return px;
-}
-inline Camera& appliedCamera() {
-    static Camera c;
+inline std::unique_ptr<Camera>& ownCamera() {  // the scene's camera when the frontend set none
+    static std::unique_ptr<Camera> c;
     return c;
-}
-inline bool sameCamera(const Camera& a, const Camera& b) {
-    return std::memcmp(a.eye.data(), b.eye.data(), 3 * sizeof(float)) == 0 &&
-           std::memcmp(a.center.data(), b.center.data(), 3 * sizeof(float)) == 0 &&
-           std::memcmp(a.up.data(), b.up.data(), 3 * sizeof(float)) == 0 && a.aspectRatio == b.aspectRatio &&
-           a.fov == b.fov && a.aperture == b.aperture && a.focusDistance == b.focusDistance &&
-           a.time0 == b.time0 && a.time1 == b.time1;
-}
-inline void applyCamera() {
-    context->setCamera(*camera);
-    appliedCamera() = *camera;
-}
-#ifdef RTMI_REALTIME
-inline float*& accumDevice() {
-    static float* p = nullptr;
-    return p;
-}
-inline uint8_t*& pixelsDevice() {
-    static uint8_t* p = nullptr;
-    return p;
-}
-inline void hipCheck(hipError_t e, const char* what) {
-    if (e != hipSuccess) throw Error(RT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
-}
-#endif
-inline rt_render_params params(uint32_t offset) {
-    return rt_render_params{width, height, samplesPerFrame, maxDepth, seed, offset, 1, 0, 1, 0, integrator, 0};
 }
 }  // namespace detail
 
-// initialize (main.cu:855-865 with the scene setup of 623-853): context on `device`,
-// scene, camera, canvas, imageData.
+// initialize (main.cu:555-865): context on `device`, scene, camera, canvas, imageData.
 inline void initialize(int32_t w, int32_t h) {
     if (context) throw Error(RT_ERR_STATE, "initialize: already initialized (call cleanup first)");
-    if (w < 1 || h < 1 || samplesPerFrame < 1) throw Error(RT_ERR_INVALID, "initialize: bad size or spp");
-#ifndef RTMI_REALTIME
-    if (realtime) throw Error(RT_ERR_INVALID, "initialize: realtime mode needs a build with -DRTMI_REALTIME");
-#endif
+    if (w < 2 || h < 2 || samplesPerFrame < 1) throw Error(RT_ERR_INVALID, "initialize: bad size or spp");
     width = w;
     height = h;
     context = new Context(device);
@@ -127,86 +83,62 @@ inline void initialize(int32_t w, int32_t h) {
         buildScene(*context, w, h);
     else
         throw Error(RT_ERR_INVALID, "initialize: set sceneFile or buildScene");
-    if (camera) detail::applyCamera();
-    context->commit();
+    if (!camera) {
+        detail::ownCamera().reset(new Camera(context->getCamera()));
+        camera = detail::ownCamera().get();
+    }
+    context->setCamera(*camera);
+    if (integrator == RT_INTEGRATOR_RAYCOLOR) context->commit();
     canvas = new Canvas(w, h);
     imageData = std::make_shared<ImageData>();
     imageData->width = w;
     imageData->height = h;
     imageData->channels = 3;
     imageData->size = w * h * 3;
-    detail::hostPixels().assign((size_t)w * h * 3, 0);
-    imageData->data = detail::hostPixels().data();
-#ifdef RTMI_REALTIME
-    if (realtime && device >= 0) {
-        detail::hipCheck(hipMalloc((void**)&detail::accumDevice(), (size_t)w * h * 3 * sizeof(float)), "hipMalloc");
-        detail::hipCheck(hipMalloc((void**)&detail::pixelsDevice(), (size_t)w * h * 3), "hipMalloc");
-    }
-#endif
-    sampleCount = 0;
-    renderingTime = 0.0f;
+    imageData->data = canvas->getPixelBuffer();
 }
 
-// clearBackBuffers (main.cu:867-873): zero the accumulation, reset the counters.
+// clearBackBuffers (main.cu:866-873)
 inline void clearBackBuffers() {
     if (!canvas) throw Error(RT_ERR_STATE, "clearBackBuffers: not initialized");
-    std::memset(canvas->data(), 0, (size_t)width * height * 3 * sizeof(float));
-#ifdef RTMI_REALTIME
-    if (detail::accumDevice())
-        detail::hipCheck(hipMemset(detail::accumDevice(), 0, (size_t)width * height * 3 * sizeof(float)),
-                         "hipMemset");
-#endif
-    sampleCount = 0;
-    renderingTime = 0.0f;
+    canvas->clearAccumulationBuffer();
+    canvas->resetSampleCount();
+    canvas->resetRenderingTime();
 }
 
 // pathTracing (main.cu:875-898)
 inline void pathTracing() {
     if (!context) throw Error(RT_ERR_STATE, "pathTracing: not initialized");
-    if (camera && !detail::sameCamera(*camera, detail::appliedCamera())) {
-        clearBackBuffers();
-        detail::applyCamera();
+    if (realtime) {
+        if (camera->isDirty()) {
+            clearBackBuffers();
+            camera->updateViewMatrix();
+            camera->resetDiryFlag();
+        }
+        canvas->incrementSampleCount();
+        canvas->incrementRenderingTime(frameTime * 1000.0f);
+        context->setCamera(*camera);  // renderKernel reads the camera object at each launch
+        context->accumulate(*canvas, samplesPerFrame, maxDepth, seed, integrator);
+    } else {
+        canvas->incrementSampleCount();
+        context->setCamera(*camera);
+        if (integrator == RT_INTEGRATOR_PATHTRACE)
+            context->pathTraceFrame(*canvas, samplesPerFrame, maxDepth, seed);
+        else
+            context->pathTracing(*canvas, samplesPerFrame, maxDepth, seed);
     }
-    if (!realtime) {
-        rt_render_params p = detail::params(0);
-        context->commit();
-        context->check(rt_render(context->raw(), &p, canvas->data()));
-        sampleCount = (uint32_t)samplesPerFrame;
-        detail::hostPixels() = canvas->pixels();
-        imageData->data = detail::hostPixels().data();
-        return;
-    }
-#ifdef RTMI_REALTIME
-    context->commit();
-    const uint32_t offset = sampleCount;
-    sampleCount += (uint32_t)samplesPerFrame;
-    renderingTime += frameTime * 1000.0f;
-    rt_render_params p = detail::params(offset);
-    context->check(rt_accumulate(context->raw(), &p, detail::accumDevice(), sampleCount, detail::pixelsDevice(),
-                                 nullptr));
-    detail::hipCheck(hipMemcpy(detail::hostPixels().data(), detail::pixelsDevice(), (size_t)width * height * 3,
-                               hipMemcpyDeviceToHost),
-                     "hipMemcpy");
-    imageData->data = detail::hostPixels().data();
-#endif
+    imageData->data = canvas->getPixelBuffer();
 }
 
 // cleanup (main.cu:900-936)
 inline void cleanup() {
-#ifdef RTMI_REALTIME
-    if (detail::accumDevice()) (void)hipFree(detail::accumDevice());
-    if (detail::pixelsDevice()) (void)hipFree(detail::pixelsDevice());
-    detail::accumDevice() = nullptr;
-    detail::pixelsDevice() = nullptr;
-#endif
-    delete canvas;
+    delete canvas;  // its device buffers before the context
     canvas = nullptr;
     delete context;
     context = nullptr;
+    if (camera == detail::ownCamera().get()) camera = nullptr;
+    detail::ownCamera().reset();
     imageData.reset();
-    detail::hostPixels().clear();
-    sampleCount = 0;
-    renderingTime = 0.0f;
 }
 
 }  // namespace host

@@ -29,6 +29,63 @@ def build() -> str:
     return LIB_PATH
 
 
+class OracleCameraState(C.Structure):
+    """The restatement's Camera object (rt_oracle.c OrcCam: Camera.h:169-195's fields)."""
+    _fields_ = [(n, C.c_float * 3) for n in ("eye", "center", "up", "forward", "right", "true_up", "origin",
+                                             "horizontal", "vertical", "lower_left")] + \
+        [(n, C.c_float) for n in ("aspect_ratio", "fov", "scale", "viewport_height", "viewport_width",
+                                  "moving_speed", "aperture", "focus_distance", "lens_radius", "time0", "time1")] + \
+        [("dirty", C.c_int32)]
+
+
+class OracleCamera:
+    """Camera (Camera.h:12-196) in the restatement: the same method names as the product's."""
+
+    def __init__(self, eye, center, up, aspectRatio, fov=90.0, aperture=2.0, focusDistance=1.0,
+                 time0=0.0, time1=0.0):
+        self.L = lib()
+        self.state = OracleCameraState()
+        self.L.orc_cam_initialize(C.byref(self.state), f3(eye), f3(center), f3(up), aspectRatio, fov, aperture,
+                                  focusDistance, time0, time1)
+
+    def walk(self, d):
+        self.L.orc_cam_walk(C.byref(self.state), d)
+
+    def strafe(self, d):
+        self.L.orc_cam_strafe(C.byref(self.state), d)
+
+    def raise_(self, d):
+        self.L.orc_cam_raise(C.byref(self.state), d)
+
+    def yaw(self, d):
+        self.L.orc_cam_yaw(C.byref(self.state), d)
+
+    def pitch(self, d):
+        self.L.orc_cam_pitch(C.byref(self.state), d)
+
+    def orbit(self, target):
+        self.L.orc_cam_orbit(C.byref(self.state), f3(target))
+
+    def updateViewMatrix(self):
+        self.L.orc_cam_update_view_matrix(C.byref(self.state))
+
+    def setAperture(self, a):
+        self.L.orc_cam_set_aperture(C.byref(self.state), a)
+
+    def setDirty(self):
+        self.state.dirty = 1
+
+    def isDirty(self):
+        return bool(self.state.dirty)
+
+    def resetDiryFlag(self):
+        self.state.dirty = 0
+
+    def apply(self, scene: "OracleScene"):
+        """The scene renders with this camera's current view (the fields getRay reads)."""
+        self.L.orc_scene_camera_from(scene.h, C.byref(self.state))
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -75,6 +132,13 @@ def lib():
         L.orc_pt_powf.argtypes = [C.c_float, C.c_float]
         L.orc_pt_powf.restype = C.c_float
         L.orc_gamma_u8.argtypes = [fp, C.c_int64, C.POINTER(C.c_uint8)]
+        cs = C.POINTER(OracleCameraState)
+        L.orc_cam_initialize.argtypes = [cs, fp, fp, fp] + [C.c_float] * 6
+        L.orc_cam_update_view_matrix.argtypes = [cs]
+        for name in ("walk", "strafe", "raise", "yaw", "pitch", "set_aperture"):
+            getattr(L, "orc_cam_" + name).argtypes = [cs, C.c_float]
+        L.orc_cam_orbit.argtypes = [cs, fp]
+        L.orc_scene_camera_from.argtypes = [vp, cs]
         _lib = L
     return _lib
 
@@ -261,17 +325,27 @@ def preseed_materials(sc: OracleScene):
     sc.material(8, 3, (1.0, 1.0, 1.0), 5.0)
 
 
+def yaml_camera(cfg, width: int, height: int) -> OracleCamera:
+    """initialize()'s camera of a scene YAML (main.cu:632-638); `cfg` = the parsed file or its path."""
+    if isinstance(cfg, str):
+        import yaml
+
+        with open(cfg) as fh:
+            cfg = yaml.safe_load(fh)
+    cam = cfg["camera"]
+    eye, center, up = cam["eye"], cam["center"], cam["up"]
+    focus = lib().orc_length(f3(np.float32(center) - np.float32(eye)))  # (center - eye).length()
+    aspect = float(np.float32(width) / np.float32(height))              # Float(width) / height
+    return OracleCamera(eye, center, up, aspect, float(cam["fov"]), float(cam["aperture"]), focus, 0.0, 1.0)
+
+
 def yaml_scene(path: str, models_dir: str, width: int, height: int) -> OracleScene:
     import yaml
 
     with open(path) as fh:
         cfg = yaml.safe_load(fh)
     sc = OracleScene()
-    cam = cfg["camera"]
-    eye, center, up = cam["eye"], cam["center"], cam["up"]
-    focus = lib().orc_length(f3(np.float32(center) - np.float32(eye)))  # (center - eye).length()
-    aspect = float(np.float32(width) / np.float32(height))              # Float(width) / height
-    sc.camera(eye, center, up, aspect, float(cam["fov"]), float(cam["aperture"]), focus, 0.0, 1.0)
+    yaml_camera(cfg, width, height).apply(sc)
     preseed_materials(sc)
     for i, entry in enumerate(cfg["objects"]):
         key = next(iter(entry))

@@ -13,6 +13,9 @@
  *   rayColor ........................ main.cu:63-94
  *   hit (closest over objects) ...... main.cu:43-57
  *   Camera initialize/update/getRay . Camera.h:19-34, 86-103, 151-168
+ *   Camera moves (walk/strafe/raise/
+ *     yaw/pitch/orbit/setAperture) .. Camera.h:40-84, 105-113; rotateY / rotate
+ *                                     LinearAlgebra.h:84-109
  *   Ray ctor (inverse dir, signs) ... Ray.h:10-16
  *   HitResult::setFaceNormal ........ HitResult.h:15-18
  *   Sphere / MovingSphere ........... Sphere.cu:3-78
@@ -917,26 +920,127 @@ int orc_mesh_obj(Scene* s, int idx, const char* path, const float scale[3], cons
     return r;
 }
 
-/* Camera::initialize + updateViewMatrix (Camera.h:19-34, 86-103) */
+/* ---- the reference's Camera object (Camera.h:12-196): fields and methods ---- */
+typedef struct {
+    V3 eye, center, up, forward, right, true_up, origin, horizontal, vertical, lower_left;
+    float aspect_ratio, fov, scale, viewport_height, viewport_width;
+    float moving_speed, aperture, focus_distance, lens_radius, time0, time1;
+    int dirty;
+} OrcCam;
+
+/* rotateY (LinearAlgebra.h:84-87) with CUDATypes.h's `#define cos cosf` / `sin sinf`. */
+static V3 rotate_y_f(V3 v, float r) { return v3(v.x * cosf(r) + v.z * sinf(r), v.y, -v.x * sinf(r) + v.z * cosf(r)); }
+
+/* rotate (LinearAlgebra.h:94-109): axis-angle rows, each product left to right. */
+static V3 rotate_axis_f(V3 v, V3 axis, float radian) {
+    float c = cosf(radian), s_ = sinf(radian);
+    float n1 = axis.x, n2 = axis.y, n3 = axis.z;
+    float r0x = n1 * n1 * (1.0f - c) + c, r0y = n1 * n2 * (1.0f - c) - n3 * s_, r0z = n1 * n3 * (1.0f - c) + n2 * s_;
+    float r1x = n1 * n2 * (1.0f - c) + n3 * s_, r1y = n2 * n2 * (1.0f - c) + c, r1z = n2 * n3 * (1.0f - c) - n1 * s_;
+    float r2x = n1 * n3 * (1.0f - c) - n2 * s_, r2y = n2 * n3 * (1.0f - c) + n1 * s_, r2z = n3 * n3 * (1.0f - c) + c;
+    return v3(r0x * v.x + r0y * v.y + r0z * v.z, r1x * v.x + r1y * v.y + r1z * v.z, r2x * v.x + r2y * v.y + r2z * v.z);
+}
+
+/* updateLensRadius (Camera.h:110-113) */
+static void cam_update_lens_radius(OrcCam* c) {
+    c->dirty = 1;
+    c->lens_radius = c->aperture / 2.0f;
+}
+
+/* updateViewMatrix (Camera.h:86-103): only while dirty. */
+void orc_cam_update_view_matrix(OrcCam* c) {
+    if (!c->dirty) return;
+    c->scale = tanf(radians_f(c->fov / 2.0f));
+    c->viewport_height = 2.0f * c->scale;
+    c->viewport_width = c->viewport_height * c->aspect_ratio;
+    c->forward = vnorm(vsub(c->center, c->eye));
+    c->right = vnorm(vcross(c->forward, c->up));
+    c->true_up = vcross(c->right, c->forward);
+    c->origin = c->eye;
+    c->horizontal = vmul(vmul(c->right, c->viewport_width), c->focus_distance);   /* viewportWidth * right * focus */
+    c->vertical = vmul(vmul(c->true_up, c->viewport_height), c->focus_distance);  /* viewportHeight * trueUp * focus */
+    c->lower_left = vadd(vsub(vsub(c->origin, vdiv(c->horizontal, 2.0f)), vdiv(c->vertical, 2.0f)),
+                         vmul(c->forward, c->focus_distance));
+    cam_update_lens_radius(c);
+}
+
+/* initialize (Camera.h:19-34) */
+void orc_cam_initialize(OrcCam* c, const float eye[3], const float center[3], const float up[3], float aspect,
+                        float fov, float aperture, float focus, float t0, float t1) {
+    memset(c, 0, sizeof(*c));
+    c->eye = v3(eye[0], eye[1], eye[2]);
+    c->center = v3(center[0], center[1], center[2]);
+    c->up = v3(up[0], up[1], up[2]);
+    c->aspect_ratio = aspect;
+    c->fov = fov;
+    c->aperture = aperture;
+    c->focus_distance = focus;
+    c->moving_speed = 1.5f;
+    c->time0 = t0;
+    c->time1 = t1;
+    c->dirty = 1;
+    orc_cam_update_view_matrix(c);
+}
+
+/* walk / strafe / raise (Camera.h:40-56): eye += axis * movingSpeed * delta, center alike */
+static void cam_move(OrcCam* c, V3 axis, float delta) {
+    c->eye = vadd(c->eye, vmul(vmul(axis, c->moving_speed), delta));
+    c->center = vadd(c->center, vmul(vmul(axis, c->moving_speed), delta));
+    c->dirty = 1;
+}
+void orc_cam_walk(OrcCam* c, float delta) { cam_move(c, c->forward, delta); }
+void orc_cam_strafe(OrcCam* c, float delta) { cam_move(c, c->right, delta); }
+void orc_cam_raise(OrcCam* c, float delta) { cam_move(c, c->up, delta); }
+
+/* yaw (Camera.h:58-67) */
+void orc_cam_yaw(OrcCam* c, float delta) {
+    c->forward = vnorm(rotate_y_f(c->forward, delta));
+    c->right = vnorm(rotate_y_f(c->right, delta));
+    c->center = vadd(c->eye, c->forward);
+    c->dirty = 1;
+}
+
+/* pitch (Camera.h:69-76) */
+void orc_cam_pitch(OrcCam* c, float delta) {
+    c->forward = vnorm(rotate_axis_f(c->forward, c->right, delta));
+    c->center = vadd(c->eye, c->forward);
+    c->dirty = 1;
+}
+
+/* orbit (Camera.h:78-84) */
+void orc_cam_orbit(OrcCam* c, const float target[3]) {
+    float x = c->eye.x, z = c->eye.z;
+    c->eye.x = (x - target[0]) * cosf(0.01f) - (z - target[2]) * sinf(0.01f) + target[0];
+    c->eye.z = (x - target[0]) * sinf(0.01f) + (z - target[2]) * cosf(0.01f) + target[2];
+    c->dirty = 1;
+}
+
+/* setAperture (Camera.h:105-108) */
+void orc_cam_set_aperture(OrcCam* c, float aperture) {
+    c->aperture = aperture;
+    cam_update_lens_radius(c);
+}
+
+/* The fields getRay reads (Camera.h:151-168) become the scene's camera. */
+void orc_scene_camera_from(Scene* s, const OrcCam* c) {
+    s->origin = c->origin;
+    s->lower_left = c->lower_left;
+    s->horizontal = c->horizontal;
+    s->vertical = c->vertical;
+    s->right = c->right;
+    s->true_up = c->true_up;
+    s->lens_radius = c->lens_radius;
+    s->time0 = c->time0;
+    s->time1 = c->time1;
+    s->has_camera = 1;
+}
+
+/* Camera::initialize + updateViewMatrix (Camera.h:19-34, 86-103) as the scene's camera */
 int orc_camera(Scene* s, const float eye[3], const float center[3], const float up[3], float aspect,
                float fov, float aperture, float focus, float t0, float t1) {
-    float scale_ = tanf(radians_f(fov / 2.0f));
-    float vh = 2.0f * scale_;
-    float vw = vh * aspect;
-    V3 E = v3(eye[0], eye[1], eye[2]), C = v3(center[0], center[1], center[2]), U = v3(up[0], up[1], up[2]);
-    V3 forward = vnorm(vsub(C, E));
-    V3 right = vnorm(vcross(forward, U));
-    V3 true_up = vcross(right, forward);
-    s->origin = E;
-    s->horizontal = vmul(vmul(right, vw), focus);
-    s->vertical = vmul(vmul(true_up, vh), focus);
-    s->lower_left = vadd(vsub(vsub(E, vdiv(s->horizontal, 2.0f)), vdiv(s->vertical, 2.0f)), vmul(forward, focus));
-    s->right = right;
-    s->true_up = true_up;
-    s->lens_radius = aperture / 2.0f;
-    s->time0 = t0;
-    s->time1 = t1;
-    s->has_camera = 1;
+    OrcCam c;
+    orc_cam_initialize(&c, eye, center, up, aspect, fov, aperture, focus, t0, t1);
+    orc_scene_camera_from(s, &c);
     return 0;
 }
 

@@ -43,6 +43,10 @@ EXPORTS = [
     "rt_build_flags", "rt_set_bvh_cache", "rt_bvh_cache_stats",
     "rt_owned_rows", "rt_max_tile_rows", "rt_render_multi_device", "rt_comm_unique_id", "rt_comm_init",
     "rt_comm_destroy", "rt_gather_rows", "rt_assemble_rows", "rt_kernel_variant_name",
+    "rt_camera_initialize", "rt_camera_update_view_matrix", "rt_camera_walk", "rt_camera_strafe", "rt_camera_raise",
+    "rt_camera_yaw", "rt_camera_pitch", "rt_camera_orbit", "rt_camera_set_aperture", "rt_camera_apply",
+    "rt_get_camera", "rt_canvas_create", "rt_canvas_destroy", "rt_canvas_clear_accumulation",
+    "rt_canvas_accumulate", "rt_canvas_read_pixels", "rt_canvas_read_accumulation",
 ]
 
 # rtmi.h RT_SCHEDULE_* and RT_VARIANT_* (rt_render_stats.variant)
@@ -68,6 +72,15 @@ class RenderParams(C.Structure):
         ("lanes_per_pixel", C.c_int32), ("integrator", C.c_int32), ("flags", C.c_uint32),
         ("col_begin", C.c_int32), ("col_count", C.c_int32), ("schedule", C.c_int32),
     ]
+
+
+class CameraState(C.Structure):
+    """rt_camera_state (rtmi.h): the fields of the reference's Camera (Camera.h:169-195)."""
+    _fields_ = [(n, C.c_float * 3) for n in ("eye", "center", "up", "forward", "right", "true_up", "origin",
+                                             "horizontal", "vertical", "lower_left")] + \
+        [(n, C.c_float) for n in ("aspect_ratio", "fov", "scale", "viewport_height", "viewport_width",
+                                  "moving_speed", "aperture", "focus_distance", "lens_radius", "time0", "time1")] + \
+        [("dirty", C.c_int32)]
 
 
 class RenderStats(C.Structure):
@@ -154,6 +167,21 @@ def lib():
     L.rt_gamma_u8.argtypes = [fp, C.c_int64, C.POINTER(C.c_uint8)]
     L.rt_build_flags.restype = C.c_uint32
     L.rt_build_flags.argtypes = []
+    cs = C.POINTER(CameraState)
+    L.rt_camera_initialize.argtypes = [cs, fp, fp, fp] + [C.c_float] * 6
+    L.rt_camera_update_view_matrix.argtypes = [cs]
+    for name in ("walk", "strafe", "raise", "yaw", "pitch", "set_aperture"):
+        getattr(L, "rt_camera_" + name).argtypes = [cs, C.c_float]
+    L.rt_camera_orbit.argtypes = [cs, fp]
+    L.rt_camera_apply.argtypes = [vp, cs]
+    L.rt_get_camera.argtypes = [vp, cs]
+    L.rt_canvas_create.argtypes = [vp, i32, i32, C.POINTER(vp)]
+    L.rt_canvas_destroy.argtypes = [vp]
+    L.rt_canvas_destroy.restype = None
+    L.rt_canvas_clear_accumulation.argtypes = [vp]
+    L.rt_canvas_accumulate.argtypes = [vp, C.POINTER(RenderParams), C.c_uint32]
+    L.rt_canvas_read_pixels.argtypes = [vp, C.POINTER(C.c_uint8)]
+    L.rt_canvas_read_accumulation.argtypes = [vp, fp]
     L.rt_kernel_variant_name.argtypes = [C.c_uint32]
     L.rt_kernel_variant_name.restype = C.c_char_p
     L.rt_set_bvh_cache.argtypes = [vp, i32]

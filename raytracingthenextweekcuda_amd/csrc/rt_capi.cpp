@@ -548,14 +548,17 @@ static rt_status rt_pathtrace_bvh_image_impl(const rt_ctx* c, uint8_t* out, int6
 rt_status rt_camera(rt_ctx* c, const float eye[3], const float center[3], const float up[3],
                     float aspect, float fov, float aperture, float focus, float t0, float t1) {
     if (!c) return RT_ERR_INVALID;
-    if (!finite3(eye) || !finite3(center) || !finite3(up) || !isfinite(aspect) || !isfinite(fov) ||
-        !isfinite(aperture) || !isfinite(focus) || !isfinite(t0) || !isfinite(t1))
+    // Camera::initialize + updateViewMatrix (rt_camera.cpp), then the view getRay reads
+    rt_camera_state st;
+    if (rt_camera_initialize(&st, eye, center, up, aspect, fov, aperture, focus, t0, t1) != RT_OK)
         return fail(c, RT_ERR_INVALID, "camera: non-finite input");
-    c->scene.camera = rt::make_camera(rt::v3{eye[0], eye[1], eye[2]},
-                                      rt::v3{center[0], center[1], center[2]},
-                                      rt::v3{up[0], up[1], up[2]}, aspect, fov, aperture, focus,
-                                      t0, t1);
-    c->scene.has_camera = true;
+    return rt_camera_apply(c, &st);
+}
+
+rt_status rt_get_camera(const rt_ctx* c, rt_camera_state* out) {
+    if (!c || !out) return RT_ERR_INVALID;
+    if (!c->scene.has_camera) return RT_ERR_STATE;
+    *out = c->cam_state;
     return RT_OK;
 }
 
@@ -1292,4 +1295,85 @@ rt_status rt_mesh_vertices(const rt_ctx* c, int32_t index, float* out, int32_t m
         return RT_ERR_INVALID;
     }
 }
+}  // extern "C"
+
+// ---- the reference's Canvas buffers on the device (Canvas.h:20-200) ----
+struct rt_canvas {
+    rt_ctx* ctx;
+    int32_t device;  // rt_canvas_destroy needs only this (safe after the context is gone)
+    int32_t width, height;
+    float* accum;     // accumulationBuffer (float RGB)
+    uint8_t* pixels;  // pixelBuffer (Canvas::gamma RGB8)
+};
+
+extern "C" {
+
+rt_status rt_canvas_create(rt_ctx* c, int32_t width, int32_t height, rt_canvas** out) {
+    if (!c || !out) return RT_ERR_INVALID;
+    *out = nullptr;
+    if (c->device < 0) return fail(c, RT_ERR_NODEV, "canvas: context has no device");
+    if (width < 2 || height < 2 || (int64_t)width * height > ((int64_t)1 << 31))
+        return fail(c, RT_ERR_INVALID, "canvas: bad size");
+    RT_HIP(c, hipSetDevice(c->device));
+    const size_t n = (size_t)width * (size_t)height * 3;
+    rt_canvas* k = new (std::nothrow) rt_canvas{c, c->device, width, height, nullptr, nullptr};
+    if (!k) return fail(c, RT_ERR_OOM, "out of host memory");
+    if (hipMalloc((void**)&k->accum, n * sizeof(float)) != hipSuccess ||
+        hipMalloc((void**)&k->pixels, n) != hipSuccess || hipMemset(k->accum, 0, n * sizeof(float)) != hipSuccess ||
+        hipMemset(k->pixels, 0, n) != hipSuccess) {
+        (void)hipGetLastError();
+        rt_canvas_destroy(k);
+        return fail(c, RT_ERR_OOM, "canvas: device allocation failed");
+    }
+    *out = k;
+    return RT_OK;
+}
+
+void rt_canvas_destroy(rt_canvas* k) {
+    if (!k) return;
+    (void)hipSetDevice(k->device);
+    (void)hipFree(k->accum);
+    (void)hipFree(k->pixels);
+    delete k;
+}
+
+rt_status rt_canvas_clear_accumulation(rt_canvas* k) {
+    if (!k) return RT_ERR_INVALID;
+    rt_ctx* c = k->ctx;
+    RT_HIP(c, hipSetDevice(c->device));
+    RT_HIP(c, hipMemset(k->accum, 0, (size_t)k->width * k->height * 3 * sizeof(float)));
+    return RT_OK;
+}
+
+rt_status rt_canvas_accumulate(rt_canvas* k, const rt_render_params* p, uint32_t sample_count) {
+    if (!k || !p) return RT_ERR_INVALID;
+    rt_ctx* c = k->ctx;
+    if (p->width != k->width || p->height != k->height || p->row_world != 1 || p->col_count != 0)
+        return fail(c, RT_ERR_INVALID, "canvas_accumulate: params must cover the canvas's full frame");
+    if (sample_count == 0) return fail(c, RT_ERR_INVALID, "canvas_accumulate: sample_count must be >= 1");
+    rt_status s = rt_accumulate(c, p, k->accum, sample_count, k->pixels, nullptr);
+    if (s != RT_OK) return s;
+    RT_HIP(c, hipStreamSynchronize(nullptr));
+    s = rt_sync_stats(c, nullptr);
+    if (s != RT_OK) return s;
+    if (c->last.overflow) return fail(c, RT_ERR_OVERFLOW, "BVH traversal stack overflow");
+    return RT_OK;
+}
+
+rt_status rt_canvas_read_pixels(const rt_canvas* k, uint8_t* out) {
+    if (!k || !out) return RT_ERR_INVALID;
+    rt_ctx* c = k->ctx;
+    RT_HIP(c, hipSetDevice(c->device));
+    RT_HIP(c, hipMemcpy(out, k->pixels, (size_t)k->width * k->height * 3, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+rt_status rt_canvas_read_accumulation(const rt_canvas* k, float* out) {
+    if (!k || !out) return RT_ERR_INVALID;
+    rt_ctx* c = k->ctx;
+    RT_HIP(c, hipSetDevice(c->device));
+    RT_HIP(c, hipMemcpy(out, k->accum, (size_t)k->width * k->height * 3 * sizeof(float), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
 }  // extern "C"

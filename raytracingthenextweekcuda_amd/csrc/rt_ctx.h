@@ -36,6 +36,7 @@ struct rt_ctx {
     int n_mats = 0;
     unsigned long long* d_counters = nullptr;
     rt::CamRec* d_cam = nullptr;  // device copy of scene.camera read by the kernels
+    rt_camera_state cam_state{};  // the Camera object scene.camera was taken from (rt_get_camera)
     rt::CamRec cam_on_device{};   // what d_cam holds (valid when cam_uploaded)
     bool cam_uploaded = false;
     bool launched_before = false;  // ev1 has been recorded by a launch

@@ -31,30 +31,6 @@ inline v3 rotate_y(v3 v, float r) {
 }
 }  // namespace
 
-CamRec make_camera(v3 eye, v3 center, v3 up, float aspect, float fov, float aperture,
-                   float focus, float time0, float time1) {
-    // Camera::updateViewMatrix (Camera.h:86-103).
-    float sc = tanf(radians(fov / 2.0f));
-    float vh = 2.0f * sc;
-    float vw = vh * aspect;
-    v3 forward = normalize(sub(center, eye));
-    v3 right = normalize(cross(forward, up));
-    v3 true_up = cross(right, forward);
-    CamRec c;
-    c.origin = eye;
-    c.horizontal = scale(scale(right, vw), focus);   // viewportWidth * right * focusDistance
-    c.vertical = scale(scale(true_up, vh), focus);   // viewportHeight * trueUp * focusDistance
-    // origin - horizontal/2 - vertical/2 + forward*focusDistance, left to right.
-    c.lower_left = add(sub(sub(eye, divs(c.horizontal, 2.0f)), divs(c.vertical, 2.0f)),
-                       scale(forward, focus));
-    c.right = right;
-    c.true_up = true_up;
-    c.lens_radius = aperture / 2.0f;  // updateLensRadius (Camera.h:110-113)
-    c.time0 = time0;
-    c.time1 = time1;
-    return c;
-}
-
 TriRec make_triangle(v3 p0, v3 p1, v3 p2) {
     v3 e1 = sub(p1, p0);
     v3 e2 = sub(p2, p0);

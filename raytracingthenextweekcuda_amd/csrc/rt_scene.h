@@ -167,10 +167,6 @@ struct HostScene {
     void build_bvh_boxes(const std::vector<v3>& lo, const std::vector<v3>& hi, CFBvh& b);
 };
 
-// Camera::initialize + updateViewMatrix (Camera.h:19-34, 86-103) on the host.
-CamRec make_camera(v3 eye, v3 center, v3 up, float aspect, float fov, float aperture,
-                   float focus, float time0, float time1);
-
 // TriRec from three world-space vertices (prepareTriangleData, main.cu:334-343).
 TriRec make_triangle(v3 p0, v3 p1, v3 p2);
 

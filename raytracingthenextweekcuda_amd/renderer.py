@@ -22,7 +22,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import RT_OK, SCHEDULES, RenderParams, RenderStats, RTError, lib, variant_name
+from ._lib import RT_OK, SCHEDULES, CameraState, RenderParams, RenderStats, RTError, lib, variant_name
 
 _f3 = C.c_float * 3
 
@@ -60,29 +60,87 @@ def _mat_index(m) -> int:
 
 
 class Camera:
-    """Camera(eye, center, up, aspectRatio, fov=90, aperture=2, focusDistance=1,
-    time0=0, time1=0) — Camera.h:14-17 defaults."""
+    """The reference's Camera (Camera.h:12-196) over the library's restatement of its
+    methods (rt_camera_*, rtmi.h), so camera moves land on the reference's floats:
+    Camera(eye, center, up, aspectRatio, fov=90, aperture=2, focusDistance=1, time0=0,
+    time1=0) - the Camera.h:14-17 defaults. Renderer.set_camera hands the current view
+    (the fields getRay reads) to a context."""
 
     def __init__(self, eye, center, up, aspectRatio, fov=90.0, aperture=2.0,
                  focusDistance=1.0, time0=0.0, time1=0.0):
+        self.state = CameraState()
         self.initialize(eye, center, up, aspectRatio, fov, aperture, focusDistance, time0, time1)
+
+    @classmethod
+    def from_state(cls, state: CameraState) -> "Camera":
+        cam = cls.__new__(cls)
+        cam.state = CameraState()
+        C.pointer(cam.state)[0] = state
+        return cam
+
+    def _call(self, name, *args):
+        st = getattr(lib(), "rt_camera_" + name)(C.byref(self.state), *args)
+        if st != RT_OK:
+            raise RTError(st, f"rt_camera_{name}")
 
     def initialize(self, eye, center, up, aspectRatio, fov=90.0, aperture=2.0,
                    focusDistance=1.0, time0=0.0, time1=0.0):
-        self.eye, self.center, self.up = tuple(eye), tuple(center), tuple(up)
-        self.aspectRatio, self.fov, self.aperture = float(aspectRatio), float(fov), float(aperture)
-        self.focusDistance, self.time0, self.time1 = float(focusDistance), float(time0), float(time1)
-        self.bIsDirty = True
+        self._call("initialize", _v(eye), _v(center), _v(up), float(aspectRatio), float(fov), float(aperture),
+                   float(focusDistance), float(time0), float(time1))
+
+    # Camera.h:40-84
+    def walk(self, delta):
+        self._call("walk", float(delta))
+
+    def strafe(self, delta):
+        self._call("strafe", float(delta))
+
+    def raise_(self, delta):  # `raise` is a Python keyword
+        self._call("raise", float(delta))
+
+    def yaw(self, delta):
+        self._call("yaw", float(delta))
+
+    def pitch(self, delta):
+        self._call("pitch", float(delta))
+
+    def orbit(self, target):
+        self._call("orbit", _v(target))
+
+    def updateViewMatrix(self):
+        self._call("update_view_matrix")
 
     def setAperture(self, a):
-        self.aperture = float(a)
-        self.bIsDirty = True
+        self._call("set_aperture", float(a))
+
+    def getAperture(self):
+        return self.state.aperture
+
+    def getFOV(self):
+        return self.state.fov
+
+    def getMovingSpeed(self):
+        return self.state.moving_speed
+
+    def setDirty(self):
+        self.state.dirty = 1
 
     def isDirty(self):
-        return self.bIsDirty
+        return bool(self.state.dirty)
 
     def resetDiryFlag(self):  # reference spelling (Camera.h:147)
-        self.bIsDirty = False
+        self.state.dirty = 0
+
+    # the constructor's parameters
+    eye = property(lambda self: tuple(self.state.eye))
+    center = property(lambda self: tuple(self.state.center))
+    up = property(lambda self: tuple(self.state.up))
+    aspectRatio = property(lambda self: self.state.aspect_ratio)
+    fov = property(lambda self: self.state.fov)
+    aperture = property(lambda self: self.state.aperture)
+    focusDistance = property(lambda self: self.state.focus_distance)
+    time0 = property(lambda self: self.state.time0)
+    time1 = property(lambda self: self.state.time1)
 
 
 class Renderer:
@@ -223,11 +281,15 @@ class Renderer:
         return out
 
     def set_camera(self, cam: Camera):
+        """The context renders with the camera's current view (rt_camera_apply)."""
         self._camera = cam
-        self._check(self.L.rt_camera(self.ctx, _v(cam.eye), _v(cam.center), _v(cam.up),
-                                     cam.aspectRatio, cam.fov, cam.aperture, cam.focusDistance,
-                                     cam.time0, cam.time1))
-        cam.resetDiryFlag()
+        self._check(self.L.rt_camera_apply(self.ctx, C.byref(cam.state)))
+
+    def get_camera(self) -> Camera:
+        """The context's current Camera object (rt_get_camera): a scene file's camera too."""
+        st = CameraState()
+        self._check(self.L.rt_get_camera(self.ctx, C.byref(st)))
+        return Camera.from_state(st)
 
     def commit(self):
         self._check(self.L.rt_commit(self.ctx))

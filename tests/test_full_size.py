@@ -131,7 +131,8 @@ def test_full_frame_bunny_properties():
     assert segs == st["segments"]
 
 
-def test_full_frame_bunny_oracle_window():
+@pytest.mark.parametrize("y,c0", [(380, 480), (430, 480)])
+def test_full_frame_bunny_oracle_window(y, c0):
     """C4 at full size against the restatement: 128 bun_zipper pixels (two 64-pixel column
     windows on the bunny, rows 380 and 430) at 1024 x 1024, 512 spp, depth 8 - bit-exact,
     with equal segment counts. The restatement scans the 69,451 triangles brute force, as
@@ -146,17 +147,16 @@ def test_full_frame_bunny_oracle_window():
         rtmi.bunny_cornell_box(r, w, h)
         full = r.render(w, h, spp, depth, lanes_per_pixel=0)
         lanes = int(r.stats()["lanes_per_pixel"])
-        for y, c0 in ((380, 480), (430, 480)):
-            win = r.render(w, h, spp, depth, row_block=1, row_rank=y, row_world=h, lanes_per_pixel=lanes,
-                           col_begin=c0, col_count=64)
-            gst = r.stats()
-            assert gst["overflow"] == 0 and gst["samples"] == 64 * spp
-            assert np.array_equal(win[0], full[y, c0:c0 + 64]), y
-            want, ost = oracle.render(w, h, spp, depth, row_block=1, row_rank=y, row_world=h, threads=THREADS,
-                                      lanes_per_pixel=lanes, col_begin=c0, col_count=64)
-            assert ost["tri_tests"] > 64 * spp * 69451, "the window must see the bunny"
-            assert np.array_equal(win, want), (y, float(np.abs(win - want).max()))
-            assert gst["segments"] == ost["segments"], y
+        win = r.render(w, h, spp, depth, row_block=1, row_rank=y, row_world=h, lanes_per_pixel=lanes,
+                       col_begin=c0, col_count=64)
+        gst = r.stats()
+    assert gst["overflow"] == 0 and gst["samples"] == 64 * spp
+    assert np.array_equal(win[0], full[y, c0:c0 + 64]), y
+    want, ost = oracle.render(w, h, spp, depth, row_block=1, row_rank=y, row_world=h, threads=THREADS,
+                              lanes_per_pixel=lanes, col_begin=c0, col_count=64)
+    assert ost["tri_tests"] > 64 * spp * 69451, "the window must see the bunny"
+    assert np.array_equal(win, want), (y, float(np.abs(win - want).max()))
+    assert gst["segments"] == ost["segments"], y
 
 
 def test_full_frame_materialball_pathtrace():

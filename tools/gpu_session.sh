@@ -16,7 +16,7 @@ mkdir -p "$O"
 stop_if_fatal() { rc=$1; name=$2; echo "$name rc=$rc"; if [ "$rc" -ne 0 ]; then echo "fatal in $name"; exit "$rc"; fi; }
 export TMPDIR=/tmp
 if [ "${TESTS:-0}" = "1" ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread > "$O/pytest_gpu.log" 2>&1
+  timeout -k 10 600 python -u -m pytest tests -m gpu -v -rf --timeout 240 --timeout-method thread --durations 15 > "$O/pytest_gpu.log" 2>&1
   stop_if_fatal $? pytest
   timeout -k 10 240 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
   stop_if_fatal $? smoke
