@@ -489,6 +489,10 @@ def build_line(args, agg: dict, world: int, cpu=None) -> dict:
             "kernel_source_sha": sha,
             "parallelism": f"row-tiles x{world} + RCCL gather" if world > 1 else "single GPU",
             "segments_per_frame": int(segs / K),
+            # traversal work per traced segment (the library's event counters)
+            "per_segment": {"node_visits": round(agg["nodes"] / segs, 3) if segs else None,
+                            "tri_tests": round(agg["tri_tests"] / segs, 3) if segs else None,
+                            "box_tests": round(agg["box_tests"] / segs, 3) if segs else None},
             "msamples_per_s": round(W * H * args.spp / (dt / K) / 1e6, 3),
         },
         # one frame at a time, outside the timed region (N_ISOLATED frames, max over ranks):
