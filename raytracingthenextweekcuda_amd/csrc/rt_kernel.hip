@@ -466,6 +466,11 @@ __device__ __forceinline__ int lane_rank(uint64_t mask) {
 #define RT_BVH_STEAL 1  // cooperative (work-stealing) mesh traversal; 0 = per-lane mesh_bvh (A/B)
 #endif
 
+#ifndef RT_LEAF_BATCH
+#define RT_LEAF_BATCH 1  // BVH leaves' triangle tests deferred to wave-wide batches (0: per-lane leaf loops, A/B)
+#endif
+
+#if !(RT_LEAF_BATCH && RT_MESH_RUN)
 // Cooperative BVH mesh traversal (called by all 64 lanes). Per-lane traversal
 // leaves most of a wave idle while its deepest rays finish (VALU lane use was
 // 18% on the bunny). Here a lane whose work ran out takes the bottom (oldest,
@@ -608,6 +613,172 @@ __device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
     }
     __builtin_amdgcn_wave_barrier();
 }
+
+#endif
+
+#if RT_LEAF_BATCH && RT_MESH_RUN
+// mesh_bvh_coop with deferred leaf tests. A lane that reaches a leaf does not test its
+// triangles itself: it appends (triangle, ray owner) pairs to a per-wave LDS queue (up to
+// three per loop trip: a larger leaf keeps its lane for more trips) and walks on. Whenever
+// 64 pairs are queued the whole wave tests them at once - one pair per lane, the three
+// triangle loads of all 64 pairs in flight together - and merges each accepted hit into its
+// ray's LDS minimum of (t, mesh-local index), the same atomic-min the per-lane loops
+// published. Lanes then re-read their ray's minimum as the pruning bound. The per-lane leaf
+// loops were divergent (a wave's inner-node lanes waited for its leaf lanes) and serialised
+// one load latency per triangle; the candidate set is unchanged (a subtree is pruned only
+// against a bound some accepted triangle reached), so the winner is the sequential scan's.
+// Ray data for a pair comes from its owner lane's registers (o, d, h.t are not modified
+// while the wave traverses), so a lane carries only the current ray's origin and inverse.
+__device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
+                                              const uint32_t* __restrict__ tri_orig,
+                                              const BvhNode* __restrict__ nodes, uint32_t root, uint32_t base,
+                                              bool want, v3 o, v3 d, v3 inv, Hit& h, int32_t obj,
+                                              uint32_t order, uint32_t* wstack, WaveLds& W, int lane,
+                                              Counters& cnt, int cap) {
+    const uint64_t wm = __ballot(want);
+    if (wm == 0) return;
+    key_reset(W.key[lane]);
+    int owner = lane;
+    v3 ro = o, ri = inv;
+    float best = h.t;  // pruning bound for the current ray (its closestSoFar until a hit lands)
+    BvhNode cur = nodes[root];
+    bool has = want;
+    if (want) ++cnt.node_visits;
+    int sp = 0, bot = 0;         // pending subtrees: wstack[k * 64 + lane], bot <= k < sp
+    uint32_t qtail = 0, qdone = 0;  // wave-uniform positions in the pair queue W.slot (256 entries)
+    constexpr uint32_t kQ = (uint32_t)kMaxRun * 64u;
+    static_assert(kQ >= 256, "the pair queue holds 63 + 3 x 64 pairs");
+    __builtin_amdgcn_wave_barrier();
+    // test `count` (<= 64) queued pairs, one per lane (wave-uniform)
+    auto batch = [&](uint32_t count) {
+        const bool act = (uint32_t)lane < count;
+        const uint32_t e = act ? W.slot[(qdone + (uint32_t)lane) & (kQ - 1)] : 0u;
+        const uint32_t k = e >> 6;
+        const int own = (int)(e & 63u);
+        const v3 po{__shfl(o.x, own, 64), __shfl(o.y, own, 64), __shfl(o.z, own, 64)};
+        const v3 pd{__shfl(d.x, own, 64), __shfl(d.y, own, 64), __shfl(d.z, own, 64)};
+        const float pt0 = __shfl(h.t, own, 64);
+        if (act) {
+            const float t = tri_t(tris[k], po, pd);
+            if (t <= pt0)
+                atomicMin(&W.key[own], ((unsigned long long)__float_as_uint(t) << 32) | tri_orig[2 * k]);
+        }
+        qdone += count;
+        __builtin_amdgcn_wave_barrier();
+    };
+    for (;;) {
+        if (__ballot(has || sp > bot) == 0) break;
+        // steal: pair the r-th idle lane with the r-th lane that has a spare subtree
+        const bool idle = !has && sp == bot;
+        const bool spare = sp - bot >= (has ? 1 : 2);
+        const uint64_t im = __ballot(idle), vm = __ballot(spare);
+        if (im != 0 && vm != 0) {
+            const int nv = __popcll(vm), ni = __popcll(im);
+            if (spare) W.src[lane_rank(vm)] = lane;
+            __builtin_amdgcn_wave_barrier();
+            int vic = lane;
+            const bool thief = idle && lane_rank(im) < nv;
+            if (thief) vic = W.src[lane_rank(im)];
+            const int vt = __shfl(bot, vic, 64);  // the victim's oldest pending subtree
+            auto take = [&](float& x) {
+                const float v = __shfl(x, vic, 64);
+                if (thief) x = v;
+            };
+            {
+                const int v_owner = __shfl(owner, vic, 64);
+                if (thief) owner = v_owner;
+            }
+            take(ro.x); take(ro.y); take(ro.z);
+            take(ri.x); take(ri.y); take(ri.z);
+            take(best);
+            if (thief) {
+                const uint32_t entry = wstack[vt * 64 + vic];
+                best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
+                sp = bot = 0;
+                cur = nodes[entry];
+                ++cnt.node_visits;
+                float tn;
+                has = node_hit(cur, ro, ri, best, tn);
+            }
+            if (spare && lane_rank(vm) < ni) ++bot;  // robbed
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (!has && sp > bot) {
+            cur = nodes[wstack[(--sp) * 64 + lane]];
+            ++cnt.node_visits;
+            // the ray's best so far over all lanes (NaN while none: fminf keeps ours)
+            best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
+            float tn;
+            has = node_hit(cur, ro, ri, best, tn);  // best improved since the push?
+        }
+        if (!has && sp == bot) sp = bot = 0;
+        uint32_t lk = 0, ln = 0;  // this trip's leaf pairs: triangles lk .. lk + ln - 1
+        if (has) {
+            if (cur.b & 0x80000000u) {
+                const uint32_t nt = cur.b & 0x7FFFFFFFu;
+                ln = nt < 3u ? nt : 3u;
+                lk = cur.a;
+                if (nt > 3u) {  // a larger leaf keeps this lane for more trips
+                    cur.a += 3u;
+                    cur.b -= 3u;
+                } else {
+                    has = false;
+                }
+                cnt.tri_tests += ln;
+            } else {
+                const uint32_t il = cur.a, ir = cur.b;
+                const BvhNode nl = nodes[il], nr = nodes[ir];
+                cnt.node_visits += 2;
+                float tl, tr;
+                const bool hl = node_hit(nl, ro, ri, best, tl);
+                const bool hr = node_hit(nr, ro, ri, best, tr);
+                if (hl && hr) {
+                    if (sp + 1 > cap) {
+                        cnt.overflow();
+                        has = false;
+                        sp = bot = 0;
+                    } else {
+                        const bool left_first = tl <= tr;
+                        wstack[(sp++) * 64 + lane] = left_first ? ir : il;
+                        cur = left_first ? nl : nr;
+                    }
+                } else if (hl) {
+                    cur = nl;
+                } else if (hr) {
+                    cur = nr;
+                } else {
+                    has = false;
+                }
+            }
+        }
+        // enqueue the leaf pairs (converged): a lane's slots follow those of the lanes below it
+        const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
+        if (b1) {
+            const uint32_t at = qtail + (uint32_t)(lane_rank(b1) + lane_rank(b2) + lane_rank(b3));
+            const uint32_t tag = (uint32_t)owner;
+            for (uint32_t j = 0; j < ln; ++j) W.slot[(at + j) & (kQ - 1)] = ((lk + j) << 6) | tag;
+            qtail += (uint32_t)(__popcll(b1) + __popcll(b2) + __popcll(b3));
+            __builtin_amdgcn_wave_barrier();
+            if (qtail - qdone >= 64u) {
+                do {
+                    batch(64u);
+                } while (qtail - qdone >= 64u);
+                if (has || sp > bot) best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
+            }
+        }
+    }
+    if (qtail > qdone) batch(qtail - qdone);
+    __builtin_amdgcn_wave_barrier();
+    if (want) {
+        const unsigned long long key = W.key[lane];
+        if (key != ~0ull) {
+            const uint32_t k = tri_orig[2 * (base + (uint32_t)(key & 0xFFFFFFFFu)) + 1];
+            h.merge(__uint_as_float((uint32_t)(key >> 32)), order, false, obj, (int32_t)k);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+#endif
 
 // One object record (64 B) as a single wave-uniform scalar load; the same
 // helper serves per-lane loads of sphere-group members.
@@ -1862,7 +2033,7 @@ __device__ __forceinline__ void pt_leaf(const KTri* __restrict__ ktris,
 // reference's exact box decisions and a bound no tighter than the owner's, so
 // the winner is the one BVH_IntersectTriangles finds. The owner recomputes the
 // winner's hit point with pt_leaf's operations.
-__device__ __forceinline__ void pt_traverse_coop(const KTri* __restrict__ ktris,
+[[maybe_unused]] __device__ __forceinline__ void pt_traverse_coop(const KTri* __restrict__ ktris,
                                                  const CFNode* __restrict__ nodes,
                                                  const int32_t* __restrict__ tri_list, uint32_t* wstack,
                                                  unsigned long long* keys, int32_t* vlist, int lane, bool want,
@@ -2021,6 +2192,222 @@ __device__ __forceinline__ void pt_traverse_coop(const KTri* __restrict__ ktris,
     __builtin_amdgcn_wave_barrier();
 }
 
+#if RT_LEAF_BATCH
+// pt_traverse_coop with deferred leaf tests (as mesh_bvh_coop): leaves append (DFS list
+// position, ray owner) pairs to a per-wave LDS queue, three per lane and trip, and the wave
+// runs pt_leaf's Kuchkuda test on 64 queued pairs at once, one per lane, each merged into its
+// ray's LDS minimum of (distance^2, list position) - the reference's first-in-DFS tie rule.
+// Pairs take their ray (origin, direction, avoidSelf) from the owner lane's registers.
+__device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict__ ktris,
+                                                         const CFNode* __restrict__ nodes,
+                                                         const int32_t* __restrict__ tri_list, uint32_t* wstack,
+                                                         unsigned long long* keys, int32_t* vlist, uint32_t* queue,
+                                                         int lane, bool want, const PtRay& ray, int avoid_in,
+                                                         float len_in, float eps_in, PtBest& out, Counters& cnt,
+                                                         int cap) {
+    const uint64_t wm = __ballot(want);
+    if (wm == 0) return;
+    key_reset(keys[lane]);
+    int owner = lane;
+    PtRay r = ray;
+    float len_d = len_in, eps = eps_in;
+    float bhz = 3.40282347e+38f, bdist = 3.40282347e+38f;  // the current ray's best (pruning bound)
+    auto pruned = [&](float tw) { return tw > 0.0f && tw * len_d > bdist * 1.0001f + eps; };
+    auto refresh = [&]() {  // the ray's best over all lanes (NaN while none)
+        const float g = __uint_as_float((uint32_t)(keys[owner] >> 32));
+        if (g < bhz) {
+            bhz = g;
+            bdist = fsqrt(g);
+        }
+    };
+    CFNode cur = nodes[0];
+    bool has = want;
+    if (want) {
+        ++cnt.node_visits;
+        if (!(cur.u0 & 0x80000000u)) {
+            float tw, od;
+            has = pt_box_decide(cur, r, tw, od);
+        }
+    }
+    int sp = 0, bot = 0;
+    uint32_t qtail = 0, qdone = 0;  // wave-uniform positions in `queue` (256 entries)
+    __builtin_amdgcn_wave_barrier();
+    auto batch = [&](uint32_t count) {
+        const bool act = (uint32_t)lane < count;
+        const uint32_t e = act ? queue[(qdone + (uint32_t)lane) & 255u] : 0u;
+        const uint32_t i = e >> 6;
+        const int own = (int)(e & 63u);
+        const v3 po{__shfl(ray.o.x, own, 64), __shfl(ray.o.y, own, 64), __shfl(ray.o.z, own, 64)};
+        const v3 pd{__shfl(ray.d.x, own, 64), __shfl(ray.d.y, own, 64), __shfl(ray.d.z, own, 64)};
+        const int pav = __shfl(avoid_in, own, 64);
+        if (act) {
+            // pt_leaf's test for list position i (CUDAPathTracer.cu:258-345)
+            const int idx = tri_list[i];
+            if (pav != idx) {
+                const float4* T = reinterpret_cast<const float4*>(ktris + idx);
+                const float4 q0 = T[0], q1 = T[1], q2 = T[2], q3 = T[3];
+                const v3 nn{q0.x, q0.y, q0.z};
+                const float k = dot(nn, pd);
+                if (k != 0.0f) {
+                    const float sd = fdiv(q0.w - dot(nn, po), k);
+                    if (sd > 0.0f && sd > 1e-3f) {  // NUDGE_FACTOR
+                        const v3 hit = add(scale(pd, sd), po);
+                        if (!(dot(v3{q1.x, q1.y, q1.z}, hit) - q1.w < 0.0f) &&
+                            !(dot(v3{q2.x, q2.y, q2.z}, hit) - q2.w < 0.0f) &&
+                            !(dot(v3{q3.x, q3.y, q3.z}, hit) - q3.w < 0.0f)) {
+                            const v3 df = sub(po, hit);
+                            const float hz = df.x * df.x + df.y * df.y + df.z * df.z;  // distancesq
+                            atomicMin(&keys[own], ((unsigned long long)__float_as_uint(hz) << 32) | i);
+                        }
+                    }
+                }
+            }
+        }
+        qdone += count;
+        __builtin_amdgcn_wave_barrier();
+    };
+    for (;;) {
+        if (__ballot(has || sp > bot) == 0) break;
+        const bool idle = !has && sp == bot;
+        const bool spare = sp - bot >= (has ? 1 : 2);
+        const uint64_t im = __ballot(idle), vm = __ballot(spare);
+        if (im != 0 && vm != 0) {
+            const int nv = __popcll(vm), ni = __popcll(im);
+            if (spare) vlist[lane_rank(vm)] = lane;
+            __builtin_amdgcn_wave_barrier();
+            int vic = lane;
+            const bool thief = idle && lane_rank(im) < nv;
+            if (thief) vic = vlist[lane_rank(im)];
+            const int vb = __shfl(bot, vic, 64);
+            auto take = [&](float& x) {
+                const float v = __shfl(x, vic, 64);
+                if (thief) x = v;
+            };
+            {
+                const int v_owner = __shfl(owner, vic, 64);
+                const int v_exact = __shfl((int)r.exact, vic, 64);
+                if (thief) {
+                    owner = v_owner;
+                    r.exact = v_exact != 0;
+                }
+            }
+            take(r.o.x); take(r.o.y); take(r.o.z);
+            take(r.d.x); take(r.d.y); take(r.d.z);
+            take(r.inv.x); take(r.inv.y); take(r.inv.z);
+            take(r.pad_t.x); take(r.pad_t.y); take(r.pad_t.z);
+            take(len_d); take(eps); take(bhz); take(bdist);
+            if (thief) {
+                const uint32_t entry = wstack[vb * 64 + vic];
+                refresh();
+                sp = bot = 0;
+                cur = nodes[entry];
+                ++cnt.node_visits;
+                float tw, od;
+                pt_box_bounds(cur, r, tw, od);
+                has = !pruned(tw);
+            }
+            if (spare && lane_rank(vm) < ni) ++bot;  // robbed
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (!has && sp > bot) {
+            cur = nodes[wstack[(--sp) * 64 + lane]];
+            ++cnt.node_visits;
+            refresh();
+            float tw, od;
+            pt_box_bounds(cur, r, tw, od);
+            has = !pruned(tw);  // the best hit improved since the push
+        }
+        if (!has && sp == bot) sp = bot = 0;
+        uint32_t lk = 0, ln = 0;  // this trip's leaf pairs: list positions lk .. lk + ln - 1
+        if (has) {
+            if (cur.u0 & 0x80000000u) {
+                const uint32_t nt = cur.u0 & 0x7FFFFFFFu;
+                ln = nt < 3u ? nt : 3u;
+                lk = cur.u1;
+                if (nt > 3u) {  // a larger leaf keeps this lane for more trips
+                    cur.u1 += 3u;
+                    cur.u0 -= 3u;
+                } else {
+                    has = false;
+                }
+                cnt.tri_tests += ln;
+            } else {
+                const uint32_t i0 = cur.u0, i1 = cur.u1;
+                const CFNode c0 = nodes[i0], c1 = nodes[i1];
+                cnt.node_visits += 2;
+                float w0, o0, w1, o1;
+                bool h0, h1;
+                if (c0.u0 & 0x80000000u) {
+                    pt_box_bounds(c0, r, w0, o0);
+                    h0 = true;
+                } else {
+                    h0 = pt_box_decide(c0, r, w0, o0);
+                }
+                if (c1.u0 & 0x80000000u) {
+                    pt_box_bounds(c1, r, w1, o1);
+                    h1 = true;
+                } else {
+                    h1 = pt_box_decide(c1, r, w1, o1);
+                }
+                h0 = h0 && !pruned(w0);
+                h1 = h1 && !pruned(w1);
+                if (h0 && h1) {
+                    if (sp + 1 > cap) {
+                        cnt.overflow();
+                        has = false;
+                        sp = bot = 0;
+                    } else {
+                        const bool first0 = o0 <= o1;
+                        wstack[(sp++) * 64 + lane] = first0 ? i1 : i0;
+                        cur = first0 ? c0 : c1;
+                    }
+                } else if (h0) {
+                    cur = c0;
+                } else if (h1) {
+                    cur = c1;
+                } else {
+                    has = false;
+                }
+            }
+        }
+        const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
+        if (b1) {
+            const uint32_t at = qtail + (uint32_t)(lane_rank(b1) + lane_rank(b2) + lane_rank(b3));
+            for (uint32_t j = 0; j < ln; ++j) queue[(at + j) & 255u] = ((lk + j) << 6) | (uint32_t)owner;
+            qtail += (uint32_t)(__popcll(b1) + __popcll(b2) + __popcll(b3));
+            __builtin_amdgcn_wave_barrier();
+            if (qtail - qdone >= 64u) {
+                do {
+                    batch(64u);
+                } while (qtail - qdone >= 64u);
+                if (has || sp > bot) refresh();
+            }
+        }
+    }
+    if (qtail > qdone) batch(qtail - qdone);
+    __builtin_amdgcn_wave_barrier();
+    if (want) {
+        const unsigned long long key = keys[lane];
+        if (key != ~0ull) {
+            // the winner's hit point with pt_leaf's operations on the owner's ray
+            const int i = (int)(uint32_t)(key & 0xFFFFFFFFu);
+            const int idx = tri_list[i];
+            const float4 q0 = reinterpret_cast<const float4*>(ktris + idx)[0];
+            const v3 nn{q0.x, q0.y, q0.z};
+            const float k = dot(nn, ray.d);
+            const float sd = fdiv(q0.w - dot(nn, ray.o), k);
+            const float hz = __uint_as_float((uint32_t)(key >> 32));
+            out.hz = hz;
+            out.dist = fsqrt(hz);
+            out.i = i;
+            out.idx = idx;
+            out.hit = add(scale(ray.d, sd), ray.o);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+#endif
+
 }  // namespace
 
 template <bool kQueue>
@@ -2031,6 +2418,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
     extern __shared__ uint32_t dyn_stacks[];  // kWavesPerBlock x L.stack_depth x 64, sized at launch
     __shared__ unsigned long long pt_keys[kWavesPerBlock][64];  // per-ray minima (cooperative traversal)
     __shared__ int32_t pt_vlist[kWavesPerBlock][64];            // victims of a steal round
+#if RT_LEAF_BATCH
+    __shared__ uint32_t pt_queue[kWavesPerBlock][256];          // deferred leaf pairs
+#endif
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     uint32_t* stack = dyn_stacks + (size_t)wave * L.stack_depth * 64 + lane;
@@ -2109,8 +2499,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
             const float eps = 1e-5f * (1.0f + fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) + L.pt_scale);
             r.pad_t = v3{eps * fabsf(r.inv.x), eps * fabsf(r.inv.y), eps * fabsf(r.inv.z)};
 #if RT_BVH_STEAL
+#if RT_LEAF_BATCH
+            pt_traverse_coop_batched(ktris, nodes, tri_list, stack - lane, pt_keys[wave], pt_vlist[wave], pt_queue[wave],
+                                     lane, alive, r, avoid, fsqrt(dot(d, d)), eps, best, cnt, L.stack_depth);
+#else
             pt_traverse_coop(ktris, nodes, tri_list, stack - lane, pt_keys[wave], pt_vlist[wave], lane, alive, r,
                              avoid, fsqrt(dot(d, d)), eps, best, cnt, L.stack_depth);
+#endif
 #else
             if (alive)
                 pt_traverse(ktris, nodes, tri_list, stack, r, avoid, fsqrt(dot(d, d)), eps, best, cnt, L.stack_depth);
@@ -2388,7 +2783,7 @@ uint32_t kernel_build_flags() {
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
     !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || RT_PT_WAVES != 5 || \
-    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE || !RT_NOSPH_VARIANT || !RT_BVH_PARTS_VARIANT
+    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE || !RT_NOSPH_VARIANT || !RT_BVH_PARTS_VARIANT || !RT_LEAF_BATCH
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;

@@ -2,7 +2,7 @@
 # One GPU session on a gpurun box, from the repository root; everything lands in gpurun_out/$TAG/.
 #   TESTS=1   pytest -m gpu + smoke()
 #   BENCH=1   the default bench line (config 2, frame overlap, CPU baseline)
-#   SCENES    bench lines of these workloads (no CPU baseline)
+#   SCENES    bench lines of these workloads (no CPU baseline); ALT = A/B libraries run after each
 #   VALU      SQ_INSTS_VALU passes of these workloads (--no-overlap), for profiles/valu_issue.json
 #   TRAFFIC   FETCH_SIZE and WRITE_SIZE passes (separate runs), for profiles/pmc_traffic.json
 #   PROF      rocprofv3 --kernel-trace --stats of these workloads (--no-overlap)
@@ -28,6 +28,10 @@ fi
 for sc in ${SCENES:-}; do
   timeout -k 10 300 python bench.py --scene $sc --no-cpu-baseline ${BENCH_ARGS:-} > "$O/bench_$sc.log" 2>&1
   stop_if_fatal $? bench_$sc
+  for alt in ${ALT:-}; do  # A/B libraries of the same sources (RTMI_LIB), same box, interleaved
+    RTMI_LIB=raytracingthenextweekcuda_amd/$alt timeout -k 10 300 python bench.py --scene $sc --no-cpu-baseline ${BENCH_ARGS:-} > "$O/bench_${sc}_${alt%.so}.log" 2>&1
+    stop_if_fatal $? bench_${sc}_$alt
+  done
 done
 for sc in ${VALU:-}; do
   timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --output-format csv -d "$O/pmc_valu_$sc" -o pmc -- python3 bench.py --scene $sc --steps 2 --warmup 1 --no-cpu-baseline --no-overlap > "$O/pmc_valu_$sc.log" 2>&1
