@@ -45,14 +45,20 @@
  *  5. abs() in Plane::hit is the float abs (CUDA device semantics).
  * Compile with -ffp-contract=off and without fast-math.
  *
- * Pinning: the reference ships no golden radiance, RNG or timing data for this
- * path. The reference cannot be built here without writing
- * stand-ins for CUDA headers, which this project does not do. The oracle is
- * therefore pinned by (a) the reference's own data files (cube_small.obj
- * triangulation and the scene YAMLs), (b) Random123 Philox4x32-10 known-answer
- * vectors, and (c) hand-derived known answers for each hit/scatter function
- * (tests/test_oracle.py). Parity of the integrator's full radiance with the
- * reference's own binary is "parity partially pinned" (see DESIGN.md §2).
+ * Pinning: the reference ships no golden radiance, RNG or timing data for
+ * this path, and it cannot be built here without writing stand-ins for CUDA
+ * headers, which this project does not do. The oracle is pinned by
+ *   (a) the reference's own data files: its four `.bvh` caches (reproduced byte for byte by
+ *       the builder restated here and traversed as-is by the pathTrace restatement), the
+ *       cube_small.obj triangulation and the scene YAMLs;
+ *   (b) the reference's own renders: images/cornellbox0_512x512_10bounces_1024spp_*.png
+ *       (rayColor, cornellbox0.yaml) and render.png (the committed pathTrace setup), matched
+ *       statistically (8-bit global and 16x16-tile means within the measured Monte Carlo
+ *       noise; tests/test_reference_renders.py, with negative controls);
+ *   (c) Random123 Philox4x32-10 known-answer vectors and hand-derived known answers for each
+ *       hit / scatter function and for the Camera moves (tests/test_oracle.py,
+ *       tests/test_camera.py).
+ * cuRAND's XORWOW stream itself stays unpinned by construction (deviation 1).
  */
 #include <math.h>
 #include <stdint.h>

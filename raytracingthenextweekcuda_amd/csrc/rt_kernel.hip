@@ -903,7 +903,7 @@ __device__ __forceinline__ float sphere_candidate(const ObjRec& ob, v3 o, v3 d, 
 
 // Sphere group: per-lane traversal of the object BVH over the scene's spheres
 // (members are ObjRecs stored after the scan list, in leaf order).
-__device__ __forceinline__ void sphere_group(const ObjRec* __restrict__ objs,
+[[maybe_unused]] __device__ __forceinline__ void sphere_group(const ObjRec* __restrict__ objs,
                                              const BvhNode* __restrict__ nodes, uint32_t root,
                                              bool live, const Ray& ray, v3 inv, Hit& h,
                                              uint32_t* stack, Counters& cnt, int cap) {
@@ -955,6 +955,129 @@ __device__ __forceinline__ void sphere_group(const ObjRec* __restrict__ objs,
         }
     }
 }
+
+#ifndef RT_SG_BATCH
+#define RT_SG_BATCH 1  // sphere groups' leaf tests deferred to wave-wide batches (0: per-lane loops, A/B)
+#endif
+#if RT_SG_BATCH && RT_MESH_RUN
+// sphere_group with deferred leaf tests (as mesh_bvh_coop, without stealing): the traversal
+// loop is wave-uniform, and lanes at a leaf queue (member, ray owner) pairs that the wave tests
+// 64 at a time. Every group member is a sphere, and among spheres at the same t the sequential
+// hit() keeps the one of highest scan order (the inclusive test, Sphere.cu:25), which also
+// wins against any other object at that t (Hit::finish). So one LDS minimum per ray of
+// (t, ~order) over the accepted members (t <= the ray's closestSoFar) is all the group adds
+// to the ray's Hit: merging that one candidate gives what merging every member would. The
+// lane whose pair set the final minimum records the member (orders are unique) in W.src.
+__device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ objs,
+                                                     const BvhNode* __restrict__ nodes, uint32_t root,
+                                                     bool live, const Ray& ray, v3 inv, Hit& h, uint32_t* wstack,
+                                                     WaveLds& W, int lane, Counters& cnt, int cap) {
+    if (__ballot(live) == 0) return;
+    key_reset(W.key[lane]);
+    const v3 o = ray.o;
+    float best = h.t;  // pruning bound: the ray's closestSoFar, then its best member so far
+    BvhNode cur = nodes[root];
+    bool has = live;
+    if (live) ++cnt.node_visits;
+    int sp = 0;
+    uint32_t qtail = 0, qdone = 0;
+    constexpr uint32_t kQ = (uint32_t)kMaxRun * 64u;
+    __builtin_amdgcn_wave_barrier();
+    auto batch = [&](uint32_t count) {
+        const bool act = (uint32_t)lane < count;
+        const uint32_t e = act ? W.slot[(qdone + (uint32_t)lane) & (kQ - 1)] : 0u;
+        const uint32_t k = e >> 6;
+        const int own = (int)(e & 63u);
+        const v3 po{__shfl(ray.o.x, own, 64), __shfl(ray.o.y, own, 64), __shfl(ray.o.z, own, 64)};
+        const v3 pd{__shfl(ray.d.x, own, 64), __shfl(ray.d.y, own, 64), __shfl(ray.d.z, own, 64)};
+        const float ptime = __shfl(ray.time, own, 64), pt0 = __shfl(h.t, own, 64);
+        unsigned long long mine = ~0ull;
+        if (act) {
+            const ObjRec ob = load_obj(objs, (int)k);
+            cnt.grp += ob.type == kObjMovingSphere ? 0x10000u : 1u;
+            const float t = sphere_candidate(ob, po, pd, ptime);
+            if (t <= pt0) {
+                mine = ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)(~ob.order);
+                atomicMin(&W.key[own], mine);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (mine != ~0ull && W.key[own] == mine) W.src[own] = (int32_t)k;  // (t, order) is unique
+        qdone += count;
+        __builtin_amdgcn_wave_barrier();
+    };
+    for (;;) {
+        if (__ballot(has || sp > 0) == 0) break;
+        if (!has && sp > 0) {
+            cur = nodes[wstack[(--sp) * 64 + lane]];
+            ++cnt.node_visits;
+            float tn;
+            has = node_hit(cur, o, inv, best, tn);  // best improved since the push?
+        }
+        uint32_t lk = 0, ln = 0;
+        if (has) {
+            if (cur.b & 0x80000000u) {
+                const uint32_t nt = cur.b & 0x7FFFFFFFu;
+                ln = nt < 3u ? nt : 3u;
+                lk = cur.a;
+                if (nt > 3u) {
+                    cur.a += 3u;
+                    cur.b -= 3u;
+                } else {
+                    has = false;
+                }
+            } else {
+                const uint32_t il = cur.a, ir = cur.b;
+                const BvhNode nl = nodes[il], nr = nodes[ir];
+                cnt.node_visits += 2;
+                float tl, tr;
+                const bool hl = node_hit(nl, o, inv, best, tl);
+                const bool hr = node_hit(nr, o, inv, best, tr);
+                if (hl && hr) {
+                    if (sp + 1 > cap) {
+                        cnt.overflow();
+                        has = false;
+                        sp = 0;
+                    } else {
+                        const bool left_first = tl <= tr;
+                        wstack[(sp++) * 64 + lane] = left_first ? ir : il;
+                        cur = left_first ? nl : nr;
+                    }
+                } else if (hl) {
+                    cur = nl;
+                } else if (hr) {
+                    cur = nr;
+                } else {
+                    has = false;
+                }
+            }
+        }
+        const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
+        if (b1) {
+            const uint32_t at = qtail + (uint32_t)(lane_rank(b1) + lane_rank(b2) + lane_rank(b3));
+            for (uint32_t j = 0; j < ln; ++j) W.slot[(at + j) & (kQ - 1)] = ((lk + j) << 6) | (uint32_t)lane;
+            qtail += (uint32_t)(__popcll(b1) + __popcll(b2) + __popcll(b3));
+            __builtin_amdgcn_wave_barrier();
+            if (qtail - qdone >= 64u) {
+                do {
+                    batch(64u);
+                } while (qtail - qdone >= 64u);
+                if (has || sp > 0) best = fminf(best, __uint_as_float((uint32_t)(W.key[lane] >> 32)));
+            }
+        }
+    }
+    if (qtail > qdone) batch(qtail - qdone);
+    __builtin_amdgcn_wave_barrier();
+    if (live) {
+        const unsigned long long key = W.key[lane];
+        if (key != ~0ull) {
+            const int32_t k = W.src[lane];
+            h.merge(__uint_as_float((uint32_t)(key >> 32)), ~(uint32_t)(key & 0xFFFFFFFFu), true, k, -1);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+#endif
 
 // Constant medium bounded by a cube (rt_constant_medium, rtmi.h; "Ray Tracing:
 // The Next Week" ConstantMedium::hit with the boundary = the six two-sided faces
@@ -1152,7 +1275,11 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             // media to the kMed variant, so its register allocation need not cover this test)
             cand(live ? medium_candidate(ob, o, d, rng) : __builtin_nanf(""), false);
         } else if (kBvh && (kParts & 2) != 0) {  // kObjSphereGroup
+#if RT_SG_BATCH && RT_MESH_RUN
+            sphere_group_batched(S.objs, S.nodes, ob.u2, live, ray, inv, h, stack - lane, W, lane, cnt, S.stack_cap);
+#else
             sphere_group(S.objs, S.nodes, ob.u2, live, ray, inv, h, stack, cnt, S.stack_cap);
+#endif
         }
         if constexpr (kMed && RT_MED_MERGE1) h.merge_seq<kOrd>(tc, ob.order, tsph, i, -1);  // NaN: no candidate
     }
@@ -2783,7 +2910,7 @@ uint32_t kernel_build_flags() {
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
     !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || RT_PT_WAVES != 5 || \
-    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE || !RT_NOSPH_VARIANT || !RT_BVH_PARTS_VARIANT || !RT_LEAF_BATCH
+    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE || !RT_NOSPH_VARIANT || !RT_BVH_PARTS_VARIANT || !RT_LEAF_BATCH || !RT_SG_BATCH
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;

@@ -274,44 +274,31 @@ RT_HD void pt_sincosf(float x, float* sf, float* cf) {
     *cf = (float)c;
 }
 
-// A double constant materialised in an SGPR pair at its use (two scalar moves, off the VALU
-// port). gfx950's VOP3 double ops take no literals, so the compiler otherwise hoists every
-// constant of a series into registers for the whole persistent loop - where, in the media
-// kernel, they were spilled to scratch and reloaded per segment.
-#if defined(__HIP_DEVICE_COMPILE__)
-__device__ __forceinline__ double kd(double v) {
-    asm volatile("" : "+s"(v));
-    return v;
-}
-#else
-inline double kd(double v) { return v; }
-#endif
-
 // ln x for a positive float x, in double: exact frexp split, atanh series on
 // [sqrt(1/2), sqrt(2)), ln 2 in two parts.
 RT_HD double ln_pos_d(float xf) {
     int e;
     double m = frexp((double)xf, &e);  // exact: m in [0.5, 1)
-    if (m < kd(0.70710678118654752440)) {
+    if (m < 0.70710678118654752440) {
         m = m * 2.0;
         e = e - 1;
     }
     const double t = (m - 1.0) / (m + 1.0), t2 = t * t;
-    double p = kd(1.0 / 23.0);
-    p = p * t2 + kd(1.0 / 21.0);
-    p = p * t2 + kd(1.0 / 19.0);
-    p = p * t2 + kd(1.0 / 17.0);
-    p = p * t2 + kd(1.0 / 15.0);
-    p = p * t2 + kd(1.0 / 13.0);
-    p = p * t2 + kd(1.0 / 11.0);
-    p = p * t2 + kd(1.0 / 9.0);
-    p = p * t2 + kd(1.0 / 7.0);
-    p = p * t2 + kd(1.0 / 5.0);
-    p = p * t2 + kd(1.0 / 3.0);
+    double p = 1.0 / 23.0;
+    p = p * t2 + 1.0 / 21.0;
+    p = p * t2 + 1.0 / 19.0;
+    p = p * t2 + 1.0 / 17.0;
+    p = p * t2 + 1.0 / 15.0;
+    p = p * t2 + 1.0 / 13.0;
+    p = p * t2 + 1.0 / 11.0;
+    p = p * t2 + 1.0 / 9.0;
+    p = p * t2 + 1.0 / 7.0;
+    p = p * t2 + 1.0 / 5.0;
+    p = p * t2 + 1.0 / 3.0;
     p = p * t2 + 1.0;
     const double ln_m = 2.0 * t * p;
     const double de = (double)e;
-    return (de * kd(6.93147180369123816490e-01) + ln_m) + de * kd(1.90821492927058770002e-10);  // ln 2 hi, lo
+    return (de * 6.93147180369123816490e-01 + ln_m) + de * 1.90821492927058770002e-10;  // ln 2 hi, lo
 }
 
 RT_HD float pt_powf(float xf, float yf) {
