@@ -9,6 +9,9 @@
 // moves it before frame K (walk + yaw, Camera.h:40-67), which clears the accumulation
 // (camera->isDirty(), main.cu:877-881).
 // --device -1 runs initialize()/cleanup() only (scene build, no GPU).
+// --save FILE.pfm writes the realtime accumulation and counters after the last frame
+// (Canvas::writeAccumulation); --resume FILE.pfm restores them after initialize(), so the
+// frames continue the sample sequence where the saved run stopped.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -30,7 +33,7 @@ int main(int argc, char** argv) {
     }
     int w = 64, h = 48, frames = 1, moveAt = -1;
     bool explicitCamera = false;
-    std::string out = "main_driver.ppm";
+    std::string out = "main_driver.ppm", save, resume;
     H::sceneFile = argv[1];
     H::modelsDir = RTMI_ASSETS "/models";
     for (int i = 2; i < argc; ++i) {
@@ -47,6 +50,8 @@ int main(int argc, char** argv) {
         else if (a == "--move-at") moveAt = atoi(v);
         else if (a == "--device") H::device = atoi(v);
         else if (a == "--out") out = v;
+        else if (a == "--save") save = v;
+        else if (a == "--resume") resume = v;
         else return 2;
     }
     rtmi::Camera cam({0.0f, 0.0f, 1.25f}, {0.0f, 0.0f, -1.0f}, {0.0f, 1.0f, 0.0f}, (float)w / (float)h, 60.0f,
@@ -60,6 +65,12 @@ int main(int argc, char** argv) {
             H::cleanup();
             return 0;
         }
+        if (!resume.empty()) {
+            // the saved camera view: nothing to clear on the first frame
+            H::camera->updateViewMatrix();
+            H::camera->resetDiryFlag();
+            H::canvas->readAccumulation(resume, H::context->raw());
+        }
         for (int f = 0; f < frames; ++f) {
             if (f == moveAt) {
                 H::camera->walk(-0.05f);
@@ -69,6 +80,7 @@ int main(int argc, char** argv) {
             H::pathTracing();
             H::frameTime = std::chrono::duration<float>(std::chrono::steady_clock::now() - t0).count();
         }
+        if (!save.empty()) H::canvas->writeAccumulation(save);
         std::printf("frames %d samples %u\n", frames,
                     H::realtime ? H::canvas->getSampleCount() * (uint32_t)H::samplesPerFrame
                                 : (uint32_t)H::samplesPerFrame);

@@ -350,6 +350,9 @@ rt_status rt_canvas_accumulate(rt_canvas* canvas, const rt_render_params* params
 /* getPixelBuffer (Canvas.h:105-107): width x height x 3 uint8; the accumulation buffer. */
 rt_status rt_canvas_read_pixels(const rt_canvas* canvas, uint8_t* out_host);
 rt_status rt_canvas_read_accumulation(const rt_canvas* canvas, float* out_host);
+/* Restores an accumulation buffer read earlier (checkpoint / resume of a long progressive
+ * render: SURVEY §5's accumulation dump; the reference loses it on exit). */
+rt_status rt_canvas_write_accumulation(rt_canvas* canvas, const float* in_host);
 
 /* Builds the device scene tables and uploads them (replaces the device-side
  * `new` factories + cudaMemcpyToSymbol, main.cu:850-851). */

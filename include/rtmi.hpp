@@ -171,6 +171,51 @@ public:
         }
         return device_;
     }
+    // Checkpoint / resume of a progressive render (the reference loses its
+    // accumulation on exit): the accumulation sums as a little-endian PFM (bottom row first,
+    // the buffer's own order) and `<path>.json` with the counters. With a device canvas the
+    // device buffer is saved / restored; resuming continues the sample sequence where it stopped.
+    void writeAccumulation(const std::string& path) {
+        std::vector<float> acc = radiance;
+        if (device_ && rt_canvas_read_accumulation(device_, acc.data()) != RT_OK)
+            throw Error(RT_ERR_HIP, "writeAccumulation: device read failed");
+        FILE* f = std::fopen(path.c_str(), "wb");
+        if (!f) throw Error(RT_ERR_IO, "cannot write " + path);
+        std::fprintf(f, "PF\n%d %d\n-1.0\n", width, height);
+        const bool ok = std::fwrite(acc.data(), sizeof(float), acc.size(), f) == acc.size();
+        std::fclose(f);
+        FILE* j = std::fopen((path + ".json").c_str(), "w");
+        if (!ok || !j) throw Error(RT_ERR_IO, "cannot write " + path);
+        std::fprintf(j, "{\"sampleCount\": %u, \"renderingTime\": %.9g, \"width\": %d, \"height\": %d}\n",
+                     sampleCount, renderingTime, width, height);
+        std::fclose(j);
+    }
+    void readAccumulation(const std::string& path, rt_ctx* ctx = nullptr) {
+        FILE* f = std::fopen(path.c_str(), "rb");
+        if (!f) throw Error(RT_ERR_IO, "cannot read " + path);
+        int w = 0, h = 0;
+        float endian = 0.0f;
+        const bool head = std::fscanf(f, "PF %d %d %f", &w, &h, &endian) == 3 && std::fgetc(f) == '\n';
+        if (!head || w != width || h != height || endian >= 0.0f) {
+            std::fclose(f);
+            throw Error(RT_ERR_IO, path + ": not a little-endian RGB PFM of this canvas's size");
+        }
+        std::vector<float> acc(radiance.size());
+        const bool ok = std::fread(acc.data(), sizeof(float), acc.size(), f) == acc.size();
+        std::fclose(f);
+        FILE* j = std::fopen((path + ".json").c_str(), "r");
+        unsigned n = 0;
+        float t = 0.0f;
+        const bool meta = j && std::fscanf(j, " { \"sampleCount\": %u, \"renderingTime\": %f", &n, &t) == 2;
+        if (j) std::fclose(j);
+        if (!ok || !meta) throw Error(RT_ERR_IO, "cannot read " + path + " / its .json");
+        radiance = acc;
+        if (ctx && rt_canvas_write_accumulation(device(ctx), acc.data()) != RT_OK)
+            throw Error(RT_ERR_HIP, "readAccumulation: device write failed");
+        sampleCount = n;
+        scale = n ? 1.0f / n : 0.0f;
+        renderingTime = t;
+    }
     // writeToPPM (Canvas.h:116-139): top row first.
     void writeToPPM(const std::string& path) const {
         const std::vector<uint8_t>& px = pixelBuffer;

@@ -46,7 +46,7 @@ EXPORTS = [
     "rt_camera_initialize", "rt_camera_update_view_matrix", "rt_camera_walk", "rt_camera_strafe", "rt_camera_raise",
     "rt_camera_yaw", "rt_camera_pitch", "rt_camera_orbit", "rt_camera_set_aperture", "rt_camera_apply",
     "rt_get_camera", "rt_canvas_create", "rt_canvas_destroy", "rt_canvas_clear_accumulation",
-    "rt_canvas_accumulate", "rt_canvas_read_pixels", "rt_canvas_read_accumulation",
+    "rt_canvas_accumulate", "rt_canvas_read_pixels", "rt_canvas_read_accumulation", "rt_canvas_write_accumulation",
 ]
 
 # rtmi.h RT_SCHEDULE_* and RT_VARIANT_* (rt_render_stats.variant)
@@ -182,6 +182,7 @@ def lib():
     L.rt_canvas_accumulate.argtypes = [vp, C.POINTER(RenderParams), C.c_uint32]
     L.rt_canvas_read_pixels.argtypes = [vp, C.POINTER(C.c_uint8)]
     L.rt_canvas_read_accumulation.argtypes = [vp, fp]
+    L.rt_canvas_write_accumulation.argtypes = [vp, fp]
     L.rt_kernel_variant_name.argtypes = [C.c_uint32]
     L.rt_kernel_variant_name.restype = C.c_char_p
     L.rt_set_bvh_cache.argtypes = [vp, i32]

@@ -7,6 +7,7 @@ Canvas::writeToPNG (Canvas.h:141-154) and writeToPPM (:116-139).
 """
 from __future__ import annotations
 
+import json
 import struct
 import zlib
 
@@ -53,6 +54,51 @@ class Canvas:
 
     def writeToPNG(self, path: str, radiance: np.ndarray | None = None):
         write_png(path, self.pixels(radiance)[::-1])
+
+    # ---- checkpoint / resume of a progressive render (an accumulation dump; the
+    # reference keeps its accumulation only in device memory and loses it on exit) ----
+    def save(self, path: str, rows=None):
+        """The accumulation sums as a PFM (float32 RGB, bottom row first - the buffer's own row
+        order) plus `<path>.json` with the sample count and rendering time; `rows` (the global
+        row ids of a rank's tile) is recorded for per-rank dumps."""
+        write_pfm(path, self.accumulation)
+        meta = {"sampleCount": int(self.sampleCount), "renderingTime": float(self.renderingTime),
+                "width": self.width, "height": self.height}
+        if rows is not None:
+            meta["rows"] = [int(r) for r in rows]
+        with open(path + ".json", "w") as fh:
+            json.dump(meta, fh)
+
+    @classmethod
+    def load(cls, path: str) -> "Canvas":
+        with open(path + ".json") as fh:
+            meta = json.load(fh)
+        acc = read_pfm(path)
+        cv = cls(acc.shape[1], acc.shape[0])
+        cv.accumulation[...] = acc
+        cv.sampleCount = int(meta["sampleCount"])
+        cv.renderingTime = float(meta["renderingTime"])
+        cv.rows = meta.get("rows")
+        return cv
+
+
+def write_pfm(path: str, rgb: np.ndarray):
+    """Portable float map, little endian (scale -1), rows bottom to top as stored."""
+    rgb = np.ascontiguousarray(rgb, "<f4")
+    h, w, _ = rgb.shape
+    with open(path, "wb") as fh:
+        fh.write(f"PF\n{w} {h}\n-1.0\n".encode())
+        fh.write(rgb.tobytes())
+
+
+def read_pfm(path: str) -> np.ndarray:
+    with open(path, "rb") as fh:
+        if fh.readline().strip() != b"PF":
+            raise ValueError(f"{path}: not an RGB PFM")
+        w, h = (int(v) for v in fh.readline().split())
+        scale = float(fh.readline())
+        data = np.frombuffer(fh.read(), "<f4" if scale < 0 else ">f4", count=w * h * 3)
+    return data.reshape(h, w, 3).astype(np.float32)
 
 
 def write_png(path: str, rgb_u8_top_down: np.ndarray):

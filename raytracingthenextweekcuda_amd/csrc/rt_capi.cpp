@@ -1368,6 +1368,14 @@ rt_status rt_canvas_read_pixels(const rt_canvas* k, uint8_t* out) {
     return RT_OK;
 }
 
+rt_status rt_canvas_write_accumulation(rt_canvas* k, const float* in) {
+    if (!k || !in) return RT_ERR_INVALID;
+    rt_ctx* c = k->ctx;
+    RT_HIP(c, hipSetDevice(c->device));
+    RT_HIP(c, hipMemcpy(k->accum, in, (size_t)k->width * k->height * 3 * sizeof(float), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
 rt_status rt_canvas_read_accumulation(const rt_canvas* k, float* out) {
     if (!k || !out) return RT_ERR_INVALID;
     rt_ctx* c = k->ctx;
