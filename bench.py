@@ -216,12 +216,13 @@ def load_pmc_traffic(workload: str):
     return d.get(workload)
 
 
-KERNEL_SOURCES = ("rt_kernel.hip", "rt_kernel.h", "rt_math.h", "rt_scene.h", "rt_bvh.h")
+KERNEL_SOURCES = ("rt_kernel.hip", "rt_kernel.h", "rt_math.h", "rt_scene.h", "rt_bvh.h", "Makefile")  # + flags
 
 
 def kernel_source_sha() -> str:
-    """sha256 of the megakernel's sources (csrc/): a VALU or traffic profile recorded with
-    the same digest (tools/valu_summary.py, tools/pmc_summary.py) was taken of this code."""
+    """sha256 of the megakernel's sources and build flags (csrc/: the kernel TU, its headers, the
+    Makefile): a VALU or traffic profile recorded with the same digest (tools/valu_summary.py,
+    tools/pmc_summary.py) was taken of this code, compiled this way."""
     import hashlib
 
     h = hashlib.sha256()

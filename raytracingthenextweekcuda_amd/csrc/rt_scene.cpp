@@ -220,6 +220,16 @@ std::string load_obj_transformed(const std::string& path, v3 scl, v3 rot, v3 off
     return "";
 }
 
+// Leaf threshold of the BVHs over rayColor meshes and sphere groups (the reference's Recurse
+// makes a leaf below 4 entries, BVH.cpp:106). Any tree gives the same hits (the closest-hit merge
+// restates the sequential scan); the pathTrace tree is always the reference's.
+#ifndef RT_MESH_LEAF_MIN
+#define RT_MESH_LEAF_MIN 4
+#endif
+#ifndef RT_GROUP_LEAF_MIN
+#define RT_GROUP_LEAF_MIN 4
+#endif
+
 void HostScene::build_bvh(const std::vector<v3>& vs, const std::vector<uint32_t>& ix, CFBvh& b,
                           const std::string& cache_ply) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -230,8 +240,8 @@ void HostScene::build_bvh(const std::vector<v3>& vs, const std::vector<uint32_t>
         else if (got < 0) ++cache_rejected;
     }
     if (got <= 0) {
-        if (bvh_gpu && gpu_build_cf_bvh(bvh_device, vs, ix, b, 4, nullptr).empty()) ++bvh_gpu_builds;
-        else build_cf_bvh(vs, ix, b);
+        if (bvh_gpu && gpu_build_cf_bvh(bvh_device, vs, ix, b, RT_MESH_LEAF_MIN, nullptr).empty()) ++bvh_gpu_builds;
+        else build_cf_bvh(vs, ix, b, RT_MESH_LEAF_MIN);
         // rt_mesh_ply meshes read caches but never write them: a mesh placed with another
         // offset / maxCoord than the pathTrace scene's would overwrite that scene's cache (and
         // the two would keep rebuilding and replacing each other's file). The reference writes
@@ -243,8 +253,8 @@ void HostScene::build_bvh(const std::vector<v3>& vs, const std::vector<uint32_t>
 
 void HostScene::build_bvh_boxes(const std::vector<v3>& lo, const std::vector<v3>& hi, CFBvh& b) {
     const auto t0 = std::chrono::steady_clock::now();
-    if (bvh_gpu && gpu_build_cf_bvh_boxes(bvh_device, lo, hi, b, 4, nullptr).empty()) ++bvh_gpu_builds;
-    else build_cf_bvh_boxes(lo, hi, b);
+    if (bvh_gpu && gpu_build_cf_bvh_boxes(bvh_device, lo, hi, b, RT_GROUP_LEAF_MIN, nullptr).empty()) ++bvh_gpu_builds;
+    else build_cf_bvh_boxes(lo, hi, b, RT_GROUP_LEAF_MIN);
     bvh_build_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
