@@ -514,4 +514,59 @@ bool write_bvh_cache(const std::string& ply_path, const CFBvh& b) {
     return fclose(fp) == 0 && ok;
 }
 
+namespace {
+struct CFPairBuilder {
+    std::vector<CFNode>& nodes;
+    int max_pairs = 0;
+    bool empty_leaf = false;
+
+    uint32_t alloc() {
+        const size_t at = nodes.size();
+        nodes.resize(at + 2, CFNode{});
+        return (uint32_t)(at / 2);
+    }
+    void set(uint32_t q, CFNode l, uint32_t ref_l, uint32_t leaf_l, CFNode r, uint32_t ref_r, uint32_t leaf_r) {
+        l.u0 = ref_l;
+        l.u1 = leaf_l;
+        r.u0 = ref_r;
+        r.u1 = leaf_r;
+        nodes[2 * (size_t)q] = l;
+        nodes[2 * (size_t)q + 1] = r;
+    }
+    uint32_t leaf(CFNode box, uint32_t first, uint32_t count, int above) {
+        if (count <= kLeafRefMax) {
+            empty_leaf |= count == 0u;
+            max_pairs = std::max(max_pairs, above);
+            return kLeafRef | ((count - 1u) << 27) | first;
+        }
+        const uint32_t q = alloc();  // a larger leaf: two halves under the leaf's box
+        const uint32_t half = count / 2u;
+        const uint32_t l = leaf(box, first, half, above + 1), r = leaf(box, first + half, count - half, above + 1);
+        set(q, box, l, 1u, box, r, 1u);
+        return q;
+    }
+    uint32_t node(uint32_t i, int above) {
+        const CFNode n = nodes[i];
+        if (n.u0 & 0x80000000u) return leaf(n, n.u1, n.u0 & 0x7FFFFFFFu, above);
+        const uint32_t q = alloc();
+        const uint32_t l = node(n.u0, above + 1), r = node(n.u1, above + 1);
+        const CFNode a = nodes[n.u0], b = nodes[n.u1];
+        set(q, a, l, (a.u0 >> 31), b, r, (b.u0 >> 31));
+        return q;
+    }
+};
+}  // namespace
+
+uint32_t cf_child_pairs(std::vector<CFNode>& nodes, int* max_pairs, bool* empty_leaf) {
+    *max_pairs = 0;
+    *empty_leaf = false;
+    if (nodes.empty()) return 0;
+    if (nodes.size() & 1u) nodes.push_back(CFNode{});
+    CFPairBuilder pb{nodes};
+    const uint32_t root = pb.node(0, 0);
+    *max_pairs = pb.max_pairs;
+    *empty_leaf = pb.empty_leaf;
+    return root;
+}
+
 }  // namespace rt

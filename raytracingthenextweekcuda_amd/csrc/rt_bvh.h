@@ -46,6 +46,21 @@ struct CFBvh {
     int max_depth = 0;
 };
 
+// Child-pair references of the batched traversals (rt_scene.cpp build_mesh_pairs,
+// cf_child_pairs): a pair index q (the children's records at nodes[2q], nodes[2q + 1]), or
+// kLeafRef | (count - 1) << 27 | first triangle / member for a leaf of 1..kLeafRefMax.
+constexpr uint32_t kLeafRef = 0x80000000u;
+constexpr uint32_t kLeafRefMax = 16;
+
+// Child-pair records of a pathTrace BVH, appended to `nodes` from an even index (each pair
+// one aligned 64 B line): per inner node (and per half of a leaf larger than kLeafRefMax)
+// its two children's records with bottom/top as built, u0 = the child's reference and
+// u1 = 1 when the child's box is a leaf's box (BVH_IntersectTriangles never box-tests a
+// leaf: only the distance pruning applies to it), else 0. Returns the root's reference;
+// *max_pairs = pair records on the longest root-to-leaf path (the stack entries a lane may
+// need), *empty_leaf = a leaf without triangles was found.
+uint32_t cf_child_pairs(std::vector<CFNode>& nodes, int* max_pairs, bool* empty_leaf);
+
 // CreateBVH + CreateCFBVH over triangles given by vertex index triples.
 // leaf_min_split = 4 is the reference's tree (byte-identical `.bvh` caches);
 // rayColor meshes, which the reference brute-forces, may use larger leaves.

@@ -94,6 +94,8 @@ void free_pathtrace(rt_ctx* c) {
     c->d_pt_list = nullptr;
     c->pt_ready = false;
     c->pt_tris = 0;
+    c->pt_root_ref = 0;
+    c->pt_pair_depth = 0;
 }
 
 }  // namespace
@@ -512,6 +514,14 @@ static rt_status rt_process_triangle_data_impl(rt_ctx* c, const float offset[3],
             return fail(c, RT_ERR_INVALID, "pathTrace BVH depth " + std::to_string(b.max_depth) +
                                                " exceeds the traversal stack (" + std::to_string(rt::kBvhStackDepth) + ")");
     }
+    std::vector<rt::CFNode> dev_nodes = b.nodes;  // + the traversal's child-pair records
+    int pair_depth = 0;
+    bool empty_leaf = false;
+    const uint32_t root_ref = rt::cf_child_pairs(dev_nodes, &pair_depth, &empty_leaf);
+    if (empty_leaf) return fail(c, RT_ERR_INVALID, "pathTrace BVH with an empty leaf");
+    if (pair_depth > rt::kBvhStackDepth)
+        return fail(c, RT_ERR_INVALID, "pathTrace BVH pair depth " + std::to_string(pair_depth) +
+                                           " exceeds the traversal stack (" + std::to_string(rt::kBvhStackDepth) + ")");
     if (out_info) {
         out_info[0] = (int32_t)kt.size();
         out_info[1] = (int32_t)b.nodes.size();
@@ -526,11 +536,13 @@ static rt_status rt_process_triangle_data_impl(rt_ctx* c, const float offset[3],
             return hipMemcpy(*dst, vec.data(), bytes, hipMemcpyHostToDevice);
         };
         RT_HIP(c, up(&c->d_pt_tris, kt));
-        RT_HIP(c, up(&c->d_pt_nodes, b.nodes));
+        RT_HIP(c, up(&c->d_pt_nodes, dev_nodes));
         RT_HIP(c, up(&c->d_pt_list, b.tri_index));
     }
     c->pt_tris = (int)kt.size();
     c->pt_scale = scale_max;
+    c->pt_root_ref = root_ref;
+    c->pt_pair_depth = pair_depth;
     c->pt_bvh = std::move(b);
     c->pt_ready = true;
     return RT_OK;
@@ -683,9 +695,11 @@ rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& 
     L.pt_has_mesh = c->pt_tris > 0 ? 1 : 0;
     // LDS traversal stacks hold one pending subtree per level below the root: the scene's
     // deepest BVH (rayColor meshes and sphere groups, or the pathTrace tree) sizes them
-    const int depth = p->integrator == RT_INTEGRATOR_PATHTRACE ? c->pt_bvh.max_depth : c->scene.bvh_max_depth;
+    const int depth = p->integrator == RT_INTEGRATOR_PATHTRACE ? std::max(c->pt_bvh.max_depth, c->pt_pair_depth)
+                                                                : c->scene.bvh_max_depth;
     L.stack_depth = depth > 0 ? depth : 1;
     L.pt_scale = c->pt_scale;
+    L.pt_root_ref = c->pt_root_ref;
     return RT_OK;
 }
 

@@ -66,7 +66,9 @@ struct rt_ctx {
     float pt_scale = 0.0f;  // max |coordinate| of the processed triangles
     rt::CFBvh pt_bvh;  // host copy (the `.bvh` cache image source)
     rt::KTri* d_pt_tris = nullptr;
-    rt::CFNode* d_pt_nodes = nullptr;
+    rt::CFNode* d_pt_nodes = nullptr;  // the tree's nodes, then its child-pair records (cf_child_pairs)
+    uint32_t pt_root_ref = 0;          // the root's child-pair reference
+    int pt_pair_depth = 0;             // pair records on the longest root-to-leaf path
     int32_t* d_pt_list = nullptr;
     double pt_build_ms = 0.0;
     int pt_gpu_builds = 0;

@@ -51,6 +51,7 @@ struct RenderLaunch {
                               // ordered traversal holds at most one pending subtree per level below the
                               // root, so the LDS stacks are sized per scene (dynamic LDS)
     float pt_scale;           // pathTrace: max |coordinate| of the triangles
+    uint32_t pt_root_ref;     // pathTrace: the root's child-pair reference (rt_bvh.h cf_child_pairs)
     // Pixel output (Canvas.h:58-98): accumulate = 0 writes the mean color/spp to
     // `out` (and gamma(mean) to u8 when set: writePixel); accumulate = 1 adds the
     // sample sum to `out` (accumulatePixel) and, when u8 is set, writes

@@ -629,7 +629,7 @@ __device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
 // against a bound some accepted triangle reached), so the winner is the sequential scan's.
 // Ray data for a pair comes from its owner lane's registers (o, d, h.t are not modified
 // while the wave traverses), so a lane carries only the current ray's origin and inverse.
-__device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
+[[maybe_unused]] __device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
                                               const uint32_t* __restrict__ tri_orig,
                                               const BvhNode* __restrict__ nodes, uint32_t root, uint32_t base,
                                               bool want, v3 o, v3 d, v3 inv, Hit& h, int32_t obj,
@@ -750,6 +750,162 @@ __device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
                     has = false;
                 }
             }
+        }
+        // enqueue the leaf pairs (converged): a lane's slots follow those of the lanes below it
+        const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
+        if (b1) {
+            const uint32_t at = qtail + (uint32_t)(lane_rank(b1) + lane_rank(b2) + lane_rank(b3));
+            const uint32_t tag = (uint32_t)owner;
+            for (uint32_t j = 0; j < ln; ++j) W.slot[(at + j) & (kQ - 1)] = ((lk + j) << 6) | tag;
+            qtail += (uint32_t)(__popcll(b1) + __popcll(b2) + __popcll(b3));
+            __builtin_amdgcn_wave_barrier();
+            if (qtail - qdone >= 64u) {
+                do {
+                    batch(64u);
+                } while (qtail - qdone >= 64u);
+                if (has || sp > bot) best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
+            }
+        }
+    }
+    if (qtail > qdone) batch(qtail - qdone);
+    __builtin_amdgcn_wave_barrier();
+    if (want) {
+        const unsigned long long key = W.key[lane];
+        if (key != ~0ull) {
+            const uint32_t k = tri_orig[2 * (base + (uint32_t)(key & 0xFFFFFFFFu)) + 1];
+            h.merge(__uint_as_float((uint32_t)(key >> 32)), order, false, obj, (int32_t)k);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+#endif
+
+#ifndef RT_BVH_PAIRS
+#define RT_BVH_PAIRS 1  // mesh BVHs traversed over child-pair records (0: node records, A/B)
+#endif
+#if RT_BVH_PAIRS && RT_LEAF_BATCH && RT_MESH_RUN
+// The batched mesh traversal over child-pair records (rt_scene.cpp build_mesh_pairs). A lane
+// holds one reference word instead of a node: a pair index, whose 64 B record carries both
+// children's boxes and references, or a leaf reference (first triangle, count). An inner
+// step is one aligned 64 B load and two box tests; the nearer hit child becomes the lane's
+// reference and the farther one is pushed as a word. Popping, stealing and reaching a leaf
+// load nothing: a leaf's triangles are queued for the wave's batched tests (up to three per
+// trip, as in the node-record traversal) in the same trip that reached it. The node-record
+// version re-loaded and re-tested every popped node before loading its children - two
+// dependent loads per pop. A popped entry is not re-tested against the improved bound
+// (its children are, on their pair load); pruning stays conservative, so the candidate set
+// still contains the sequential scan's winner and the (t, index) minimum picks it.
+__device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
+                                               const uint32_t* __restrict__ tri_orig,
+                                               const BvhNode* __restrict__ nodes, uint32_t root, uint32_t base,
+                                               bool want, v3 o, v3 d, v3 inv, Hit& h, int32_t obj,
+                                               uint32_t order, uint32_t* wstack, WaveLds& W, int lane,
+                                               Counters& cnt, int cap) {
+    const uint64_t wm = __ballot(want);
+    if (wm == 0) return;
+    key_reset(W.key[lane]);
+    int owner = lane;
+    v3 ro = o, ri = inv;
+    float best = h.t;  // pruning bound for the current ray (its closestSoFar until a hit lands)
+    uint32_t cur = root;  // pair index or leaf reference
+    bool has = want;
+    int sp = 0, bot = 0;            // pending references: wstack[k * 64 + lane], bot <= k < sp
+    uint32_t qtail = 0, qdone = 0;  // wave-uniform positions in the pair queue W.slot (256 entries)
+    constexpr uint32_t kQ = (uint32_t)kMaxRun * 64u;
+    static_assert(kQ >= 256, "the pair queue holds 63 + 3 x 64 pairs");
+    __builtin_amdgcn_wave_barrier();
+    // test `count` (<= 64) queued pairs, one per lane (wave-uniform)
+    auto batch = [&](uint32_t count) {
+        const bool act = (uint32_t)lane < count;
+        const uint32_t e = act ? W.slot[(qdone + (uint32_t)lane) & (kQ - 1)] : 0u;
+        const uint32_t k = e >> 6;
+        const int own = (int)(e & 63u);
+        const v3 po{__shfl(o.x, own, 64), __shfl(o.y, own, 64), __shfl(o.z, own, 64)};
+        const v3 pd{__shfl(d.x, own, 64), __shfl(d.y, own, 64), __shfl(d.z, own, 64)};
+        const float pt0 = __shfl(h.t, own, 64);
+        if (act) {
+            const float t = tri_t(tris[k], po, pd);
+            if (t <= pt0)
+                atomicMin(&W.key[own], ((unsigned long long)__float_as_uint(t) << 32) | tri_orig[2 * k]);
+        }
+        qdone += count;
+        __builtin_amdgcn_wave_barrier();
+    };
+    for (;;) {
+        if (__ballot(has || sp > bot) == 0) break;
+        // steal: pair the r-th idle lane with the r-th lane that has a spare reference
+        const bool idle = !has && sp == bot;
+        const bool spare = sp - bot >= (has ? 1 : 2);
+        const uint64_t im = __ballot(idle), vm = __ballot(spare);
+        if (im != 0 && vm != 0) {
+            const int nv = __popcll(vm), ni = __popcll(im);
+            if (spare) W.src[lane_rank(vm)] = lane;
+            __builtin_amdgcn_wave_barrier();
+            int vic = lane;
+            const bool thief = idle && lane_rank(im) < nv;
+            if (thief) vic = W.src[lane_rank(im)];
+            const int vt = __shfl(bot, vic, 64);  // the victim's oldest pending reference
+            auto take = [&](float& x) {
+                const float v = __shfl(x, vic, 64);
+                if (thief) x = v;
+            };
+            {
+                const int v_owner = __shfl(owner, vic, 64);
+                if (thief) owner = v_owner;
+            }
+            take(ro.x); take(ro.y); take(ro.z);
+            take(ri.x); take(ri.y); take(ri.z);
+            take(best);
+            if (thief) {
+                cur = wstack[vt * 64 + vic];
+                best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
+                sp = bot = 0;
+                has = true;
+            }
+            if (spare && lane_rank(vm) < ni) ++bot;  // robbed
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (!has && sp > bot) {
+            cur = wstack[(--sp) * 64 + lane];
+            has = true;
+            // the ray's best so far over all lanes (NaN while none: fminf keeps ours)
+            best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
+        }
+        if (!has && sp == bot) sp = bot = 0;
+        if (has && !(cur & kLeafRef)) {
+            const BvhNode nl = nodes[2 * (size_t)cur], nr = nodes[2 * (size_t)cur + 1];
+            cnt.node_visits += 2;
+            float tl, tr;
+            const bool hl = node_hit(nl, ro, ri, best, tl);
+            const bool hr = node_hit(nr, ro, ri, best, tr);
+            if (hl && hr) {
+                if (sp + 1 > cap) {
+                    cnt.overflow();
+                    has = false;
+                    sp = bot = 0;
+                } else {
+                    const bool left_first = tl <= tr;
+                    wstack[(sp++) * 64 + lane] = left_first ? nr.a : nl.a;
+                    cur = left_first ? nl.a : nr.a;
+                }
+            } else if (hl) {
+                cur = nl.a;
+            } else if (hr) {
+                cur = nr.a;
+            } else {
+                has = false;
+            }
+        }
+        uint32_t lk = 0, ln = 0;  // this trip's leaf pairs: triangles lk .. lk + ln - 1
+        if (has && (cur & kLeafRef)) {
+            const uint32_t nt = ((cur >> 27) & 15u) + 1u;
+            lk = cur & 0x07FFFFFFu;
+            ln = nt < 3u ? nt : 3u;
+            if (nt > 3u)  // a larger leaf keeps this lane for more trips
+                cur = kLeafRef | ((nt - 4u) << 27) | (lk + 3u);
+            else
+                has = false;
+            cnt.tri_tests += ln;
         }
         // enqueue the leaf pairs (converged): a lane's slots follow those of the lanes below it
         const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
@@ -959,6 +1115,9 @@ __device__ __forceinline__ float sphere_candidate(const ObjRec& ob, v3 o, v3 d, 
 #ifndef RT_SG_BATCH
 #define RT_SG_BATCH 1  // sphere groups' leaf tests deferred to wave-wide batches (0: per-lane loops, A/B)
 #endif
+#ifndef RT_SG_PAIRS
+#define RT_SG_PAIRS 1  // ... over child-pair records (as mesh_bvh_pairs; 0: node records, A/B)
+#endif
 #if RT_SG_BATCH && RT_MESH_RUN
 // sphere_group with deferred leaf tests (as mesh_bvh_coop, without stealing): the traversal
 // loop is wave-uniform, and lanes at a leaf queue (member, ray owner) pairs that the wave tests
@@ -976,9 +1135,13 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
     key_reset(W.key[lane]);
     const v3 o = ray.o;
     float best = h.t;  // pruning bound: the ray's closestSoFar, then its best member so far
+#if RT_SG_PAIRS
+    uint32_t cur = root;  // pair index or leaf reference (root: the group's root pair)
+#else
     BvhNode cur = nodes[root];
-    bool has = live;
     if (live) ++cnt.node_visits;
+#endif
+    bool has = live;
     int sp = 0;
     uint32_t qtail = 0, qdone = 0;
     constexpr uint32_t kQ = (uint32_t)kMaxRun * 64u;
@@ -1008,6 +1171,46 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
     };
     for (;;) {
         if (__ballot(has || sp > 0) == 0) break;
+#if RT_SG_PAIRS
+        if (!has && sp > 0) {
+            cur = wstack[(--sp) * 64 + lane];
+            has = true;
+        }
+        if (has && !(cur & kLeafRef)) {
+            const BvhNode nl = nodes[2 * (size_t)cur], nr = nodes[2 * (size_t)cur + 1];
+            cnt.node_visits += 2;
+            float tl, tr;
+            const bool hl = node_hit(nl, o, inv, best, tl);
+            const bool hr = node_hit(nr, o, inv, best, tr);
+            if (hl && hr) {
+                if (sp + 1 > cap) {
+                    cnt.overflow();
+                    has = false;
+                    sp = 0;
+                } else {
+                    const bool left_first = tl <= tr;
+                    wstack[(sp++) * 64 + lane] = left_first ? nr.a : nl.a;
+                    cur = left_first ? nl.a : nr.a;
+                }
+            } else if (hl) {
+                cur = nl.a;
+            } else if (hr) {
+                cur = nr.a;
+            } else {
+                has = false;
+            }
+        }
+        uint32_t lk = 0, ln = 0;
+        if (has && (cur & kLeafRef)) {
+            const uint32_t nt = ((cur >> 27) & 15u) + 1u;
+            lk = cur & 0x07FFFFFFu;
+            ln = nt < 3u ? nt : 3u;
+            if (nt > 3u)
+                cur = kLeafRef | ((nt - 4u) << 27) | (lk + 3u);
+            else
+                has = false;
+        }
+#else
         if (!has && sp > 0) {
             cur = nodes[wstack[(--sp) * 64 + lane]];
             ++cnt.node_visits;
@@ -1052,6 +1255,7 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
                 }
             }
         }
+#endif
         const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
         if (b1) {
             const uint32_t at = qtail + (uint32_t)(lane_rank(b1) + lane_rank(b2) + lane_rank(b3));
@@ -1259,7 +1463,10 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 RT_ACC(3, t_m0, t_m1);
             } else {
 #endif
-#if RT_BVH_STEAL
+#if RT_BVH_STEAL && RT_BVH_PAIRS && RT_LEAF_BATCH && RT_MESH_RUN
+                mesh_bvh_pairs(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0, want, o, d, inv, h, i,
+                               ob.order, stack - lane, W, lane, cnt, S.stack_cap);
+#elif RT_BVH_STEAL
                 mesh_bvh_coop(S.tris, S.tri_orig, S.nodes, root, ob.u0, want, o, d, inv, h, i, ob.order,
                               stack - lane, W, lane, cnt, S.stack_cap);
 #else
@@ -1276,7 +1483,8 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             cand(live ? medium_candidate(ob, o, d, rng) : __builtin_nanf(""), false);
         } else if (kBvh && (kParts & 2) != 0) {  // kObjSphereGroup
 #if RT_SG_BATCH && RT_MESH_RUN
-            sphere_group_batched(S.objs, S.nodes, ob.u2, live, ray, inv, h, stack - lane, W, lane, cnt, S.stack_cap);
+            sphere_group_batched(S.objs, S.nodes, RT_SG_PAIRS ? __float_as_uint(ob.f[8]) : ob.u2, live, ray, inv, h,
+                                 stack - lane, W, lane, cnt, S.stack_cap);
 #else
             sphere_group(S.objs, S.nodes, ob.u2, live, ray, inv, h, stack, cnt, S.stack_cap);
 #endif
@@ -2319,6 +2527,9 @@ __device__ __forceinline__ void pt_leaf(const KTri* __restrict__ ktris,
     __builtin_amdgcn_wave_barrier();
 }
 
+#ifndef RT_PT_PAIRS
+#define RT_PT_PAIRS 1  // pathTrace traversal over child-pair records (cf_child_pairs; 0: node records, A/B)
+#endif
 #if RT_LEAF_BATCH
 // pt_traverse_coop with deferred leaf tests (as mesh_bvh_coop): leaves append (DFS list
 // position, ray owner) pairs to a per-wave LDS queue, three per lane and trip, and the wave
@@ -2331,7 +2542,7 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
                                                          unsigned long long* keys, int32_t* vlist, uint32_t* queue,
                                                          int lane, bool want, const PtRay& ray, int avoid_in,
                                                          float len_in, float eps_in, PtBest& out, Counters& cnt,
-                                                         int cap) {
+                                                         int cap, uint32_t root_ref) {
     const uint64_t wm = __ballot(want);
     if (wm == 0) return;
     key_reset(keys[lane]);
@@ -2347,13 +2558,19 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
             bdist = fsqrt(g);
         }
     };
+#if RT_PT_PAIRS
+    uint32_t cur = root_ref;  // pair index or leaf reference
+#else
+    (void)root_ref;
     CFNode cur = nodes[0];
+#endif
     bool has = want;
     if (want) {
         ++cnt.node_visits;
-        if (!(cur.u0 & 0x80000000u)) {
+        const CFNode root = nodes[0];
+        if (!(root.u0 & 0x80000000u)) {
             float tw, od;
-            has = pt_box_decide(cur, r, tw, od);
+            has = pt_box_decide(root, r, tw, od);
         }
     }
     int sp = 0, bot = 0;
@@ -2427,15 +2644,76 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
                 const uint32_t entry = wstack[vb * 64 + vic];
                 refresh();
                 sp = bot = 0;
+#if RT_PT_PAIRS
+                cur = entry;
+                has = true;
+#else
                 cur = nodes[entry];
                 ++cnt.node_visits;
                 float tw, od;
                 pt_box_bounds(cur, r, tw, od);
                 has = !pruned(tw);
+#endif
             }
             if (spare && lane_rank(vm) < ni) ++bot;  // robbed
             __builtin_amdgcn_wave_barrier();
         }
+#if RT_PT_PAIRS
+        if (!has && sp > bot) {
+            cur = wstack[(--sp) * 64 + lane];
+            refresh();
+            has = true;
+        }
+        if (!has && sp == bot) sp = bot = 0;
+        if (has && !(cur & kLeafRef)) {
+            const CFNode c0 = nodes[2 * (size_t)cur], c1 = nodes[2 * (size_t)cur + 1];
+            cnt.node_visits += 2;
+            float w0, o0, w1, o1;
+            bool h0, h1;
+            if (c0.u1) {  // a leaf's box: distance pruning only
+                pt_box_bounds(c0, r, w0, o0);
+                h0 = true;
+            } else {
+                h0 = pt_box_decide(c0, r, w0, o0);
+            }
+            if (c1.u1) {
+                pt_box_bounds(c1, r, w1, o1);
+                h1 = true;
+            } else {
+                h1 = pt_box_decide(c1, r, w1, o1);
+            }
+            h0 = h0 && !pruned(w0);
+            h1 = h1 && !pruned(w1);
+            if (h0 && h1) {
+                if (sp + 1 > cap) {
+                    cnt.overflow();
+                    has = false;
+                    sp = bot = 0;
+                } else {
+                    const bool first0 = o0 <= o1;
+                    wstack[(sp++) * 64 + lane] = first0 ? c1.u0 : c0.u0;
+                    cur = first0 ? c0.u0 : c1.u0;
+                }
+            } else if (h0) {
+                cur = c0.u0;
+            } else if (h1) {
+                cur = c1.u0;
+            } else {
+                has = false;
+            }
+        }
+        uint32_t lk = 0, ln = 0;  // this trip's leaf pairs: list positions lk .. lk + ln - 1
+        if (has && (cur & kLeafRef)) {
+            const uint32_t nt = ((cur >> 27) & 15u) + 1u;
+            lk = cur & 0x07FFFFFFu;
+            ln = nt < 3u ? nt : 3u;
+            if (nt > 3u)  // a larger leaf keeps this lane for more trips
+                cur = kLeafRef | ((nt - 4u) << 27) | (lk + 3u);
+            else
+                has = false;
+            cnt.tri_tests += ln;
+        }
+#else
         if (!has && sp > bot) {
             cur = nodes[wstack[(--sp) * 64 + lane]];
             ++cnt.node_visits;
@@ -2497,6 +2775,7 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
                 }
             }
         }
+#endif
         const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
         if (b1) {
             const uint32_t at = qtail + (uint32_t)(lane_rank(b1) + lane_rank(b2) + lane_rank(b3));
@@ -2628,7 +2907,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
 #if RT_BVH_STEAL
 #if RT_LEAF_BATCH
             pt_traverse_coop_batched(ktris, nodes, tri_list, stack - lane, pt_keys[wave], pt_vlist[wave], pt_queue[wave],
-                                     lane, alive, r, avoid, fsqrt(dot(d, d)), eps, best, cnt, L.stack_depth);
+                                     lane, alive, r, avoid, fsqrt(dot(d, d)), eps, best, cnt, L.stack_depth,
+                                     L.pt_root_ref);
 #else
             pt_traverse_coop(ktris, nodes, tri_list, stack - lane, pt_keys[wave], pt_vlist[wave], lane, alive, r,
                              avoid, fsqrt(dot(d, d)), eps, best, cnt, L.stack_depth);
@@ -2910,7 +3190,7 @@ uint32_t kernel_build_flags() {
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
     !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || RT_PT_WAVES != 5 || \
-    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE || !RT_NOSPH_VARIANT || !RT_BVH_PARTS_VARIANT || !RT_LEAF_BATCH || !RT_SG_BATCH
+    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE || !RT_NOSPH_VARIANT || !RT_BVH_PARTS_VARIANT || !RT_LEAF_BATCH || !RT_SG_BATCH || !RT_BVH_PAIRS || !RT_SG_PAIRS || !RT_PT_PAIRS
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;

@@ -410,6 +410,84 @@ std::string HostScene::flatten() {
     const std::string err = group_spheres();
     if (!err.empty()) return err;
     mark_mesh_runs();
+    return build_mesh_pairs();
+}
+
+namespace {
+// Child-pair records of one mesh BVH (see HostScene::build_mesh_pairs).
+struct PairBuilder {
+    std::vector<BvhNode>& nodes;
+    int max_pairs = 0;  // pair records on the longest root-to-leaf path = stack entries a lane may need
+    bool empty_leaf = false;
+
+    uint32_t alloc() {
+        const size_t at = nodes.size();
+        nodes.resize(at + 2, BvhNode{});
+        return (uint32_t)(at / 2);
+    }
+    void set(uint32_t q, BvhNode l, uint32_t ref_l, BvhNode r, uint32_t ref_r) {
+        l.a = ref_l;
+        l.b = 0;
+        r.a = ref_r;
+        r.b = 0;
+        nodes[2 * (size_t)q] = l;
+        nodes[2 * (size_t)q + 1] = r;
+    }
+    // reference to triangles [first, first + count) of a leaf whose box is `box`; `above` = pairs above it
+    uint32_t leaf(BvhNode box, uint32_t first, uint32_t count, int above) {
+        if (count <= kLeafRefMax) {
+            empty_leaf |= count == 0u;
+            max_pairs = std::max(max_pairs, above);
+            return kLeafRef | ((count - 1u) << 27) | first;
+        }
+        const uint32_t q = alloc();  // a larger leaf: two halves under the same box
+        const uint32_t half = count / 2u;
+        const uint32_t l = leaf(box, first, half, above + 1), r = leaf(box, first + half, count - half, above + 1);
+        set(q, box, l, box, r);
+        return q;
+    }
+    uint32_t node(uint32_t i, int above) {
+        const BvhNode n = nodes[i];
+        if (n.b & 0x80000000u) return leaf(n, n.a, n.b & 0x7FFFFFFFu, above);
+        const uint32_t q = alloc();
+        const uint32_t l = node(n.a, above + 1), r = node(n.b, above + 1);
+        set(q, nodes[n.a], l, nodes[n.b], r);
+        return q;
+    }
+};
+}  // namespace
+
+// The batched traversals (rt_kernel.hip mesh_bvh_pairs, sphere_group_batched) read each inner
+// node of a mesh or sphere-group BVH as one 64 B child-pair record - both children's boxes, each with a reference word: a
+// pair index (the child's own pair at nodes[2q], nodes[2q + 1]) or a leaf reference
+// (kLeafRef | (count - 1) << 27 | first triangle or member, count <= 16; larger leaves become pairs of
+// halves under the leaf's box). A lane therefore never loads a node to learn what its stack
+// entry is: one dependent load per inner step, none for leaves. The records follow the
+// node table (from an even index, so each pair is one aligned 64 B line); the mesh or group
+// record keeps its node root in u2 and carries its root reference in f[8] (as u32 bits). Any
+// tree over the same primitives gives the same hit (conservative boxes, the (t, index) minimum).
+std::string HostScene::build_mesh_pairs() {
+    auto tree = [&](const ObjRec& r) {
+        return (r.type == kObjMesh || r.type == kObjSphereGroup) && r.u2 != kNoBvh;
+    };
+    bool any = false;
+    for (int k = 0; k < n_scan; ++k) any |= tree(objs[k]);
+    if (!any) return "";
+    if (tris.size() >= (size_t(1) << 26) || objs.size() >= (size_t(1) << 26))
+        return "too many triangles or objects for the BVH references (2^26)";
+    if (nodes.size() & 1u) nodes.push_back(BvhNode{});
+    for (int k = 0; k < n_scan; ++k) {
+        ObjRec& r = objs[k];
+        if (!tree(r)) continue;
+        PairBuilder pb{nodes};
+        const uint32_t root = pb.node(r.u2, 0);
+        if (pb.empty_leaf) return "BVH with an empty leaf";
+        if (pb.max_pairs > kBvhStackDepth)
+            return "BVH pair depth " + std::to_string(pb.max_pairs) + " exceeds the traversal stack (" +
+                   std::to_string(kBvhStackDepth) + ")";
+        bvh_max_depth = std::max(bvh_max_depth, pb.max_pairs);
+        memcpy(&r.f[8], &root, 4);
+    }
     return "";
 }
 

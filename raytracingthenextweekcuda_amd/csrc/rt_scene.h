@@ -24,7 +24,7 @@ enum ObjType : uint32_t {
     kObjMovingSphere = 1,
     kObjPlane = 2,
     kObjMesh = 3,
-    kObjSphereGroup = 4,  // BVH over (moving) spheres: u0 = first member, u1 = count, u2 = root
+    kObjSphereGroup = 4,  // BVH over (moving) spheres: u0 = first member, u1 = count, u2 = root, f[8] = root pair ref
     kObjMedium = 5        // constant medium in a cube: f = center xyz, extend xyz, -1/density; u0 = slot
 };
 
@@ -43,7 +43,8 @@ struct alignas(16) ObjRec {
     // plane: position xyz, normal xyz, rectangle bounds (lo_a, hi_a, lo_b, hi_b) on the
     //        orientation's axes a, b (XY: x, y; YZ: y, z; XZ: x, z)
     // mesh: boundsMin xyz, boundsMax xyz (computeMeshAABB, main.cu:261-281), f[6] = the bits of
-    //       ceil(2^32 / triangle count) (the brute-force compaction's division)
+    //       ceil(2^32 / triangle count) (the brute-force compaction's division), f[7] = mesh-run
+    //       length (brute force), f[8] = root child-pair reference (BVH meshes)
     float f[10];
 };
 constexpr uint32_t kNoBvh = 0xFFFFFFFFu;
@@ -160,6 +161,7 @@ struct HostScene {
     std::string flatten();
     std::string group_spheres();
     void mark_mesh_runs();
+    std::string build_mesh_pairs();
     // A mesh BVH: read from `<cache_ply>.bvh` when the cache mode allows and the file is
     // fresh and valid, else built (and written when the mode says so).
     void build_bvh(const std::vector<v3>& vs, const std::vector<uint32_t>& ix, CFBvh& b,
