@@ -20,6 +20,8 @@ def main(src):
           "VALU issue (frac) | HBM bytes / launch (frac) |")
     for sc in SCENES:
         f = os.path.join(src, f"bench_{sc}.log")
+        if not os.path.exists(f) and sc == "cornellbox1":  # the default line (gpu_session.sh BENCH=1)
+            f = os.path.join(src, "bench.log")
         if not os.path.exists(f):
             continue
         line = next(json.loads(s) for s in open(f) if s.startswith("{"))
