@@ -4,11 +4,11 @@
 One step = one full frame: every rank renders its interleaved pixel-row tiles
 with the HIP megakernel (librtmi.so) straight into an HBM buffer, then the
 tiles are gathered to rank 0 with one RCCL gather over xGMI (N > 1), which
-overlaps the next frame's render (double-buffered tiles); the timed region ends
+overlaps the next frame's render (one tile buffer per context); the timed region ends
 after the last frame is assembled on rank 0. The frame work is fixed as N grows
-(strong scaling). Consecutive frames alternate between two renderer contexts on two
-HIP streams, so a frame's launch overlaps the tail of the previous one (--no-overlap:
-one context, one stream, for per-launch measurements).
+(strong scaling). Consecutive frames rotate over --contexts (3) renderer contexts on as
+many HIP streams, so a frame's launch overlaps the tail of the previous one
+(--no-overlap: one context, one stream, for per-launch measurements).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 N > 1 is launched by torch.distributed.run (one process per GPU).
@@ -72,6 +72,10 @@ def parse():
                     help="rows per round-robin block (2: per-rank shard times within 1.1%% at N=8, tools/shard_balance.py)")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per pixel (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--contexts", type=int, default=3,
+                    help="frame overlap: renderer contexts / HIP streams that consecutive frames rotate over "
+                         "(tools/overlap_probe.py: CB1 N = 8 shard 1.00 / 0.887 / 0.842 / 0.879 ms/frame with "
+                         "1 / 2 / 3 / 4; N = 1 unchanged from 2 to 3)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="one context and stream: consecutive frames do not overlap (per-launch roofline)")
     ap.add_argument("--cpu-spp", type=int, default=None)
@@ -260,12 +264,16 @@ def measure(args, world, rank, local, rehearsal):
 
     _lib.require_parity_build("bench.py")  # an ablation / timer build would not measure the shipped kernel
     W, H = args.width, args.height
-    # Frame overlap (default): two contexts on two streams take alternate frames, so frame
+    # Frame overlap (default): --contexts (3) contexts on as many streams take turns at frames, so frame
     # k+1's launch fills the SIMDs that frame k's persistent launch leaves idle while its
     # last work items drain (tools/overlap_probe.py: CB1 N = 8 shard 1.17 -> 1.00 ms/frame,
     # N = 1 7.57 -> 7.42). Every frame is still rendered completely.
-    overlap = not args.no_overlap and not rehearsal
-    rs = [rtmi.Renderer(device=local) for _ in range(2 if overlap else 1)]
+    if args.contexts < 2 and not args.no_overlap:
+        raise SystemExit("--contexts must be >= 2 (or use --no-overlap)")
+    # every context takes at least one timed frame (its first timed launch resets its counters)
+    n_ctx = min(args.contexts, args.steps)
+    overlap = not args.no_overlap and not rehearsal and n_ctx >= 2
+    rs = [rtmi.Renderer(device=local) for _ in range(n_ctx if overlap else 1)]
     for rr in rs:
         getattr(rtmi, SCENES[args.scene][0])(rr, W, H)
     r = rs[0]
@@ -298,7 +306,9 @@ def measure(args, world, rank, local, rehearsal):
         else:
             rs[b].render_device(p, tile.data_ptr(), launch_stream(b).cuda_stream)
 
-    for _ in range(args.warmup):
+    # every context renders at least one untimed frame (its first launch allocates its work queue
+    # and partial sums), however small --warmup is
+    for _ in range(max(args.warmup, len(rs))):
         if overlap:
             frame.submit(lambda tile, b: render_into(tile, params, b))
         else:
@@ -380,7 +390,7 @@ def measure(args, world, rank, local, rehearsal):
         "lanes_per_pixel": int(st["lanes_per_pixel"]), "refill": int(st["refill"]),
         "queue_blocks": int(st["queue_blocks"]), "variant": st["variant_name"],
         "object_bytes_per_segment": object_bytes_per_segment(r) if integrator != "pathTrace" else 0,
-        "n_cu": n_cu, "overlap": overlap,
+        "n_cu": n_cu, "overlap": overlap, "contexts": len(rs),
     }
     for rr in rs:
         rr.close()
@@ -396,7 +406,7 @@ def selftest_measure(args, world, rank):
         "nodes": 0.0, "grp_bytes": 0.0, "rows": float(args.height // world),
         "kernel_ms": 5.0 + rank, "kernel_ms_isolated": 4.0 + rank, "gather_ms": 0.05 * (rank + 1),
         "frame_ms_isolated": 6.0 + 0.5 * rank, "launch_ms": 5.5 + rank, "lanes_per_pixel": 32, "refill": 8,
-        "queue_blocks": 1536, "variant": "render_kernel<false, true, false, false, 3>",
+        "queue_blocks": 1536, "variant": "render_kernel<selftest>",  # matches no profile: refused
         "object_bytes_per_segment": 240, "n_cu": 256, "overlap": False,
     }
 
@@ -486,7 +496,7 @@ def build_line(args, agg: dict, world: int, cpu=None) -> dict:
             "width": W, "height": H, "spp": args.spp, "depth": args.depth,
             "row_block": args.row_block, "lanes_per_pixel": agg["lanes_per_pixel"],
             "variant": agg["variant"], "queue": agg["queue_blocks"] > 0,
-            "refill": agg["refill"], "queue_blocks": agg["queue_blocks"],
+            "refill": agg["refill"], "queue_blocks": agg["queue_blocks"], "contexts": agg.get("contexts", 1),
             "kernel_source_sha": sha,
             "parallelism": f"row-tiles x{world} + RCCL gather" if world > 1 else "single GPU",
             "segments_per_frame": int(segs / K),

@@ -59,35 +59,36 @@ class RowShardedFrame:
         self.src_rows = None
         self.pending = None  # (async gather work, landing block index) of the last submitted frame
         self.n_submitted = 0
-        # Frame overlap (streams = two torch.cuda.Streams): consecutive frames alternate
-        # between two buffers AND two streams, so frame k+1's render runs while frame k's
-        # launch drains its last work items (a persistent launch's tail leaves SIMDs idle);
-        # render_into(tile, b) must then launch on streams[b]. Without streams every frame
-        # runs on the current stream.
+        # Frame overlap (streams = n >= 2 torch.cuda.Streams): consecutive frames rotate over
+        # n buffers AND n streams, so frame k+1's render runs while frame k's launch drains
+        # its last work items (a persistent launch's tail leaves SIMDs idle); render_into(tile,
+        # b) must then launch on streams[b]. Without streams every frame runs on the current
+        # stream.
         self.streams = streams
+        self.nbuf = len(streams) if streams else (2 if pipeline else 1)
         if self.world == 1:
             # one rank owns every row in order: render straight into the frame
             self.frame = torch.zeros((height, width, 3), dtype=torch.float32, device=self.device)
             self.tile = self.frame
-            self.frames = [self.frame] + ([torch.zeros_like(self.frame)] if streams else [])
+            self.frames = [self.frame] + [torch.zeros_like(self.frame) for _ in range(self.nbuf - 1 if streams else 0)]
             return
         if streams and not pipeline:
             raise ValueError("frame overlap (streams) needs pipeline=True")
         self.tile = torch.zeros((self.max_rows, width, 3), dtype=torch.float32, device=self.device)
-        # pipelined frames (submit/drain): two tile buffers (and two landing blocks on rank 0),
+        # pipelined frames (submit/drain): nbuf tile buffers (and landing blocks on rank 0),
         # so frame k's gather overlaps frame k+1's render
         self.pipeline = pipeline
-        self.tiles = [self.tile] + ([torch.zeros_like(self.tile)] if pipeline else [])
+        self.tiles = [self.tile] + [torch.zeros_like(self.tile) for _ in range(self.nbuf - 1)]
         if self.rank == 0:
             self.frame = torch.zeros((height, width, 3), dtype=torch.float32, device=self.device)
-            self.frames = [self.frame] + ([torch.zeros_like(self.frame)] if streams else [])
+            self.frames = [self.frame] + [torch.zeros_like(self.frame) for _ in range(self.nbuf - 1 if streams else 0)]
             # the gather lands in one (world * max_rows) block; frame row y is
             # block row rank(y) * max_rows + (its position in that rank's tile)
             self.gathered = torch.empty((self.world * self.max_rows, width, 3), dtype=torch.float32,
                                         device=self.device)
             self.gather_list = list(self.gathered.view(self.world, self.max_rows, width, 3).unbind(0))
             self.landing = [(self.gathered, self.gather_list)]
-            if pipeline:
+            for _ in range(self.nbuf - 1):
                 g2 = torch.empty_like(self.gathered)
                 self.landing.append((g2, list(g2.view(self.world, self.max_rows, width, 3).unbind(0))))
             src = [0] * height
@@ -140,7 +141,7 @@ class RowShardedFrame:
         waiting for it; the previous frame's gather (which ran under this render) is
         completed and assembled on rank 0 after this frame's render is enqueued. With
         frame overlap, render_into(tile, b) is called and must launch on streams[b]."""
-        b = self.n_submitted % 2
+        b = self.n_submitted % self.nbuf
         self.n_submitted += 1
         if self.world == 1:
             if self.streams:
@@ -169,11 +170,11 @@ class RowShardedFrame:
         With frame overlap the frame was rendered (world 1) or assembled (rank 0) on
         streams[b]: the caller's current stream is made to wait for that stream, so work the
         caller enqueues on it reads the finished frame. The frame buffer is reused by the
-        second-next submit()."""
+        nbuf-th next submit()."""
         if self.pending is not None:
             self._finish_pending()
         if self.streams and self.n_submitted:
-            self.torch.cuda.current_stream().wait_stream(self.streams[(self.n_submitted - 1) % 2])
+            self.torch.cuda.current_stream().wait_stream(self.streams[(self.n_submitted - 1) % self.nbuf])
         return self.frame if self.rank == 0 else None
 
 

@@ -14,17 +14,18 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_row_sharded_frame_overlap_keeps_every_frame():
+@pytest.mark.parametrize("n_ctx", [2, 3])
+def test_row_sharded_frame_overlap_keeps_every_frame(n_ctx):
     import torch
 
     import raytracingthenextweekcuda_amd as rtmi
     from raytracingthenextweekcuda_amd.distributed import RowShardedFrame
 
     w, h, spp, depth = 96, 64, 8, 6
-    rs = [rtmi.Renderer(0), rtmi.Renderer(0)]
+    rs = [rtmi.Renderer(0) for _ in range(n_ctx)]
     for r in rs:
         rtmi.cornell_box1(r, w, h)
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    streams = [torch.cuda.Stream() for _ in range(n_ctx)]
     fr = RowShardedFrame(w, h, 2, device=torch.device("cuda"), streams=streams)
     seeds = [11, 12, 13, 14, 15]
     got = []
@@ -57,7 +58,10 @@ def _bench(*extra):
 def test_bench_line_with_and_without_overlap():
     a = _bench()
     b = _bench("--no-overlap")
+    c = _bench("--contexts", "2")
     assert a["roofline"]["overlap"] is True and b["roofline"]["overlap"] is False
+    assert (a["config"]["contexts"], b["config"]["contexts"], c["config"]["contexts"]) == (3, 1, 2)
+    assert c["config"]["segments_per_frame"] == a["config"]["segments_per_frame"]
     assert a["config"]["segments_per_frame"] == b["config"]["segments_per_frame"]
     assert a["value"] > 0 and b["value"] > 0 and a["steps"] == 3
     # the work-queue schedule the line was measured with (rt_render_stats.refill / queue_blocks)

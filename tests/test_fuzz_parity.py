@@ -198,3 +198,56 @@ def test_gpu_mesh_runs_parity(seed, lanes):
     want, ost = build_oracle(spec).render(w, h, spp, depth, lanes_per_pixel=lanes)
     assert np.array_equal(got, want)
     assert st["segments"] == ost["segments"]
+
+
+def large_leaf_spec(seed):
+    """BVH leaves larger than a child-pair leaf reference holds (16 primitives: rt_scene.cpp
+    build_mesh_pairs splits them into halves under the leaf's box): a 160-triangle mesh whose
+    first 100 triangles are one triangle repeated (equal centroids: the SAH builder cannot split
+    them, and at equal t the lowest mesh-local index must win), and 40 spheres of which 24 are
+    one sphere repeated with different materials (a sphere-group leaf of 24; at equal t the
+    highest scan order wins)."""
+    rng = np.random.RandomState(seed)
+    mats = [("lambertian", 0, (0.8, 0.3, 0.3)), ("metal", 1, (0.9, 0.9, 0.5), 0.3),
+            ("lambertian", 2, (0.2, 0.7, 0.3)), ("emission", 3, (1.0, 0.9, 0.8), 4.0),
+            ("dielectric", 4, 1.5)]
+    one = rng.uniform(-0.4, 0.4, size=(1, 9)).astype(np.float32)
+    rest = rng.uniform(-0.6, 0.6, size=(60, 9)).astype(np.float32)
+    tris = np.concatenate([np.repeat(one, 100, axis=0), rest]).reshape(-1)
+    objs = [("mesh", 0, tris, 0), ("plane", 1, (0.0, -0.8, 0.0), (0.0, 1.0, 0.0), (2.0, 2.0, 2.0), 0, 2, True)]
+    slot = 2
+    for k in range(40):
+        c = (0.3, 0.9, -0.2) if k < 24 else tuple(rng.uniform(-1.2, 1.2, 3))
+        objs.append(("sphere", slot, c, 0.25 if k < 24 else float(rng.uniform(0.05, 0.2)), k % 5))
+        slot += 1
+    cam = ((0.3, 0.4, 2.6), (0.0, 0.1, 0.0), (0.0, 1.0, 0.0), 1.33, 50.0, 0.0, 2.5, 0.0, 1.0)
+    return {"camera": cam, "materials": mats, "objects": objs}
+
+
+def test_large_leaf_specs_build_on_host():
+    import raytracingthenextweekcuda_amd as rtmi
+
+    for seed in range(2):
+        r = rtmi.Renderer(-1)
+        build_product(r, large_leaf_spec(seed))
+        c = r.object_counts()
+        r.close()
+        assert c["bvh_node"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,lanes", [(0, 1), (1, 8)])
+def test_gpu_large_leaf_parity(seed, lanes):
+    import raytracingthenextweekcuda_amd as rtmi
+
+    spec = large_leaf_spec(seed)
+    w, h, spp, depth = 48, 36, 8, 6
+    r = rtmi.Renderer(0)
+    build_product(r, spec)
+    got = r.render(w, h, spp, depth, lanes_per_pixel=lanes)
+    st = r.stats()
+    r.close()
+    want, ost = build_oracle(spec).render(w, h, spp, depth, lanes_per_pixel=lanes)
+    assert st["overflow"] == 0
+    assert np.array_equal(got, want)
+    assert st["segments"] == ost["segments"]

@@ -1,7 +1,7 @@
 """Does overlapping consecutive frames fill the SIMDs that a launch's tail leaves idle?
 Renders K frames (rank 0's shard of a world-W row tiling) back to back on one context and
-stream, then alternating two contexts on two streams, and prints ms per frame of each.
-Usage: [SCENE=cornellbox1] python tools/overlap_probe.py W [K]"""
+stream, then rotating over n contexts on n streams, and prints ms per frame of each.
+Usage: [SCENE=cornellbox1] [CTX="1 2"] python tools/overlap_probe.py W [K]"""
 import os
 import sys
 import time
@@ -17,11 +17,12 @@ SCENE = os.environ.get("SCENE", "cornellbox1")
 loader, W, H, SPP, DEPTH, _ = bench.SCENES[SCENE]
 world = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-rs = [rtmi.Renderer(0), rtmi.Renderer(0)]
+NCTX = [int(c) for c in os.environ.get("CTX", "1 2").split()]
+rs = [rtmi.Renderer(0) for _ in range(max(NCTX))]
 for r in rs:
     getattr(rtmi, loader)(r, W, H)
 outs = [torch.empty((H, W, 3), dtype=torch.float32, device="cuda") for _ in rs]
-streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+streams = [torch.cuda.Stream() for _ in rs]
 p = rs[0].params(W, H, SPP, DEPTH, 1984, 0, 2, 0, world, 0, bench.INTEGRATOR.get(SCENE, "rayColor"))
 
 
@@ -35,6 +36,6 @@ def run(n_ctx):
     return (time.perf_counter() - t0) * 1e3 / K
 
 
-for n in (1, 2, 1, 2):
+for n in NCTX + NCTX:
     run(n)  # warm-up of this mode
     print(f"{SCENE} world {world}: {n} context(s) {run(n):.4f} ms/frame", flush=True)
