@@ -6,8 +6,9 @@ with the HIP megakernel (librtmi.so) straight into an HBM buffer, then the
 tiles are gathered to rank 0 with one RCCL gather over xGMI (N > 1), which
 overlaps the next frame's render (one tile buffer per context); the timed region ends
 after the last frame is assembled on rank 0. The frame work is fixed as N grows
-(strong scaling). Consecutive frames rotate over --contexts (3) renderer contexts on as
-many HIP streams, so a frame's launch overlaps the tail of the previous one
+(strong scaling). Consecutive frames rotate over --contexts renderer contexts on as
+many HIP streams (3 for frames of up to 2^25 samples per rank, else 2), so a frame's launch
+overlaps the tail of the previous one
 (--no-overlap: one context, one stream, for per-launch measurements).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -72,10 +73,11 @@ def parse():
                     help="rows per round-robin block (2: per-rank shard times within 1.1%% at N=8, tools/shard_balance.py)")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per pixel (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--contexts", type=int, default=3,
-                    help="frame overlap: renderer contexts / HIP streams that consecutive frames rotate over "
-                         "(tools/overlap_probe.py: CB1 N = 8 shard 1.00 / 0.887 / 0.842 / 0.879 ms/frame with "
-                         "1 / 2 / 3 / 4; N = 1 unchanged from 2 to 3)")
+    ap.add_argument("--contexts", type=int, default=0,
+                    help="frame overlap: renderer contexts / HIP streams that consecutive frames rotate over; "
+                         "0 = auto: 3 when a rank's frame is at most 2^25 samples, else 2 (tools/ctx_probe.sh: "
+                         "CB1 N = 8 shard 1.00 / 0.887 / 0.842 / 0.879 ms/frame with 1 / 2 / 3 / 4 contexts, "
+                         "N = 1 5.88 -> 5.82 from 2 to 3; the 300 ms bunny frame 2.5 %% slower with 3)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="one context and stream: consecutive frames do not overlap (per-launch roofline)")
     ap.add_argument("--cpu-spp", type=int, default=None)
@@ -264,14 +266,18 @@ def measure(args, world, rank, local, rehearsal):
 
     _lib.require_parity_build("bench.py")  # an ablation / timer build would not measure the shipped kernel
     W, H = args.width, args.height
-    # Frame overlap (default): --contexts (3) contexts on as many streams take turns at frames, so frame
+    # Frame overlap (default): --contexts contexts on as many streams take turns at frames, so frame
     # k+1's launch fills the SIMDs that frame k's persistent launch leaves idle while its
     # last work items drain (tools/overlap_probe.py: CB1 N = 8 shard 1.17 -> 1.00 ms/frame,
     # N = 1 7.57 -> 7.42). Every frame is still rendered completely.
-    if args.contexts < 2 and not args.no_overlap:
-        raise SystemExit("--contexts must be >= 2 (or use --no-overlap)")
+    contexts = args.contexts
+    if contexts == 0:  # auto: a third context pays off where the launch's tail is a visible share of it
+        samples = rtmi.owned_rows(H, args.row_block, rank, world) * W * args.spp
+        contexts = 3 if samples <= (1 << 25) else 2
+    if contexts < 2 and not args.no_overlap:
+        raise SystemExit("--contexts must be >= 2 (or 0 = auto, or --no-overlap)")
     # every context takes at least one timed frame (its first timed launch resets its counters)
-    n_ctx = min(args.contexts, args.steps)
+    n_ctx = min(contexts, args.steps)
     overlap = not args.no_overlap and not rehearsal and n_ctx >= 2
     rs = [rtmi.Renderer(device=local) for _ in range(n_ctx if overlap else 1)]
     for rr in rs:

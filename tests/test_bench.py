@@ -60,6 +60,7 @@ def test_bench_line_with_and_without_overlap():
     b = _bench("--no-overlap")
     c = _bench("--contexts", "2")
     assert a["roofline"]["overlap"] is True and b["roofline"]["overlap"] is False
+    # auto: 3 contexts for this small frame (<= 2^25 samples per rank)
     assert (a["config"]["contexts"], b["config"]["contexts"], c["config"]["contexts"]) == (3, 1, 2)
     assert c["config"]["segments_per_frame"] == a["config"]["segments_per_frame"]
     assert a["config"]["segments_per_frame"] == b["config"]["segments_per_frame"]
