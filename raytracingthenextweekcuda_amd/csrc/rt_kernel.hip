@@ -216,7 +216,7 @@ struct Hit {
 };
 
 #ifndef RT_MESH_TWO_PHASE
-#define RT_MESH_TWO_PHASE 1  // cull-filtered compaction (mesh_compact); 0 = one pass (A/B only)
+#define RT_MESH_TWO_PHASE 1  // cull-filtered compaction (mesh_compact); 0 = one pass (A/B only; mesh runs are always two-phase)
 #endif
 
 #ifndef RT_MESH_RUN
@@ -231,9 +231,7 @@ struct WaveLds {
     uint32_t slot[kMaxRun * 64];  // mesh_run: ray slot -> lane | triangle base << 6
 #endif
     uint32_t grp_s[64], grp_m[64];  // per-lane sphere-group test counts (Counters::grp drained per trip)
-#if RT_MESH_TWO_PHASE
     uint16_t ring[128];          // pair ids that passed the backface cull, awaiting the full test
-#endif
 };
 
 // Event counters of one wave, laid out to keep the VGPR file free for the traversal:
@@ -2003,9 +2001,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             v3 att;
             bool scattered;
             v3 nd;
+            // randomInUnitSphere is the first draw of Lambertian, Metal and isotropic scatter alike:
+            // drawn here once for all three, each lane's draw sequence is unchanged, and a wave whose
+            // lanes hit two of these materials runs one rejection loop instead of two
+            v3 rp{0.0f, 0.0f, 0.0f};
+            if (m.type == 0u || (kSph && (m.type == 1u || m.type == 4u))) rp = random_in_unit_sphere(rng);
             if (m.type == 0u) {
                 // Lambertian::scatter (Material.cu:3-19).
-                v3 u = normalize(random_in_unit_sphere(rng));
+                v3 u = normalize(rp);
                 v3 sd = add(n, u);
                 if ((fabsf(sd.x) < 1e-8f) && (fabsf(sd.y) < 1e-8f) && (fabsf(sd.z) < 1e-8f)) sd = n;
                 nd = normalize(sd);
@@ -2014,7 +2017,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             } else if (kSph && m.type == 1u) {
                 // Metal::scatter (Material.h:45-51).
                 v3 refl = reflect(normalize(ray.d), n);
-                nd = add(refl, scale(random_in_unit_sphere(rng), m.p0));
+                nd = add(refl, scale(rp, m.p0));
                 scattered = dot(nd, n) > 0.0f;
                 att = scale(v3{m.a0, m.a1, m.a2}, scattered ? 1.0f : 0.0f);
             } else if (kSph && m.type == 2u) {
@@ -2038,7 +2041,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                 scattered = true;
             } else if (kSph && m.type == 4u) {
                 // isotropic::scatter: Ray(p, randomInUnitSphere(), time), attenuation = albedo.
-                nd = random_in_unit_sphere(rng);
+                nd = rp;
                 att = v3{m.a0, m.a1, m.a2};
                 scattered = true;
             } else {
