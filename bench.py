@@ -7,7 +7,7 @@ tiles are gathered to rank 0 with one RCCL gather over xGMI (N > 1), which
 overlaps the next frame's render (one tile buffer per context); the timed region ends
 after the last frame is assembled on rank 0. The frame work is fixed as N grows
 (strong scaling). Consecutive frames rotate over --contexts renderer contexts on as
-many HIP streams (3 for frames of up to 2^25 samples per rank, else 2), so a frame's launch
+many HIP streams (3 for rayColor frames of up to 2^25 samples per rank, else 2), so a frame's launch
 overlaps the tail of the previous one
 (--no-overlap: one context, one stream, for per-launch measurements).
 
@@ -75,9 +75,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--contexts", type=int, default=0,
                     help="frame overlap: renderer contexts / HIP streams that consecutive frames rotate over; "
-                         "0 = auto: 3 when a rank's frame is at most 2^25 samples, else 2 (tools/ctx_probe.sh: "
-                         "CB1 N = 8 shard 1.00 / 0.887 / 0.842 / 0.879 ms/frame with 1 / 2 / 3 / 4 contexts, "
-                         "N = 1 5.88 -> 5.82 from 2 to 3; the 300 ms bunny frame 2.5 %% slower with 3)")
+                         "0 = auto: 3 when a rank's rayColor frame is at most 2^25 samples, else 2 "
+                         "(tools/ctx_probe.sh, tools/layout_probe.sh: CB1 N = 8 shard 1.00 / 0.887 / 0.842 / "
+                         "0.879 ms/frame with 1 / 2 / 3 / 4 contexts, N = 1 5.88 -> 5.82 from 2 to 3; the 300 ms "
+                         "bunny frame 2.5 %% and the pathTrace materialball frame 2 %% slower with 3)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="one context and stream: consecutive frames do not overlap (per-launch roofline)")
     ap.add_argument("--cpu-spp", type=int, default=None)
@@ -273,7 +274,8 @@ def measure(args, world, rank, local, rehearsal):
     contexts = args.contexts
     if contexts == 0:  # auto: a third context pays off where the launch's tail is a visible share of it
         samples = rtmi.owned_rows(H, args.row_block, rank, world) * W * args.spp
-        contexts = 3 if samples <= (1 << 25) else 2
+        small = samples <= (1 << 25) and INTEGRATOR.get(args.scene, "rayColor") != "pathTrace"
+        contexts = 3 if small else 2
     if contexts < 2 and not args.no_overlap:
         raise SystemExit("--contexts must be >= 2 (or 0 = auto, or --no-overlap)")
     # every context takes at least one timed frame (its first timed launch resets its counters)
