@@ -721,8 +721,9 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
         const uint64_t items = tiles * 64u * (uint64_t)L.lanes_per_pixel;
         const size_t bytes = (size_t)items * 3 * sizeof(float);
         // partial sums: 12 B per item (up to a few GB of the 288 GB HBM); a frame whose
-        // items do not fit the 32-bit item index or the allocation runs on the static grid
-        bool have = items < 0xFFFFFFFFull && bytes <= ((size_t)16 << 30);
+        // items do not fit the 31-bit item index (bit 31 is the kernels' camera-slot flag) or the
+        // allocation runs on the static grid
+        bool have = items < 0x80000000ull && bytes <= ((size_t)16 << 30);
         if (have && bytes > c->d_partial_bytes) {
             (void)hipFree(c->d_partial);
             c->d_partial = nullptr;

@@ -250,6 +250,15 @@ struct Counters {
     __device__ __forceinline__ void overflow() const { *reinterpret_cast<uint32_t*>(overflow_flag) = 1u; }
 };
 
+// Camera slots of one wave (linear-scan kernels, RT_CAM_SLOTS): each lane's NEXT sample of its
+// item, prepared ahead - the camera ray and the sample's stream state right after the camera's
+// draws (o.xyz d.x | d.yz time s0 | s1 s2 s3 -). A lane that finishes a sample starts the
+// prepared one from here; the camera pass itself then runs for many lanes at once (render_kernel).
+struct CamSlots {
+    float4 a[64], b[64];
+    uint4 c[64];
+};
+
 // Diagnostic build only (RT_STAMPS): wave-uniform s_memtime section timers,
 // summed per wave into counters[8..15]. Never enabled in shipped builds.
 #ifdef RT_STAMPS
@@ -1712,6 +1721,16 @@ __global__ __launch_bounds__(256) void combine_kernel(RenderLaunch L, float* __r
 #ifndef RT_TAIL_STEAL
 #define RT_TAIL_STEAL 1  // lanes idle at the end of the queue take other lanes' last samples
 #endif
+#ifndef RT_CAM_SLOTS
+#define RT_CAM_SLOTS 1  // linear-scan kernels prepare each lane's next camera sample in LDS (0: A/B)
+#endif
+#ifndef RT_CAM_BATCH
+#define RT_CAM_BATCH 32  // lanes lacking a prepared next sample that start a camera pass on their own
+#endif
+// Camera slots: bit 31 of a lane's work-queue item is set while its slot holds the lane's next
+// sample (s if need_cam, else s + SP): a flag in a VGPR already live, not a lane mask in SGPRs (the
+// megakernels' scarce registers). Item indices stay below 2^31 (rt_capi.cpp caps them).
+constexpr uint32_t kPrepared = 0x80000000u;
 
 // End (exclusive) of sub-stream c's sample sequence c, c + SP, ... < spp.
 __device__ __forceinline__ int sub_end(int spp, int c, int SP, int sp_log2) {
@@ -1770,7 +1789,7 @@ __device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, i
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if ((tl_pack >> (8 * k)) & 0xFFu) sum = add(sum, vals[k]);  // positions ascend with samples
-            store_partial(L, item, sum);
+            store_partial(L, item & ~kPrepared, sum);
             waiting = false;
             tl_pack = 0;
         }
@@ -1795,11 +1814,12 @@ __device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, i
     const bool thief = idle && ri < nv;
     const int vic = thief ? W.src[ri] : lane;
     const int v_end = __shfl(own_end, vic, 64);
-    const uint32_t v_item = (uint32_t)__shfl((int)item, vic, 64);
+    const uint32_t v_item = (uint32_t)__shfl((int)item, vic, 64) & ~kPrepared;
     if (spare && rv < ni) {  // robbed: its last unstarted sample goes to the thief of the same rank
         own_end -= SP;
         const int pos = (own_end - c) >> L.sp_log2;
         tl_pack |= ((uint32_t)W.key[rv] + 1u) << (8 * pos);
+        if ((item & kPrepared) && (need_cam ? s : s + SP) >= own_end) item &= ~kPrepared;  // the taken one was prepared
     }
     if (thief) {  // the thief's own item is finished: it carries the victim's (pixel, sub-stream)
         towner = vic;
@@ -1842,6 +1862,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
     float* __restrict__ out, unsigned long long* __restrict__ counters) {
     const SceneArgs S{objs, tris, mats, nodes, tri_orig, n_objs, 0, kBvh, L.stack_depth};
     __shared__ WaveLds lds[kWavesPerBlock];
+    // camera slots: the linear-scan kernels only (the traversal kernels' LDS holds their stacks)
+    constexpr bool kCamPf = RT_CAM_SLOTS && !kBvh;
+    __shared__ CamSlots cslots[kCamPf ? kWavesPerBlock : 1];
     // traversal stacks (kBvh): kWavesPerBlock x L.stack_depth x 64 lanes, sized per scene at launch
     extern __shared__ uint32_t dyn_stacks[];
 
@@ -1934,7 +1957,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         if (__ballot(alive || waiting || held || (kQueue && !exhausted)) == 0) break;  // wave-uniform exit
         RT_STAMP(t_a);
         RT_ACC(7, t_q, t_a);
-        if (alive && need_cam) {
+        if constexpr (kCamPf) {
+            // Camera slots. A lane starting a sample takes it from its slot when it was prepared;
+            // the camera pass (Philox seeding, getRay's draws and arithmetic) runs when some lane
+            // must start a sample that is not prepared, or once RT_CAM_BATCH lanes lack a prepared
+            // next sample - and then for all of those lanes at once: a lane that is tracing
+            // prepares its item's next sample into the slot. Each sample's ray and stream are the
+            // same whichever pass computes them (the stream is keyed by pixel and sample).
+            CamSlots& C = cslots[wave];
+            const bool now = alive && need_cam && !(item & kPrepared);
+            const bool nxt = alive && !need_cam && !(item & kPrepared) && towner < 0 && s + SP < own_end;
+            if (__ballot(now) != 0 || __popcll(__ballot(nxt)) >= RT_CAM_BATCH) {
+                if (now || nxt) {
+                    if (kQueue) {
+                        int ic, ilr;
+                        queue_item(L, item, ic, px, ilr);
+                        y = global_row_of(L, ilr);
+                        pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
+                    }
+                    Rng r2{1u, 0u, 0u, 0u};
+                    const Ray cr = camera_sample(cam, L, r2, pixel, px, y, now ? s : s + SP, (float)(L.width - 1),
+                                                 (float)(L.height - 1));
+                    C.a[lane] = float4{cr.o.x, cr.o.y, cr.o.z, cr.d.x};
+                    C.b[lane] = float4{cr.d.y, cr.d.z, cr.time, __uint_as_float(r2.s0)};
+                    C.c[lane] = uint4{r2.s1, r2.s2, r2.s3, 0u};
+                    item |= kPrepared;
+                }
+            }
+            const bool started = alive && need_cam && (item & kPrepared);  // prepared earlier or by this pass
+            if (started) {
+                const float4 a = C.a[lane], b = C.b[lane];
+                const uint4 e = C.c[lane];
+                ray = Ray{{a.x, a.y, a.z}, {a.w, b.x, b.y}, b.z};
+                rng = Rng{__float_as_uint(b.w), e.x, e.y, e.z};
+                item &= ~kPrepared;
+                need_cam = false;
+                thr = v3{1.0f, 1.0f, 1.0f};
+                depth = 0;
+                if (L.max_depth <= 0)  // rayColor with BOUNCES = 0 returns black
+                    sample_done(L, v3{0.0f, 0.0f, 0.0f}, SP, item & ~kPrepared, own_end, s, sum, thr, alive, need_cam,
+                                towner, held, waiting, tl_pack);
+            }
+        } else if (alive && need_cam) {
             if (kQueue) {
                 int ic, ilr;
                 queue_item(L, item, ic, px, ilr);
@@ -1946,7 +2010,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             depth = 0;
             need_cam = false;
             if (L.max_depth <= 0)  // rayColor with BOUNCES = 0 returns black
-                sample_done(L, v3{0.0f, 0.0f, 0.0f}, SP, item, own_end, s, sum, thr, alive, need_cam, towner,
+                sample_done(L, v3{0.0f, 0.0f, 0.0f}, SP, item & ~kPrepared, own_end, s, sum, thr, alive, need_cam, towner,
                             held, waiting, tl_pack);
         }
         const bool live = alive && !need_cam;
@@ -2069,7 +2133,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             done = true;
         }
         if (done)
-            sample_done(L, contrib, SP, item, own_end, s, sum, thr, alive, need_cam, towner, held, waiting,
+            sample_done(L, contrib, SP, item & ~kPrepared, own_end, s, sum, thr, alive, need_cam, towner, held, waiting,
                         tl_pack);
 #ifdef RT_STAMPS
         {
@@ -3193,7 +3257,7 @@ uint32_t kernel_build_flags() {
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
     !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || RT_PT_WAVES != 5 || \
-    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE || !RT_NOSPH_VARIANT || !RT_BVH_PARTS_VARIANT || !RT_LEAF_BATCH || !RT_SG_BATCH || !RT_BVH_PAIRS || !RT_SG_PAIRS || !RT_PT_PAIRS
+    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE || !RT_NOSPH_VARIANT || !RT_BVH_PARTS_VARIANT || !RT_LEAF_BATCH || !RT_SG_BATCH || !RT_BVH_PAIRS || !RT_SG_PAIRS || !RT_PT_PAIRS || !RT_CAM_SLOTS || RT_CAM_BATCH != 32
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;
