@@ -1543,8 +1543,10 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 // kernel at 4 (128 VGPRs, spill-free; its sphere-group-only and simple-scene mesh variants at 5), the linear-scan
 // rayColor kernel at 6 (89 VGPRs at 5
 // since it no longer carries the medium test; 9 spilled at 6 and still faster), its
-// sphere-free variant at 7, its media variant at 6 and the pathTrace kernel at 5 (same-box
-// A/B in DESIGN.md §4; profiles/r02/ab_occ*.txt, ab_no_medium.txt, ab_no_spheres.txt).
+// sphere-free variant at 7, its media variant at 6 and the pathTrace kernel at 6 (same-box
+// A/B in DESIGN.md §4; profiles/r02/ab_occ*.txt, ab_no_medium.txt, ab_no_spheres.txt; pathTrace
+// at 6 since it derives the pixel from the work item, 6 VGPRs spilled and 7 % faster than 5:
+// profiles/r03/ptd/).
 // -DRT_WAVES_PER_EU=k forces all to k.
 #ifndef RT_BVH_WAVES
 #define RT_BVH_WAVES 4
@@ -1565,7 +1567,7 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #define RT_BVH_SIMPLE_WAVES 5
 #endif
 #ifndef RT_PT_WAVES
-#define RT_PT_WAVES 5
+#define RT_PT_WAVES 6
 #endif
 #ifdef RT_WAVES_PER_EU
 #undef RT_BVH_WAVES
@@ -2594,6 +2596,9 @@ __device__ __forceinline__ void pt_leaf(const KTri* __restrict__ ktris,
     __builtin_amdgcn_wave_barrier();
 }
 
+#ifndef RT_PT_DERIVE
+#define RT_PT_DERIVE 1  // pathTrace queue mode derives the pixel from the work item at the camera (0: kept, A/B)
+#endif
 #ifndef RT_PT_PAIRS
 #define RT_PT_PAIRS 1  // pathTrace traversal over child-pair records (cf_child_pairs; 0: node records, A/B)
 #endif
@@ -2930,11 +2935,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
         const bool has_mesh = L.pt_has_mesh != 0;
         if (kQueue) {
             queue_refill(L, lane, alive, exhausted, shard, shards_tried, [&](uint32_t it) {
+#if RT_PT_DERIVE
+                // only `item` is kept across the traversal: the pixel is derived from it at the
+                // camera (as render_kernel does), which frees four VGPRs for the traversal
+                int ic, ipx, ilr;
+                if (!queue_item(L, it, ic, ipx, ilr)) return;  // past the frame edge: ask again
+                item = it;
+                s = ic;
+#else
                 if (!queue_item(L, it, c, px, lrow)) return;  // past the frame edge: ask again
                 item = it;
                 y = global_row_of(L, lrow);
                 pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
                 s = c;
+#endif
                 sum = v3{0.0f, 0.0f, 0.0f};
                 alive = s < L.spp;
                 // a sub-stream with no samples (S > spp) still owns its partial-sum slot
@@ -2944,6 +2958,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
         }
         if (__ballot(alive || (kQueue && !exhausted)) == 0) break;
         if (alive && need_cam) {
+#if RT_PT_DERIVE
+            if (kQueue) {
+                int ic, ilr;
+                queue_item(L, item, ic, px, ilr);
+                y = global_row_of(L, ilr);
+                pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
+            }
+#endif
             const Ray r = camera_sample(cam, L, rng, pixel, px, y, s, (float)(L.width - 1), (float)(L.height - 1));
             o = r.o;
             d = r.d;
@@ -3256,8 +3278,8 @@ uint32_t kernel_build_flags() {
     f |= 2u;  // RT_BUILD_STAMPS
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
-    !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || RT_PT_WAVES != 5 || \
-    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE || !RT_NOSPH_VARIANT || !RT_BVH_PARTS_VARIANT || !RT_LEAF_BATCH || !RT_SG_BATCH || !RT_BVH_PAIRS || !RT_SG_PAIRS || !RT_PT_PAIRS || !RT_CAM_SLOTS || RT_CAM_BATCH != 32
+    !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || RT_PT_WAVES != 6 || \
+    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE || !RT_NOSPH_VARIANT || !RT_BVH_PARTS_VARIANT || !RT_LEAF_BATCH || !RT_SG_BATCH || !RT_BVH_PAIRS || !RT_SG_PAIRS || !RT_PT_PAIRS || !RT_CAM_SLOTS || RT_CAM_BATCH != 32 || !RT_PT_DERIVE
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;
