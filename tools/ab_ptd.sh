@@ -1,3 +1,6 @@
+#!/bin/bash
+# Same-box pathTrace A/B behind DESIGN §4 (late round 3; profiles/r03/ptd/). Libraries as built then:
+# librtmi.so = RT_PT_DERIVE at 5 waves, librtmi_pt6.so = -DRT_PT_WAVES=6, librtmi_base.so = -DRT_PT_DERIVE=0.
 set -u
 cd "${GRAFT_REPO_ROOT}"
 O=gpurun_out/r03i_ptd; mkdir -p $O
