@@ -1,7 +1,7 @@
 """Does overlapping consecutive frames fill the SIMDs that a launch's tail leaves idle?
 Renders K frames (rank 0's shard of a world-W row tiling) back to back on one context and
 stream, then rotating over n contexts on n streams, and prints ms per frame of each.
-Usage: [SCENE=cornellbox1] [CTX="1 2"] python tools/overlap_probe.py W [K]"""
+Usage: [SCENE=cornellbox1] [CTX="1 2"] [LANES=0] python tools/overlap_probe.py W [K]"""
 import os
 import sys
 import time
@@ -23,7 +23,8 @@ for r in rs:
     getattr(rtmi, loader)(r, W, H)
 outs = [torch.empty((H, W, 3), dtype=torch.float32, device="cuda") for _ in rs]
 streams = [torch.cuda.Stream() for _ in rs]
-p = rs[0].params(W, H, SPP, DEPTH, 1984, 0, 2, 0, world, 0, bench.INTEGRATOR.get(SCENE, "rayColor"))
+LANES = int(os.environ.get("LANES", "0"))  # sub-streams per pixel (0 = auto)
+p = rs[0].params(W, H, SPP, DEPTH, 1984, 0, 2, 0, world, LANES, bench.INTEGRATOR.get(SCENE, "rayColor"))
 
 
 def run(n_ctx):
@@ -38,4 +39,4 @@ def run(n_ctx):
 
 for n in NCTX + NCTX:
     run(n)  # warm-up of this mode
-    print(f"{SCENE} world {world}: {n} context(s) {run(n):.4f} ms/frame", flush=True)
+    print(f"{SCENE} world {world} lanes {LANES}: {n} context(s) {run(n):.4f} ms/frame", flush=True)
