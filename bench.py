@@ -79,6 +79,8 @@ def parse():
                          "(tools/ctx_probe.sh, tools/layout_probe.sh: CB1 N = 8 shard 1.00 / 0.887 / 0.842 / "
                          "0.879 ms/frame with 1 / 2 / 3 / 4 contexts, N = 1 5.88 -> 5.82 from 2 to 3; the 300 ms "
                          "bunny frame 2.5 %% and the pathTrace materialball frame 2 %% slower with 3)")
+    ap.add_argument("--in-flight-layout", action="store_true",
+                    help="use the frames-in-flight layout even without overlap (profiling passes of the timed layout)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="one context and stream: consecutive frames do not overlap (per-launch roofline)")
     ap.add_argument("--cpu-spp", type=int, default=None)
@@ -296,11 +298,15 @@ def measure(args, world, rank, local, rehearsal):
                             device=torch.device("cpu") if rehearsal else torch.device("cuda", local),
                             pipeline=world > 1, streams=streams)
     integrator = INTEGRATOR.get(args.scene, "rayColor")
-    params = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, world, args.lanes, integrator)
+    # three or more frames in flight: the library may pick a layout for throughput
+    # (RT_RENDER_FRAMES_IN_FLIGHT; the isolated frames below use the same layout)
+    in_flight = (overlap and n_ctx >= 3) or args.in_flight_layout
+    params = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, world, args.lanes, integrator,
+                      frames_in_flight=in_flight)
     # timed launches add to the device counters (one read after the loop, no
     # per-frame host sync); each context's first timed launch resets them
     params_keep = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, world, args.lanes, integrator,
-                           keep_counters=True)
+                           keep_counters=True, frames_in_flight=in_flight)
     stream = torch.cuda.current_stream()
     scratch = torch.empty(frame.tile.shape, dtype=torch.float32, device="cuda") if rehearsal else None
 
@@ -398,7 +404,7 @@ def measure(args, world, rank, local, rehearsal):
         "lanes_per_pixel": int(st["lanes_per_pixel"]), "refill": int(st["refill"]),
         "queue_blocks": int(st["queue_blocks"]), "variant": st["variant_name"],
         "object_bytes_per_segment": object_bytes_per_segment(r) if integrator != "pathTrace" else 0,
-        "n_cu": n_cu, "overlap": overlap, "contexts": len(rs),
+        "n_cu": n_cu, "overlap": overlap, "contexts": len(rs), "frames_in_flight": in_flight,
     }
     for rr in rs:
         rr.close()
@@ -505,6 +511,7 @@ def build_line(args, agg: dict, world: int, cpu=None) -> dict:
             "row_block": args.row_block, "lanes_per_pixel": agg["lanes_per_pixel"],
             "variant": agg["variant"], "queue": agg["queue_blocks"] > 0,
             "refill": agg["refill"], "queue_blocks": agg["queue_blocks"], "contexts": agg.get("contexts", 1),
+            "frames_in_flight": bool(agg.get("frames_in_flight", False)),
             "kernel_source_sha": sha,
             "parallelism": f"row-tiles x{world} + RCCL gather" if world > 1 else "single GPU",
             "segments_per_frame": int(segs / K),

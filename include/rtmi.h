@@ -79,7 +79,13 @@ typedef struct rt_render_params {
                                pathTrace bounces max_depth times (reference: 5). */
     uint32_t flags;         /* RT_RENDER_KEEP_COUNTERS: add this launch's counters to the
                                previous ones instead of resetting them (one rt_sync_stats
-                               after many launches, no per-launch host sync) */
+                               after many launches, no per-launch host sync).
+                               RT_RENDER_FRAMES_IN_FLIGHT: the caller keeps three or more
+                               launches in flight on other contexts/streams (frame overlap);
+                               the auto layout (lanes_per_pixel = 0) of a linear-scan rayColor
+                               work-queue launch then takes at most 16 sub-streams per pixel
+                               (items of more samples, whose longer tail the next frames fill).
+                               The image is that of lanes_per_pixel = the reported value. */
     /* Column window of every owned row: columns [col_begin, col_begin + col_count);
      * col_count = 0 = the whole width. Output rows are col_count wide. The pixels are
      * those of the full frame (camera and RNG keyed by the frame position). */
@@ -92,7 +98,7 @@ typedef struct rt_render_params {
      * bit-identical. rt_render_stats.variant reports the kernel that ran. */
     int32_t schedule;
 } rt_render_params;
-enum { RT_RENDER_KEEP_COUNTERS = 1 };
+enum { RT_RENDER_KEEP_COUNTERS = 1, RT_RENDER_FRAMES_IN_FLIGHT = 2 };
 enum { RT_SCHEDULE_AUTO = 0, RT_SCHEDULE_STATIC = 1 };
 
 /* The megakernel instantiation a launch ran (rt_render_stats.variant). renderKernel

@@ -640,7 +640,8 @@ rt_status rt_scene_info(const rt_ctx* c, int32_t out[8]) {
 rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& L) {
     if (!p) return fail(c, RT_ERR_INVALID, "null params");
     if (c->device < 0) return fail(c, RT_ERR_NODEV, "context has no device");
-    if (p->flags & ~(uint32_t)RT_RENDER_KEEP_COUNTERS) return fail(c, RT_ERR_INVALID, "unknown flags");
+    if (p->flags & ~(uint32_t)(RT_RENDER_KEEP_COUNTERS | RT_RENDER_FRAMES_IN_FLIGHT))
+        return fail(c, RT_ERR_INVALID, "unknown flags");
     if (p->integrator != RT_INTEGRATOR_RAYCOLOR && p->integrator != RT_INTEGRATOR_PATHTRACE)
         return fail(c, RT_ERR_INVALID, "unknown integrator");
     if (p->integrator == RT_INTEGRATOR_RAYCOLOR && !c->committed)
@@ -680,6 +681,12 @@ rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& 
         return fail(c, RT_ERR_INVALID, "lanes_per_pixel must be 0 (auto) or a power of two <= 128 (64 static)");
     const bool bvh = p->integrator == RT_INTEGRATOR_PATHTRACE || !c->scene.nodes.empty();
     rt::choose_layout(L, s, queue, bvh);
+    // Frames in flight: with three launches overlapped, CornellBox1 runs faster at S = 16 than at
+    // the auto S = 32 (N = 1 5.55 vs 5.68 ms/frame, N = 8 shard 0.816 vs 0.834) and slower alone
+    // (5.85 vs 5.83): larger items cut the dequeues, and the next frames fill their longer tail
+    // (profiles/r03/lanes/). BVH launches keep their S (Suzanne, materialball: slower).
+    if (s == 0 && queue && !bvh && (p->flags & RT_RENDER_FRAMES_IN_FLIGHT) && L.lanes_per_pixel > 16)
+        rt::choose_layout(L, 16, queue, bvh);
     L.accumulate = 0;
     L.accum_scale = 0.0f;
     L.u8 = nullptr;

@@ -318,17 +318,20 @@ class Renderer:
     @staticmethod
     def params(width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,
                row_rank=0, row_world=1, lanes_per_pixel=1, integrator="rayColor",
-               keep_counters=False, col_begin=0, col_count=0, schedule="auto") -> RenderParams:
+               keep_counters=False, col_begin=0, col_count=0, schedule="auto",
+               frames_in_flight=False) -> RenderParams:
         """rt_render_params; schedule "auto" = the persistent work queue (the static grid when
-        the frame's partial sums do not fit), "static" = the static grid (same image)."""
+        the frame's partial sums do not fit), "static" = the static grid (same image).
+        frames_in_flight: the caller overlaps three or more launches (RT_RENDER_FRAMES_IN_FLIGHT;
+        the auto layout of linear-scan launches then takes at most 16 sub-streams)."""
+        flags = (KEEP_COUNTERS if keep_counters else 0) | (FRAMES_IN_FLIGHT if frames_in_flight else 0)
         return RenderParams(width, height, spp, max_depth, seed, sample_offset, row_block,
                             row_rank, row_world, lanes_per_pixel, _integrator(integrator),
-                            KEEP_COUNTERS if keep_counters else 0, col_begin, col_count,
-                            SCHEDULES[schedule])
+                            flags, col_begin, col_count, SCHEDULES[schedule])
 
     def render(self, width, height, spp, max_depth, seed=1984, sample_offset=0, row_block=1,
                row_rank=0, row_world=1, lanes_per_pixel=1, integrator="rayColor",
-               col_begin=0, col_count=0, schedule="auto") -> np.ndarray:
+               col_begin=0, col_count=0, schedule="auto", frames_in_flight=False) -> np.ndarray:
         """Mean radiance of the owned rows, shape (rows, width, 3), y = 0 bottom.
         lanes_per_pixel=1 keeps the reference's sequential per-pixel sample sum;
         0 lets the library pick a lane layout that fills the GPU. integrator
@@ -337,7 +340,8 @@ class Renderer:
         col_count > 0 renders only columns [col_begin, col_begin + col_count) of the
         frame's rows (shape (rows, col_count, 3)); the pixels are the full frame's."""
         p = self.params(width, height, spp, max_depth, seed, sample_offset, row_block, row_rank,
-                        row_world, lanes_per_pixel, integrator, False, col_begin, col_count, schedule)
+                        row_world, lanes_per_pixel, integrator, False, col_begin, col_count, schedule,
+                        frames_in_flight)
         rows = owned_rows(height, row_block, row_rank, row_world)
         out = np.zeros((rows, col_count or width, 3), np.float32)
         self._check(self.L.rt_render(self.ctx, C.byref(p), out.ctypes.data_as(C.POINTER(C.c_float))))
@@ -388,6 +392,7 @@ class Renderer:
 REFLECTION_TYPES = {"DIFFUSE": 0, "METAL": 1, "SPECULAR": 2, "REFRACTION": 3, "COAT": 4}
 INTEGRATORS = {"rayColor": 0, "pathTrace": 1}
 KEEP_COUNTERS = 1  # rtmi.h RT_RENDER_KEEP_COUNTERS
+FRAMES_IN_FLIGHT = 2  # rtmi.h RT_RENDER_FRAMES_IN_FLIGHT
 
 
 def _reflection_type(t) -> int:

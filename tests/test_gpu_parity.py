@@ -222,6 +222,26 @@ def test_auto_lane_layout(rtmi):
         assert r.stats()["lanes_per_pixel"] == 8  # 4M pixels x 8 = 2^25 work items
 
 
+def test_frames_in_flight_layout(rtmi):
+    # RT_RENDER_FRAMES_IN_FLIGHT: the auto layout of linear-scan work-queue launches takes at
+    # most 16 sub-streams (rt_capi.cpp validate); the image is that of the reported S, and the
+    # hint leaves explicit layouts, small S and BVH launches alone
+    with rtmi.Renderer(0) as r:
+        rtmi.cornell_box1(r, 48, 32)
+        img = r.render(48, 32, 64, 4, lanes_per_pixel=0, frames_in_flight=True)
+        assert r.stats()["lanes_per_pixel"] == 16
+        assert np.array_equal(img, r.render(48, 32, 64, 4, lanes_per_pixel=16))
+        assert r.stats()["lanes_per_pixel"] == 16
+        r.render(48, 32, 64, 4, lanes_per_pixel=32, frames_in_flight=True)
+        assert r.stats()["lanes_per_pixel"] == 32
+        r.render(48, 32, 8, 4, lanes_per_pixel=0, frames_in_flight=True)
+        assert r.stats()["lanes_per_pixel"] == 8
+    with rtmi.Renderer(0) as r:
+        rtmi.suzanne_cornell_box(r, 64, 64)
+        r.render(64, 64, 32, 3, lanes_per_pixel=0, frames_in_flight=True)
+        assert r.stats()["lanes_per_pixel"] == 32
+
+
 def test_auto_lane_layout_bvh(rtmi):
     # launches that traverse BVHs: largest power of two S <= min(128, spp) with
     # pixels * S <= 2^27 (rt_kernel.h choose_layout)
