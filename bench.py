@@ -488,6 +488,7 @@ def build_line(args, agg: dict, world: int, cpu=None) -> dict:
     valu_launch = vp["valu_insts_per_segment"] * seg_launch if vp else None
     achieved = valu_launch / (t_iso * 1e-3) / 1e9 if vp and not vp_bad else None
     achieved_ovl = valu_launch / (ms_frame * 1e-3) / 1e9 if vp and not vp_bad else None
+    lane_u = vp.get("valu_lane_util") if vp and not vp_bad else None
     tp = load_pmc_traffic(workload)
     tp_bad = profile_check(tp, agg["variant"], sha)
     traffic = float(tp["hbm_bytes_per_launch"]) if tp and not tp_bad else None
@@ -534,6 +535,11 @@ def build_line(args, agg: dict, world: int, cpu=None) -> dict:
             "peak": round(valu_peak, 1),
             "unit": "Ginst/s (wave64 VALU instructions)",
             "frac": round(achieved / valu_peak, 4) if achieved else None,
+            # issued wave-instructions count every masked-off lane as work: the profiled lane
+            # utilisation (SQ_THREAD_CYCLES_VALU / 64 / SQ_ACTIVE_INST_VALU of the same pass) turns
+            # frac into the fraction of the chip's lane-operations that did useful work
+            "valu_lane_util": round(lane_u, 4) if lane_u else None,
+            "useful_frac": round(achieved / valu_peak * lane_u, 4) if achieved and lane_u else None,
             "traffic": traffic,
             # the isolated launch's megakernel time (library event pair, combine pass excluded)
             "kernel_ms": round(t_iso, 4),
@@ -553,7 +559,8 @@ def build_line(args, agg: dict, world: int, cpu=None) -> dict:
                      "(kernel_ms: one launch at a time after the timed loop, library event pair, combine pass "
                      "excluded - what rocprofv3's kernel trace measures); frac_overlapped divides by the timed "
                      "frame time instead (two launches in flight); peak = CUs x 4 SIMDs x 2.4 GHz / 2 cycles per "
-                     "wave64 VALU op. traffic = HBM-side bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, "
+                     "wave64 VALU op; useful_frac = frac x valu_lane_util (the same pass's SQ_THREAD_CYCLES_VALU "
+                     "/ 64 / SQ_ACTIVE_INST_VALU: active lanes per issued instruction). traffic = HBM-side bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, "
                      "profiles/pmc_traffic.json), hbm_frac its share of 8 TB/s; a profile of another kernel "
                      "symbol or other kernel sources is not used (profile_mismatch); record_* = SURVEY 8(d)'s "
                      "cache-served record-byte model"),

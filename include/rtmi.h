@@ -92,7 +92,8 @@ typedef struct rt_render_params {
     int32_t col_begin;
     int32_t col_count;
     /* Launch schedule: RT_SCHEDULE_AUTO (0) = the persistent work queue, or the static grid
-     * when the frame's partial sums do not fit (more than 2^32 items or 16 GB);
+     * when the frame's partial sums do not fit (2^31 items or more - bit 31 of an item index
+     * is the kernels' camera-slot flag - or more than 16 GB);
      * RT_SCHEDULE_STATIC (1) = the static grid (one lane per (pixel, sub-stream), the
      * reference's launch shape). Both compute the same partial sums: the image is
      * bit-identical. rt_render_stats.variant reports the kernel that ran. */

@@ -108,6 +108,8 @@ def lib():
         L.orc_load_obj.argtypes = [C.c_char_p, fp, fp, fp, C.POINTER(fp)]
         L.orc_free.argtypes = [vp]
         L.orc_load_ply.argtypes = [C.c_char_p, fp, C.c_float, C.POINTER(fp)]
+        L.orc_bvh_image.restype = C.c_int64
+        L.orc_bvh_image.argtypes = [fp, C.c_int, C.POINTER(C.POINTER(C.c_uint8))]
         L.orc_camera.argtypes = [vp, fp, fp, fp] + [C.c_float] * 6
         L.orc_length.argtypes = [fp]
         L.orc_length.restype = C.c_float
@@ -177,6 +179,20 @@ def load_ply(path, offset=(0, 0, 0), max_coord=1.0) -> np.ndarray:
     arr = np.ctypeslib.as_array(p, shape=(max(n, 1) * 9,)).copy()[: n * 9]
     lib().orc_free(p)
     return arr.reshape(n, 9)
+
+
+def bvh_image(soup: np.ndarray) -> bytes:
+    """CreateBVH + Recurse + CreateCFBVH (BVH.cpp:94-497) with the reference's own
+    O(N x bins) split search over a triangle soup (n x 9 floats, e.g. load_ply's):
+    the `.bvh` cache image."""
+    soup = np.ascontiguousarray(soup, np.float32).reshape(-1, 9)
+    p = C.POINTER(C.c_uint8)()
+    n = lib().orc_bvh_image(soup.ctypes.data_as(C.POINTER(C.c_float)), len(soup), C.byref(p))
+    if n < 0:
+        raise ValueError("oracle BVH build failed")
+    img = C.string_at(p, n)
+    lib().orc_free(p)
+    return img
 
 
 def gamma_u8(rgb: np.ndarray) -> np.ndarray:

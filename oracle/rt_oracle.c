@@ -30,6 +30,8 @@
  *                                     (tinyobjloader/tiny_obj_loader.h:837-975,
  *                                     1397-1495)
  *   Canvas::gamma ................... Canvas.h:198-200
+ *   CreateBVH / Recurse / CreateCFBVH BVH.cpp:94-333, 335-392, 432-497 (the
+ *                                     reference's O(N x bins) split search)
  *
  * Deliberate, documented deviations from the reference:
  *  1. cuRAND XORWOW is replaced by a counter-based stream per (pixel, sample):
@@ -1590,4 +1592,184 @@ int orc_pt_render(const PtScene* p, const Scene* cam, int width, int height, int
     }
     if (stats) { stats[0] = segs; stats[1] = tests; stats[2] = (uint64_t)overflow; }
     return 0;
+}
+
+/* ---- BVH construction: CreateBVH + Recurse + CreateCFBVH (BVH.cpp:94-333, 335-392,
+ * 432-497), the reference's own O(N x bins) split search. It pins the product builder's
+ * O(N log N) search (rt_bvh.cpp search_fast) and the GPU builder on meshes the reference
+ * ships no `.bvh` cache for (tests/test_bvh.py). Output: the `.bvh` cache image
+ * (BVH.cpp:537-540): u32 nodes, u32 indices, 32 B nodes (bottom, top, u0, u1), i32
+ * indices. ---- */
+typedef struct { V3 bottom, top, center; int32_t tri; } OrcBBox; /* BBoxTmp, BVH.cpp:60-75 */
+typedef struct { V3 bottom, top; int left, right; int32_t* tris; int ntris; } OrcBNode;
+typedef struct { OrcBNode* v; int n, cap; } OrcBPool;
+
+static V3 min3_(V3 a, V3 b) { return v3(a.x < b.x ? a.x : b.x, a.y < b.y ? a.y : b.y, a.z < b.z ? a.z : b.z); }
+static V3 max3_(V3 a, V3 b) { return v3(a.x > b.x ? a.x : b.x, a.y > b.y ? a.y : b.y, a.z > b.z ? a.z : b.z); }
+static float axis_(V3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+
+static int bpool_new(OrcBPool* P) {
+    if (P->n == P->cap) {
+        P->cap = P->cap ? 2 * P->cap : 1024;
+        P->v = (OrcBNode*)realloc(P->v, (size_t)P->cap * sizeof(OrcBNode));
+    }
+    OrcBNode* b = &P->v[P->n];
+    memset(b, 0, sizeof *b);
+    b->left = b->right = -1;
+    return P->n++;
+}
+
+static int bvh_leaf_(OrcBPool* P, const OrcBBox* work, size_t n) {
+    int me = bpool_new(P);
+    P->v[me].tris = (int32_t*)malloc((n ? n : 1) * sizeof(int32_t));
+    for (size_t i = 0; i < n; ++i) P->v[me].tris[i] = work[i].tri;
+    P->v[me].ntris = (int)n;
+    return me;
+}
+
+/* Recurse (BVH.cpp:94-333). `work` is freed here (work.clear()). */
+static int bvh_recurse_(OrcBPool* P, OrcBBox* work, size_t n, int depth) {
+    if (n < 4) {
+        int l = bvh_leaf_(P, work, n);
+        free(work);
+        return l;
+    }
+    V3 bottom = v3(FLT_MAX_, FLT_MAX_, FLT_MAX_), top = v3(-FLT_MAX_, -FLT_MAX_, -FLT_MAX_);
+    for (size_t i = 0; i < n; ++i) {
+        bottom = min3_(bottom, work[i].bottom);
+        top = max3_(top, work[i].top);
+    }
+    float side1 = top.x - bottom.x, side2 = top.y - bottom.y, side3 = top.z - bottom.z;
+    float min_cost = (float)n * (side1 * side2 + side2 * side3 + side3 * side1);
+    float best_split = FLT_MAX_;
+    int best_axis = -1;
+    for (int axis = 0; axis < 3; ++axis) {
+        float start = axis_(bottom, axis), stop = axis_(top, axis);
+        if (fabsf(stop - start) < 1e-4) continue; /* float vs double literal, as BVH.cpp:164 */
+        float step = (stop - start) / (1024.0f / ((float)depth + 1.0f));
+        for (float split = start + step; split < stop - step; split += step) {
+            V3 lb = v3(FLT_MAX_, FLT_MAX_, FLT_MAX_), lt = v3(-FLT_MAX_, -FLT_MAX_, -FLT_MAX_);
+            V3 rb = v3(FLT_MAX_, FLT_MAX_, FLT_MAX_), rt = v3(-FLT_MAX_, -FLT_MAX_, -FLT_MAX_);
+            int nl = 0, nr = 0;
+            for (size_t i = 0; i < n; ++i) {
+                if (axis_(work[i].center, axis) < split) {
+                    lb = min3_(lb, work[i].bottom);
+                    lt = max3_(lt, work[i].top);
+                    nl++;
+                } else {
+                    rb = min3_(rb, work[i].bottom);
+                    rt = max3_(rt, work[i].top);
+                    nr++;
+                }
+            }
+            if (nl <= 1 || nr <= 1) continue;
+            float l1 = lt.x - lb.x, l2 = lt.y - lb.y, l3 = lt.z - lb.z;
+            float r1 = rt.x - rb.x, r2 = rt.y - rb.y, r3 = rt.z - rb.z;
+            float sl = l1 * l2 + l2 * l3 + l3 * l1, sr = r1 * r2 + r2 * r3 + r3 * r1;
+            float cost = sl * (float)nl + sr * (float)nr;
+            if (cost < min_cost) {
+                min_cost = cost;
+                best_split = split;
+                best_axis = axis;
+            }
+        }
+    }
+    if (best_axis == -1) {
+        int l = bvh_leaf_(P, work, n);
+        free(work);
+        return l;
+    }
+    OrcBBox* left = (OrcBBox*)malloc(n * sizeof(OrcBBox));
+    OrcBBox* right = (OrcBBox*)malloc(n * sizeof(OrcBBox));
+    size_t nl = 0, nr = 0;
+    V3 lb = v3(FLT_MAX_, FLT_MAX_, FLT_MAX_), lt = v3(-FLT_MAX_, -FLT_MAX_, -FLT_MAX_);
+    V3 rb = v3(FLT_MAX_, FLT_MAX_, FLT_MAX_), rt = v3(-FLT_MAX_, -FLT_MAX_, -FLT_MAX_);
+    for (size_t i = 0; i < n; ++i) {
+        if (axis_(work[i].center, best_axis) < best_split) {
+            left[nl++] = work[i];
+            lb = min3_(lb, work[i].bottom);
+            lt = max3_(lt, work[i].top);
+        } else {
+            right[nr++] = work[i];
+            rb = min3_(rb, work[i].bottom);
+            rt = max3_(rt, work[i].top);
+        }
+    }
+    free(work);
+    int me = bpool_new(P);
+    int l = bvh_recurse_(P, left, nl, depth + 1);
+    P->v[l].bottom = lb;
+    P->v[l].top = lt;
+    int r = bvh_recurse_(P, right, nr, depth + 1);
+    P->v[r].bottom = rb;
+    P->v[r].top = rt;
+    P->v[me].left = l;
+    P->v[me].right = r;
+    return me;
+}
+
+/* PopulateCacheFriendlyBVH (BVH.cpp:432-465): depth first, left first. */
+static void bvh_populate_(const OrcBPool* P, int nd, unsigned* idx_boxes, unsigned* idx_tri, float* nodes,
+                          int32_t* tri_list) {
+    unsigned cur = *idx_boxes;
+    const OrcBNode* b = &P->v[nd];
+    float* c = nodes + 8 * (size_t)cur;
+    c[0] = b->bottom.x; c[1] = b->bottom.y; c[2] = b->bottom.z;
+    c[3] = b->top.x; c[4] = b->top.y; c[5] = b->top.z;
+    uint32_t u0, u1;
+    if (b->left >= 0) {
+        unsigned il = ++*idx_boxes;
+        bvh_populate_(P, b->left, idx_boxes, idx_tri, nodes, tri_list);
+        unsigned ir = ++*idx_boxes;
+        bvh_populate_(P, b->right, idx_boxes, idx_tri, nodes, tri_list);
+        u0 = il;
+        u1 = ir;
+    } else {
+        u0 = 0x80000000u | (uint32_t)b->ntris;
+        u1 = *idx_tri;
+        for (int k = 0; k < b->ntris; ++k) tri_list[(*idx_tri)++] = b->tris[k];
+    }
+    memcpy(c + 6, &u0, 4);
+    memcpy(c + 7, &u1, 4);
+}
+
+/* CreateBVH (BVH.cpp:335-392) over a triangle soup (9 floats per triangle, the vertices
+ * of idx1, idx2, idx3) + CreateCFBVH. Returns the image size, *out malloc'ed; -1 on
+ * failure. */
+int64_t orc_bvh_image(const float* soup, int n_tris, uint8_t** out) {
+    if (n_tris < 1) return -1;
+    OrcBBox* work = (OrcBBox*)malloc((size_t)n_tris * sizeof(OrcBBox));
+    V3 bottom = v3(FLT_MAX_, FLT_MAX_, FLT_MAX_), top = v3(-FLT_MAX_, -FLT_MAX_, -FLT_MAX_);
+    for (int j = 0; j < n_tris; ++j) {
+        OrcBBox b;
+        b.tri = j;
+        b.bottom = v3(FLT_MAX_, FLT_MAX_, FLT_MAX_);
+        b.top = v3(-FLT_MAX_, -FLT_MAX_, -FLT_MAX_);
+        for (int k = 0; k < 3; ++k) {
+            const float* q = soup + 9 * (size_t)j + 3 * k;
+            b.bottom = min3_(b.bottom, v3(q[0], q[1], q[2]));
+        }
+        for (int k = 0; k < 3; ++k) {
+            const float* q = soup + 9 * (size_t)j + 3 * k;
+            b.top = max3_(b.top, v3(q[0], q[1], q[2]));
+        }
+        bottom = min3_(bottom, b.bottom);
+        top = max3_(top, b.top);
+        b.center = vmul(vadd(b.top, b.bottom), 0.5f);
+        work[j] = b;
+    }
+    OrcBPool P = {NULL, 0, 0};
+    int root = bvh_recurse_(&P, work, (size_t)n_tris, 0);
+    P.v[root].bottom = bottom;
+    P.v[root].top = top;
+    size_t nn = (size_t)P.n, size = 8 + nn * 32 + (size_t)n_tris * 4;
+    uint8_t* img = (uint8_t*)calloc(size, 1);
+    uint32_t h[2] = {(uint32_t)nn, (uint32_t)n_tris};
+    memcpy(img, h, 8);
+    unsigned idx_boxes = 0, idx_tri = 0;
+    bvh_populate_(&P, root, &idx_boxes, &idx_tri, (float*)(img + 8), (int32_t*)(img + 8 + nn * 32));
+    for (int i = 0; i < P.n; ++i) free(P.v[i].tris);
+    free(P.v);
+    *out = img;
+    return (int64_t)size;
 }

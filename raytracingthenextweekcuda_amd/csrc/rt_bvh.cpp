@@ -48,7 +48,6 @@ struct Builder {
         return (int)pool.size() - 1;
     }
 
-    bool reference_search = false;  // true: the reference's O(N x bins) split search
     size_t leaf_min_split = 4;      // Recurse makes a leaf below 4 entries (BVH.cpp:106)
 
     // Split search of Recurse (BVH.cpp:136-260) in O(N log N + bins log N) per
@@ -147,40 +146,9 @@ struct Builder {
         float best_split = FLT_MAX;
         int best_axis = -1;
 
-        if (!reference_search) search_fast(work, bottom, top, depth, min_cost, best_split, best_axis);
-        for (int axis = 0; reference_search && axis < 3; ++axis) {
-            const float start = axis_of(bottom, axis), stop = axis_of(top, axis);
-            // fabsf(stop - start) < 1e-4 compares in double (BVH.cpp:164).
-            if ((double)fabsf(stop - start) < 1e-4) continue;
-            const float step = (stop - start) / (1024.0f / ((float)depth + 1.0f));
-            for (float split = start + step; split < stop - step; split += step) {
-                v3 lb{FLT_MAX, FLT_MAX, FLT_MAX}, lt{-FLT_MAX, -FLT_MAX, -FLT_MAX};
-                v3 rb{FLT_MAX, FLT_MAX, FLT_MAX}, rtp{-FLT_MAX, -FLT_MAX, -FLT_MAX};
-                int nl = 0, nr = 0;
-                for (const Entry& v : work) {
-                    if (axis_of(v.center, axis) < split) {
-                        lb = min3v(lb, v.bottom);
-                        lt = max3v(lt, v.top);
-                        ++nl;
-                    } else {
-                        rb = min3v(rb, v.bottom);
-                        rtp = max3v(rtp, v.top);
-                        ++nr;
-                    }
-                }
-                if (nl <= 1 || nr <= 1) continue;
-                const float l1 = lt.x - lb.x, l2 = lt.y - lb.y, l3 = lt.z - lb.z;
-                const float r1 = rtp.x - rb.x, r2 = rtp.y - rb.y, r3 = rtp.z - rb.z;
-                const float sl = l1 * l2 + l2 * l3 + l3 * l1;
-                const float sr = r1 * r2 + r2 * r3 + r3 * r1;
-                const float cost = sl * (float)nl + sr * (float)nr;
-                if (cost < min_cost) {
-                    min_cost = cost;
-                    best_split = split;
-                    best_axis = axis;
-                }
-            }
-        }
+        // (the reference's O(N x bins) loop, BVH.cpp:160-260, is restated in the oracle,
+        // oracle/rt_oracle.c orc_bvh_image, which tests/test_bvh.py compares with this search)
+        search_fast(work, bottom, top, depth, min_cost, best_split, best_axis);
         if (best_axis == -1) return make_leaf(work);
 
         std::vector<Entry> left, right;
@@ -331,8 +299,6 @@ void build_cf_bvh_boxes(const std::vector<v3>& bottoms, const std::vector<v3>& t
     }
     Builder B;
     B.leaf_min_split = (size_t)leaf_min_split;
-    // test knob: the reference's own O(N x bins) search (tests/test_bvh.py compares both)
-    B.reference_search = getenv("RTMI_BVH_REFERENCE_SEARCH") != nullptr;
     B.pool.reserve(nt);
     const int root = B.recurse(work, 0);
     B.pool[root].bottom = bottom;

@@ -514,6 +514,12 @@ static rt_status rt_process_triangle_data_impl(rt_ctx* c, const float offset[3],
             return fail(c, RT_ERR_INVALID, "pathTrace BVH depth " + std::to_string(b.max_depth) +
                                                " exceeds the traversal stack (" + std::to_string(rt::kBvhStackDepth) + ")");
     }
+    // the traversal's references pack a list position in 27 bits (kLeafRef | (count - 1) << 27 |
+    // first) and its leaf queue entries pack (position << 6 | owner lane) in 32: positions and
+    // triangles stay below 2^26, as build_mesh_pairs requires for the rayColor meshes
+    if (kt.size() >= (size_t(1) << 26) || b.tri_index.size() >= (size_t(1) << 26) ||
+        b.nodes.size() >= (size_t(1) << 30))
+        return fail(c, RT_ERR_INVALID, "pathTrace scene too large for the BVH references (2^26 triangles)");
     std::vector<rt::CFNode> dev_nodes = b.nodes;  // + the traversal's child-pair records
     int pair_depth = 0;
     bool empty_leaf = false;
@@ -1328,27 +1334,42 @@ struct rt_canvas {
     uint8_t* pixels;  // pixelBuffer (Canvas::gamma RGB8)
 };
 
+// The canvas entry points keep C++ exceptions (std::bad_alloc from an error message, say)
+// inside the ABI, as the *_impl wrappers of the other entry points do.
+template <typename F>
+static rt_status canvas_guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return RT_ERR_OOM;
+    } catch (...) {
+        return RT_ERR_INVALID;
+    }
+}
+
 extern "C" {
 
 rt_status rt_canvas_create(rt_ctx* c, int32_t width, int32_t height, rt_canvas** out) {
-    if (!c || !out) return RT_ERR_INVALID;
-    *out = nullptr;
-    if (c->device < 0) return fail(c, RT_ERR_NODEV, "canvas: context has no device");
-    if (width < 2 || height < 2 || (int64_t)width * height > ((int64_t)1 << 31))
-        return fail(c, RT_ERR_INVALID, "canvas: bad size");
-    RT_HIP(c, hipSetDevice(c->device));
-    const size_t n = (size_t)width * (size_t)height * 3;
-    rt_canvas* k = new (std::nothrow) rt_canvas{c, c->device, width, height, nullptr, nullptr};
-    if (!k) return fail(c, RT_ERR_OOM, "out of host memory");
-    if (hipMalloc((void**)&k->accum, n * sizeof(float)) != hipSuccess ||
-        hipMalloc((void**)&k->pixels, n) != hipSuccess || hipMemset(k->accum, 0, n * sizeof(float)) != hipSuccess ||
-        hipMemset(k->pixels, 0, n) != hipSuccess) {
-        (void)hipGetLastError();
-        rt_canvas_destroy(k);
-        return fail(c, RT_ERR_OOM, "canvas: device allocation failed");
-    }
-    *out = k;
-    return RT_OK;
+    return canvas_guarded([&]() -> rt_status {
+        if (!c || !out) return RT_ERR_INVALID;
+        *out = nullptr;
+        if (c->device < 0) return fail(c, RT_ERR_NODEV, "canvas: context has no device");
+        if (width < 2 || height < 2 || (int64_t)width * height > ((int64_t)1 << 31))
+            return fail(c, RT_ERR_INVALID, "canvas: bad size");
+        RT_HIP(c, hipSetDevice(c->device));
+        const size_t n = (size_t)width * (size_t)height * 3;
+        rt_canvas* k = new (std::nothrow) rt_canvas{c, c->device, width, height, nullptr, nullptr};
+        if (!k) return fail(c, RT_ERR_OOM, "out of host memory");
+        if (hipMalloc((void**)&k->accum, n * sizeof(float)) != hipSuccess ||
+            hipMalloc((void**)&k->pixels, n) != hipSuccess || hipMemset(k->accum, 0, n * sizeof(float)) != hipSuccess ||
+            hipMemset(k->pixels, 0, n) != hipSuccess) {
+            (void)hipGetLastError();
+            rt_canvas_destroy(k);
+            return fail(c, RT_ERR_OOM, "canvas: device allocation failed");
+        }
+        *out = k;
+        return RT_OK;
+    });
 }
 
 void rt_canvas_destroy(rt_canvas* k) {
@@ -1360,50 +1381,60 @@ void rt_canvas_destroy(rt_canvas* k) {
 }
 
 rt_status rt_canvas_clear_accumulation(rt_canvas* k) {
-    if (!k) return RT_ERR_INVALID;
-    rt_ctx* c = k->ctx;
-    RT_HIP(c, hipSetDevice(c->device));
-    RT_HIP(c, hipMemset(k->accum, 0, (size_t)k->width * k->height * 3 * sizeof(float)));
-    return RT_OK;
+    return canvas_guarded([&]() -> rt_status {
+        if (!k) return RT_ERR_INVALID;
+        rt_ctx* c = k->ctx;
+        RT_HIP(c, hipSetDevice(c->device));
+        RT_HIP(c, hipMemset(k->accum, 0, (size_t)k->width * k->height * 3 * sizeof(float)));
+        return RT_OK;
+    });
 }
 
 rt_status rt_canvas_accumulate(rt_canvas* k, const rt_render_params* p, uint32_t sample_count) {
-    if (!k || !p) return RT_ERR_INVALID;
-    rt_ctx* c = k->ctx;
-    if (p->width != k->width || p->height != k->height || p->row_world != 1 || p->col_count != 0)
-        return fail(c, RT_ERR_INVALID, "canvas_accumulate: params must cover the canvas's full frame");
-    if (sample_count == 0) return fail(c, RT_ERR_INVALID, "canvas_accumulate: sample_count must be >= 1");
-    rt_status s = rt_accumulate(c, p, k->accum, sample_count, k->pixels, nullptr);
-    if (s != RT_OK) return s;
-    RT_HIP(c, hipStreamSynchronize(nullptr));
-    s = rt_sync_stats(c, nullptr);
-    if (s != RT_OK) return s;
-    if (c->last.overflow) return fail(c, RT_ERR_OVERFLOW, "BVH traversal stack overflow");
-    return RT_OK;
+    return canvas_guarded([&]() -> rt_status {
+        if (!k || !p) return RT_ERR_INVALID;
+        rt_ctx* c = k->ctx;
+        if (p->width != k->width || p->height != k->height || p->row_world != 1 || p->col_count != 0)
+            return fail(c, RT_ERR_INVALID, "canvas_accumulate: params must cover the canvas's full frame");
+        if (sample_count == 0) return fail(c, RT_ERR_INVALID, "canvas_accumulate: sample_count must be >= 1");
+        rt_status s = rt_accumulate(c, p, k->accum, sample_count, k->pixels, nullptr);
+        if (s != RT_OK) return s;
+        RT_HIP(c, hipStreamSynchronize(nullptr));
+        s = rt_sync_stats(c, nullptr);
+        if (s != RT_OK) return s;
+        if (c->last.overflow) return fail(c, RT_ERR_OVERFLOW, "BVH traversal stack overflow");
+        return RT_OK;
+    });
 }
 
 rt_status rt_canvas_read_pixels(const rt_canvas* k, uint8_t* out) {
-    if (!k || !out) return RT_ERR_INVALID;
-    rt_ctx* c = k->ctx;
-    RT_HIP(c, hipSetDevice(c->device));
-    RT_HIP(c, hipMemcpy(out, k->pixels, (size_t)k->width * k->height * 3, hipMemcpyDeviceToHost));
-    return RT_OK;
+    return canvas_guarded([&]() -> rt_status {
+        if (!k || !out) return RT_ERR_INVALID;
+        rt_ctx* c = k->ctx;
+        RT_HIP(c, hipSetDevice(c->device));
+        RT_HIP(c, hipMemcpy(out, k->pixels, (size_t)k->width * k->height * 3, hipMemcpyDeviceToHost));
+        return RT_OK;
+    });
 }
 
 rt_status rt_canvas_write_accumulation(rt_canvas* k, const float* in) {
-    if (!k || !in) return RT_ERR_INVALID;
-    rt_ctx* c = k->ctx;
-    RT_HIP(c, hipSetDevice(c->device));
-    RT_HIP(c, hipMemcpy(k->accum, in, (size_t)k->width * k->height * 3 * sizeof(float), hipMemcpyHostToDevice));
-    return RT_OK;
+    return canvas_guarded([&]() -> rt_status {
+        if (!k || !in) return RT_ERR_INVALID;
+        rt_ctx* c = k->ctx;
+        RT_HIP(c, hipSetDevice(c->device));
+        RT_HIP(c, hipMemcpy(k->accum, in, (size_t)k->width * k->height * 3 * sizeof(float), hipMemcpyHostToDevice));
+        return RT_OK;
+    });
 }
 
 rt_status rt_canvas_read_accumulation(const rt_canvas* k, float* out) {
-    if (!k || !out) return RT_ERR_INVALID;
-    rt_ctx* c = k->ctx;
-    RT_HIP(c, hipSetDevice(c->device));
-    RT_HIP(c, hipMemcpy(out, k->accum, (size_t)k->width * k->height * 3 * sizeof(float), hipMemcpyDeviceToHost));
-    return RT_OK;
+    return canvas_guarded([&]() -> rt_status {
+        if (!k || !out) return RT_ERR_INVALID;
+        rt_ctx* c = k->ctx;
+        RT_HIP(c, hipSetDevice(c->device));
+        RT_HIP(c, hipMemcpy(out, k->accum, (size_t)k->width * k->height * 3 * sizeof(float), hipMemcpyDeviceToHost));
+        return RT_OK;
+    });
 }
 
 }  // extern "C"

@@ -10,22 +10,23 @@
 //    from 8 sharded queue heads (one per XCD band), one atomic per wave once
 //    L.refill lanes are idle (4 or 8, chosen per launch); each lane folds its
 //    sub-stream's samples in order and stores a partial sum, and combine_kernel
-//    sums a pixel's S partials in a fixed order (the static grid, RTMI_QUEUE=0,
-//    computes the same sums for A/B);
+//    sums a pixel's S partials in a fixed order (the static grid,
+//    rt_render_params.schedule = RT_SCHEDULE_STATIC, computes the same sums);
 //  * path regeneration: a lane whose path terminates starts its next sample in
 //    the same loop trip, so lanes stay busy until their last sample; once the
 //    queue is dry, idle lanes trace other lanes' last samples (tail stealing);
 //  * the main loop is wave-uniform (exits on an empty __ballot of live lanes),
 //    so the whole wave is available for cooperative work inside a trip;
 //  * small meshes (the reference's brute-force TriangleMesh) are tested with
-//    two-phase ballot compaction: the (ray, triangle) pairs of the lanes whose
-//    rays hit the mesh box are packed densely over all 64 lanes, backface-culled,
-//    then fully tested in batches; per-ray results merge with a 64-bit LDS
-//    atomic-min on (t, triangle index);
-//  * large meshes and the pathTrace triangles use the reference's binned-SAH BVH
-//    (BVH.cpp) with per-lane traversal stacks in LDS (32 entries x 64 lanes per
-//    wave, lane i always on bank i) and cooperative traversal: idle lanes steal
-//    pending subtrees, per-ray minima merge by LDS atomic-min;
+//    two-phase ballot compaction over runs of equal meshes: the (ray, triangle)
+//    pairs of the lanes whose rays hit a mesh box are packed densely over all 64
+//    lanes, backface-culled, then fully tested in batches; per-ray results merge
+//    with a 64-bit LDS atomic-min on (t, triangle index);
+//  * large meshes, sphere groups and the pathTrace triangles use the reference's
+//    binned-SAH BVH (BVH.cpp) over child-pair records, with per-lane traversal
+//    stacks in LDS (sized per scene, lane i always on bank i), cooperative
+//    traversal (idle lanes steal pending subtrees) and leaf tests deferred to
+//    wave-wide batches; per-ray minima merge by LDS atomic-min;
 //  * scene records of the closest-hit scan are read at wave-uniform addresses
 //    (scalar loads broadcast to 64 lanes); materials/nodes per lane;
 //  * counter-based RNG (rt_math.h): no init kernel and no RNG state in HBM.
@@ -136,7 +137,7 @@ __device__ __forceinline__ float tri_t(const TriRec& tr, v3 o, v3 d) {
 }
 
 // tri_t for a pair already known to pass the backface cull.
-[[maybe_unused]] __device__ __forceinline__ float tri_t_culled(const TriRec& tr, v3 o, v3 d) {
+__device__ __forceinline__ float tri_t_culled(const TriRec& tr, v3 o, v3 d) {
     const float kNo = __builtin_nanf("");
     v3 e1{tr.e1x, tr.e1y, tr.e1z}, e2{tr.e2x, tr.e2y, tr.e2z};
     v3 s = sub(o, v3{tr.v0x, tr.v0y, tr.v0z});
@@ -215,21 +216,12 @@ struct Hit {
     }
 };
 
-#ifndef RT_MESH_TWO_PHASE
-#define RT_MESH_TWO_PHASE 1  // cull-filtered compaction (mesh_compact); 0 = one pass (A/B only; mesh runs are always two-phase)
-#endif
-
-#ifndef RT_MESH_RUN
-#define RT_MESH_RUN 1  // runs of equal brute-force meshes share one compaction (mesh_run); 0 = per mesh (A/B)
-#endif
 constexpr int kMaxRun = (int)kMeshRunMax;  // meshes per run (rt_scene.cpp marks the runs)
 
 struct WaveLds {
     unsigned long long key[64];  // per-ray (t bits << 32 | triangle) minima
     int32_t src[64];             // rank -> lane of the rays wanting a mesh
-#if RT_MESH_RUN
-    uint32_t slot[kMaxRun * 64];  // mesh_run: ray slot -> lane | triangle base << 6
-#endif
+    uint32_t slot[kMaxRun * 64];  // mesh_run ray slots / the BVH traversals' deferred leaf pairs
     uint32_t grp_s[64], grp_m[64];  // per-lane sphere-group test counts (Counters::grp drained per trip)
     uint16_t ring[128];          // pair ids that passed the backface cull, awaiting the full test
 };
@@ -250,7 +242,7 @@ struct Counters {
     __device__ __forceinline__ void overflow() const { *reinterpret_cast<uint32_t*>(overflow_flag) = 1u; }
 };
 
-// Camera slots of one wave (linear-scan kernels, RT_CAM_SLOTS): each lane's NEXT sample of its
+// Camera slots of one wave (linear-scan kernels): each lane's NEXT sample of its
 // item, prepared ahead - the camera ray and the sample's stream state right after the camera's
 // draws (o.xyz d.x | d.yz time s0 | s1 s2 s3 -). A lane that finishes a sample starts the
 // prepared one from here; the camera pass itself then runs for many lanes at once (render_kernel).
@@ -303,503 +295,18 @@ __device__ __forceinline__ int lane_rank(uint64_t mask) {
                                           __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// Brute-force mesh (TriangleMesh::hit) with ballot compaction. Called by all 64
-// lanes of the wave (uniform control flow); `want` = this lane's ray hit the
-// mesh box. The result equals the reference's sequential scan: the smallest t
-// below the caller's closestSoFar, ties resolved to the lowest triangle index.
-[[maybe_unused]] __device__ __forceinline__ void mesh_compact(const TriRec* __restrict__ tris, uint32_t base,
-                                             uint32_t m, uint32_t mesh_magic, bool want, v3 o, v3 d, Hit& h, int32_t obj,
-                                             uint32_t order, WaveLds& W, int lane) {
-    const uint64_t mask = __ballot(want);
-    if (mask == 0) return;
-    const int rank = lane_rank(mask);
-    if (want) {
-        W.src[rank] = lane;
-        key_reset(W.key[rank]);
-    }
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t total = (uint32_t)__popcll(mask) * m;
-    const float t0 = h.t;
-    // p / m as a multiply-high: magic = ceil(2^32 / m) is exact for p < 2^26 (p < 64 * 64
-    // here); m = 1 (2^32 does not fit) divides by itself
-    const uint32_t magic = mesh_magic;  // ceil(2^32 / m), precomputed at commit (rt_scene.cpp)
-#if RT_MESH_TWO_PHASE
-    // Phase 1 runs only TriangleMesh.cu:72's backface cull over the packed pairs and
-    // queues the survivors (about half of a closed mesh's pairs) in a 128-entry LDS
-    // ring; phase 2 runs the rest of the test on full batches of 64 survivors. The
-    // accepted set, and so the atomic-min result, is that of the one-pass scan.
-    uint32_t queued = 0, tested = 0;  // wave-uniform ring positions
-    auto full_test = [&](uint32_t count) {
-        const uint32_t i = tested + (uint32_t)lane;
-        const bool act = (uint32_t)lane < count;
-        const uint32_t p = act ? (uint32_t)W.ring[i & 127u] : 0u;
-        const uint32_t r = m > 1u ? __umulhi(p, magic) : p;
-        const uint32_t k = p - r * m;
-        const int src = W.src[r];
-        const v3 ro{__shfl(o.x, src, 64), __shfl(o.y, src, 64), __shfl(o.z, src, 64)};
-        const v3 rd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
-        const float rt0 = __shfl(t0, src, 64);
-        if (act) {
-            const float t = tri_t_culled(tris[base + k], ro, rd);
-            if (t <= rt0) {
-                const unsigned long long key =
-                    ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)k;
-                atomicMin(&W.key[r], key);
-            }
-        }
-        tested += count;
-    };
-    for (uint32_t p0 = 0; p0 < total; p0 += 64) {
-        const uint32_t p = p0 + (uint32_t)lane;
-        const bool act = p < total;
-        const uint32_t r = act ? (m > 1u ? __umulhi(p, magic) : p) : 0u;
-        const uint32_t k = act ? p - r * m : 0u;
-        const int src = W.src[r];
-        const v3 rd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
-        bool keep = false;
-        if (act) {
-            const TriRec& tr = tris[base + k];
-            keep = !(dot(rd, v3{tr.nx, tr.ny, tr.nz}) > kFltEpsilon);
-        }
-        const uint64_t km = __ballot(keep);
-        if (keep) W.ring[(queued + (uint32_t)lane_rank(km)) & 127u] = (uint16_t)p;
-        queued += (uint32_t)__popcll(km);
-        __builtin_amdgcn_wave_barrier();
-        if (queued - tested >= 64u) full_test(64u);
-    }
-    if (queued > tested) full_test(queued - tested);
-#else
-    for (uint32_t p0 = 0; p0 < total; p0 += 64) {
-        const uint32_t p = p0 + (uint32_t)lane;
-        const bool act = p < total;
-        const uint32_t r = act ? (m > 1u ? __umulhi(p, magic) : p) : 0u;
-        const uint32_t k = act ? p - r * m : 0u;
-        const int src = W.src[r];
-        const v3 ro{__shfl(o.x, src, 64), __shfl(o.y, src, 64), __shfl(o.z, src, 64)};
-        const v3 rd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
-        const float rt0 = __shfl(t0, src, 64);
-        if (act) {
-            const float t = tri_t(tris[base + k], ro, rd);
-            if (t <= rt0) {
-                const unsigned long long key =
-                    ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)k;
-                atomicMin(&W.key[r], key);
-            }
-        }
-    }
-#endif
-    __builtin_amdgcn_wave_barrier();
-    if (want) {
-        const unsigned long long key = W.key[rank];
-        if (key != ~0ull)
-            h.merge(__uint_as_float((uint32_t)(key >> 32)), order, false, obj,
-                    (int32_t)(base + (uint32_t)(key & 0xFFFFFFFFu)));
-    }
-    __builtin_amdgcn_wave_barrier();
-}
-
-// BVH mesh: per-lane traversal of the reference's SAH tree (DFS node order,
-// leaves own contiguous ranges of `tris`, `tri_orig` holds the mesh-local
-// triangle index for the lowest-index tie rule of the sequential scan).
-// Ordered traversal: both children are tested at their parent, the nearer one
-// is descended first (kept in registers), the farther one waits on the LDS
-// stack and is re-tested against the best t when popped. The candidate set and
-// the (t, original index) merge make the result independent of the order.
-[[maybe_unused]] __device__ __forceinline__ void mesh_bvh(const TriRec* __restrict__ tris,
-                                         const uint32_t* __restrict__ tri_orig,
-                                         const BvhNode* __restrict__ nodes, uint32_t root, bool want,
-                                         v3 o, v3 d, v3 inv, Hit& h, int32_t obj, uint32_t order,
-                                         uint32_t* stack, Counters& cnt, int cap) {
-    if (!want) return;
-    const float t0 = h.t;
-    float best = t0;
-    uint32_t best_orig = 0xFFFFFFFFu, best_k = 0;
-    BvhNode cur = nodes[root];
-    ++cnt.node_visits;
-    bool has = true;
-    int sp = 0;
-    for (;;) {
-        if (!has) {
-            if (sp == 0) break;
-            cur = nodes[stack[(--sp) * 64]];
-            ++cnt.node_visits;
-            float tn;
-            if (!node_hit(cur, o, inv, best, tn)) continue;  // best improved since the push
-            has = true;
-        }
-        if (cur.b & 0x80000000u) {
-            const uint32_t nt = cur.b & 0x7FFFFFFFu;
-            cnt.tri_tests += nt;
-            for (uint32_t k = cur.a; k < cur.a + nt; ++k) {
-                const float t = tri_t(tris[k], o, d);
-                if (t <= t0) {
-                    const uint32_t orig = tri_orig[2 * k];
-                    if (t < best || (t == best && orig < best_orig)) {
-                        best = t;
-                        best_orig = orig;
-                        best_k = k;
-                    }
-                }
-            }
-            has = false;
-            continue;
-        }
-        const uint32_t il = cur.a, ir = cur.b;
-        const BvhNode nl = nodes[il], nr = nodes[ir];
-        cnt.node_visits += 2;
-        float tl, tr;
-        const bool hl = node_hit(nl, o, inv, best, tl);
-        const bool hr = node_hit(nr, o, inv, best, tr);
-        if (hl && hr) {
-            if (sp + 1 > cap) {
-                cnt.overflow();
-                break;
-            }
-            const bool left_first = tl <= tr;
-            stack[(sp++) * 64] = left_first ? ir : il;
-            cur = left_first ? nl : nr;
-        } else if (hl) {
-            cur = nl;
-        } else if (hr) {
-            cur = nr;
-        } else {
-            has = false;
-        }
-    }
-    if (best_orig != 0xFFFFFFFFu) h.merge(best, order, false, obj, (int32_t)best_k);
-}
-
-#ifndef RT_BVH_STEAL
-#define RT_BVH_STEAL 1  // cooperative (work-stealing) mesh traversal; 0 = per-lane mesh_bvh (A/B)
-#endif
-
-#ifndef RT_LEAF_BATCH
-#define RT_LEAF_BATCH 1  // BVH leaves' triangle tests deferred to wave-wide batches (0: per-lane leaf loops, A/B)
-#endif
-
-#if !(RT_LEAF_BATCH && RT_MESH_RUN)
-// Cooperative BVH mesh traversal (called by all 64 lanes). Per-lane traversal
-// leaves most of a wave idle while its deepest rays finish (VALU lane use was
-// 18% on the bunny). Here a lane whose work ran out takes the bottom (oldest,
-// shallowest) pending subtree of a lane that still has one, together with that
-// ray (origin, direction, inverse, closestSoFar) and its current best distance
-// as the pruning bound. Each lane's stack is a deque in the LDS: owners push and
-// pop at the top, thieves take from the bottom, all in the wave's one
-// instruction stream. A lane reports the best (t, mesh-local index) it found
-// for a ray with a 64-bit LDS atomic-min on that ray's slot before it switches
-// rays. Every subtree is still traversed exactly once, against a bound no
-// tighter than the one the owner would have used, so the candidate set and the
-// (t, lowest index) winner are those of the sequential scan.
-__device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
-                                              const uint32_t* __restrict__ tri_orig,
-                                              const BvhNode* __restrict__ nodes, uint32_t root, uint32_t base,
-                                              bool want, v3 o, v3 d, v3 inv, Hit& h, int32_t obj,
-                                              uint32_t order, uint32_t* wstack, WaveLds& W, int lane,
-                                              Counters& cnt, int cap) {
-    const uint64_t wm = __ballot(want);
-    if (wm == 0) return;
-    key_reset(W.key[lane]);
-    int owner = lane;
-    v3 ro = o, rd = d, ri = inv;
-    float t0 = h.t;    // the ray's closestSoFar: accept t <= t0
-    float best = t0;   // this lane's pruning bound for the ray
-    uint32_t best_orig = 0xFFFFFFFFu;
-    BvhNode cur = nodes[root];
-    bool has = want;
-    if (want) ++cnt.node_visits;
-    int sp = 0, bot = 0;  // pending subtrees: wstack[k * 64 + lane], bot <= k < sp
-    auto flush = [&]() {
-        if (best_orig != 0xFFFFFFFFu)
-            atomicMin(&W.key[owner], ((unsigned long long)__float_as_uint(best) << 32) | best_orig);
-        best_orig = 0xFFFFFFFFu;
-    };
-    __builtin_amdgcn_wave_barrier();
-    for (;;) {
-        if (__ballot(has || sp > bot) == 0) break;
-        // steal: pair the r-th idle lane with the r-th lane that has a spare subtree
-        const bool idle = !has && sp == bot;
-        const bool spare = sp - bot >= (has ? 1 : 2);
-        const uint64_t im = __ballot(idle), vm = __ballot(spare);
-        if (im != 0 && vm != 0) {
-            const int nv = __popcll(vm), ni = __popcll(im);
-            if (spare) W.src[lane_rank(vm)] = lane;
-            __builtin_amdgcn_wave_barrier();
-            int vic = lane;
-            const bool thief = idle && lane_rank(im) < nv;
-            if (thief) vic = W.src[lane_rank(im)];
-            const int vt = __shfl(bot, vic, 64);  // the victim's oldest pending subtree (newest: same speed)
-            if (thief) flush();  // publish this lane's result for its old ray first
-            // take over the victim's ray one register at a time (few temporaries live at once)
-            auto take = [&](float& x) {
-                const float v = __shfl(x, vic, 64);
-                if (thief) x = v;
-            };
-            {
-                const int v_owner = __shfl(owner, vic, 64);
-                if (thief) owner = v_owner;
-            }
-            take(ro.x); take(ro.y); take(ro.z);
-            take(rd.x); take(rd.y); take(rd.z);
-            take(ri.x); take(ri.y); take(ri.z);
-            take(t0);
-            take(best);
-            if (thief) {
-                const uint32_t entry = wstack[vt * 64 + vic];
-                best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
-                sp = bot = 0;
-                cur = nodes[entry];
-                ++cnt.node_visits;
-                float tn;
-                has = node_hit(cur, ro, ri, best, tn);
-            }
-            if (spare && lane_rank(vm) < ni) ++bot;  // robbed
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (!has) {
-            if (sp > bot) {
-                cur = nodes[wstack[(--sp) * 64 + lane]];
-                ++cnt.node_visits;
-                // the ray's best so far over all lanes (NaN while none: fminf keeps ours)
-                best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
-                float tn;
-                has = node_hit(cur, ro, ri, best, tn);  // best improved since the push?
-            }
-            if (sp == bot) sp = bot = 0;
-            if (!has) continue;
-        }
-        if (cur.b & 0x80000000u) {
-            const uint32_t nt = cur.b & 0x7FFFFFFFu;
-            cnt.tri_tests += nt;
-            for (uint32_t k = cur.a; k < cur.a + nt; ++k) {
-                const float t = tri_t(tris[k], ro, rd);
-                if (t <= t0) {
-                    const uint32_t orig = tri_orig[2 * k];
-                    if (t < best || (t == best && orig < best_orig)) {
-                        best = t;
-                        best_orig = orig;
-                    }
-                }
-            }
-            // publish at once: the ray's owner and the other lanes working on it prune with it
-            flush();
-            has = false;
-            continue;
-        }
-        const uint32_t il = cur.a, ir = cur.b;
-        const BvhNode nl = nodes[il], nr = nodes[ir];
-        cnt.node_visits += 2;
-        float tl, tr;
-        const bool hl = node_hit(nl, ro, ri, best, tl);
-        const bool hr = node_hit(nr, ro, ri, best, tr);
-        if (hl && hr) {
-            if (sp + 1 > cap) {
-                cnt.overflow();
-                has = false;
-                sp = bot = 0;
-                continue;
-            }
-            const bool left_first = tl <= tr;
-            wstack[(sp++) * 64 + lane] = left_first ? ir : il;
-            cur = left_first ? nl : nr;
-        } else if (hl) {
-            cur = nl;
-        } else if (hr) {
-            cur = nr;
-        } else {
-            has = false;
-        }
-    }
-    flush();
-    __builtin_amdgcn_wave_barrier();
-    if (want) {
-        const unsigned long long key = W.key[lane];
-        if (key != ~0ull) {
-            const uint32_t k = tri_orig[2 * (base + (uint32_t)(key & 0xFFFFFFFFu)) + 1];
-            h.merge(__uint_as_float((uint32_t)(key >> 32)), order, false, obj, (int32_t)k);
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-}
-
-#endif
-
-#if RT_LEAF_BATCH && RT_MESH_RUN
-// mesh_bvh_coop with deferred leaf tests. A lane that reaches a leaf does not test its
-// triangles itself: it appends (triangle, ray owner) pairs to a per-wave LDS queue (up to
-// three per loop trip: a larger leaf keeps its lane for more trips) and walks on. Whenever
-// 64 pairs are queued the whole wave tests them at once - one pair per lane, the three
-// triangle loads of all 64 pairs in flight together - and merges each accepted hit into its
-// ray's LDS minimum of (t, mesh-local index), the same atomic-min the per-lane loops
-// published. Lanes then re-read their ray's minimum as the pruning bound. The per-lane leaf
-// loops were divergent (a wave's inner-node lanes waited for its leaf lanes) and serialised
-// one load latency per triangle; the candidate set is unchanged (a subtree is pruned only
-// against a bound some accepted triangle reached), so the winner is the sequential scan's.
-// Ray data for a pair comes from its owner lane's registers (o, d, h.t are not modified
-// while the wave traverses), so a lane carries only the current ray's origin and inverse.
-[[maybe_unused]] __device__ __forceinline__ void mesh_bvh_coop(const TriRec* __restrict__ tris,
-                                              const uint32_t* __restrict__ tri_orig,
-                                              const BvhNode* __restrict__ nodes, uint32_t root, uint32_t base,
-                                              bool want, v3 o, v3 d, v3 inv, Hit& h, int32_t obj,
-                                              uint32_t order, uint32_t* wstack, WaveLds& W, int lane,
-                                              Counters& cnt, int cap) {
-    const uint64_t wm = __ballot(want);
-    if (wm == 0) return;
-    key_reset(W.key[lane]);
-    int owner = lane;
-    v3 ro = o, ri = inv;
-    float best = h.t;  // pruning bound for the current ray (its closestSoFar until a hit lands)
-    BvhNode cur = nodes[root];
-    bool has = want;
-    if (want) ++cnt.node_visits;
-    int sp = 0, bot = 0;         // pending subtrees: wstack[k * 64 + lane], bot <= k < sp
-    uint32_t qtail = 0, qdone = 0;  // wave-uniform positions in the pair queue W.slot (256 entries)
-    constexpr uint32_t kQ = (uint32_t)kMaxRun * 64u;
-    static_assert(kQ >= 256, "the pair queue holds 63 + 3 x 64 pairs");
-    __builtin_amdgcn_wave_barrier();
-    // test `count` (<= 64) queued pairs, one per lane (wave-uniform)
-    auto batch = [&](uint32_t count) {
-        const bool act = (uint32_t)lane < count;
-        const uint32_t e = act ? W.slot[(qdone + (uint32_t)lane) & (kQ - 1)] : 0u;
-        const uint32_t k = e >> 6;
-        const int own = (int)(e & 63u);
-        const v3 po{__shfl(o.x, own, 64), __shfl(o.y, own, 64), __shfl(o.z, own, 64)};
-        const v3 pd{__shfl(d.x, own, 64), __shfl(d.y, own, 64), __shfl(d.z, own, 64)};
-        const float pt0 = __shfl(h.t, own, 64);
-        if (act) {
-            const float t = tri_t(tris[k], po, pd);
-            if (t <= pt0)
-                atomicMin(&W.key[own], ((unsigned long long)__float_as_uint(t) << 32) | tri_orig[2 * k]);
-        }
-        qdone += count;
-        __builtin_amdgcn_wave_barrier();
-    };
-    for (;;) {
-        if (__ballot(has || sp > bot) == 0) break;
-        // steal: pair the r-th idle lane with the r-th lane that has a spare subtree
-        const bool idle = !has && sp == bot;
-        const bool spare = sp - bot >= (has ? 1 : 2);
-        const uint64_t im = __ballot(idle), vm = __ballot(spare);
-        if (im != 0 && vm != 0) {
-            const int nv = __popcll(vm), ni = __popcll(im);
-            if (spare) W.src[lane_rank(vm)] = lane;
-            __builtin_amdgcn_wave_barrier();
-            int vic = lane;
-            const bool thief = idle && lane_rank(im) < nv;
-            if (thief) vic = W.src[lane_rank(im)];
-            const int vt = __shfl(bot, vic, 64);  // the victim's oldest pending subtree
-            auto take = [&](float& x) {
-                const float v = __shfl(x, vic, 64);
-                if (thief) x = v;
-            };
-            {
-                const int v_owner = __shfl(owner, vic, 64);
-                if (thief) owner = v_owner;
-            }
-            take(ro.x); take(ro.y); take(ro.z);
-            take(ri.x); take(ri.y); take(ri.z);
-            take(best);
-            if (thief) {
-                const uint32_t entry = wstack[vt * 64 + vic];
-                best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
-                sp = bot = 0;
-                cur = nodes[entry];
-                ++cnt.node_visits;
-                float tn;
-                has = node_hit(cur, ro, ri, best, tn);
-            }
-            if (spare && lane_rank(vm) < ni) ++bot;  // robbed
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (!has && sp > bot) {
-            cur = nodes[wstack[(--sp) * 64 + lane]];
-            ++cnt.node_visits;
-            // the ray's best so far over all lanes (NaN while none: fminf keeps ours)
-            best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
-            float tn;
-            has = node_hit(cur, ro, ri, best, tn);  // best improved since the push?
-        }
-        if (!has && sp == bot) sp = bot = 0;
-        uint32_t lk = 0, ln = 0;  // this trip's leaf pairs: triangles lk .. lk + ln - 1
-        if (has) {
-            if (cur.b & 0x80000000u) {
-                const uint32_t nt = cur.b & 0x7FFFFFFFu;
-                ln = nt < 3u ? nt : 3u;
-                lk = cur.a;
-                if (nt > 3u) {  // a larger leaf keeps this lane for more trips
-                    cur.a += 3u;
-                    cur.b -= 3u;
-                } else {
-                    has = false;
-                }
-                cnt.tri_tests += ln;
-            } else {
-                const uint32_t il = cur.a, ir = cur.b;
-                const BvhNode nl = nodes[il], nr = nodes[ir];
-                cnt.node_visits += 2;
-                float tl, tr;
-                const bool hl = node_hit(nl, ro, ri, best, tl);
-                const bool hr = node_hit(nr, ro, ri, best, tr);
-                if (hl && hr) {
-                    if (sp + 1 > cap) {
-                        cnt.overflow();
-                        has = false;
-                        sp = bot = 0;
-                    } else {
-                        const bool left_first = tl <= tr;
-                        wstack[(sp++) * 64 + lane] = left_first ? ir : il;
-                        cur = left_first ? nl : nr;
-                    }
-                } else if (hl) {
-                    cur = nl;
-                } else if (hr) {
-                    cur = nr;
-                } else {
-                    has = false;
-                }
-            }
-        }
-        // enqueue the leaf pairs (converged): a lane's slots follow those of the lanes below it
-        const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
-        if (b1) {
-            const uint32_t at = qtail + (uint32_t)(lane_rank(b1) + lane_rank(b2) + lane_rank(b3));
-            const uint32_t tag = (uint32_t)owner;
-            for (uint32_t j = 0; j < ln; ++j) W.slot[(at + j) & (kQ - 1)] = ((lk + j) << 6) | tag;
-            qtail += (uint32_t)(__popcll(b1) + __popcll(b2) + __popcll(b3));
-            __builtin_amdgcn_wave_barrier();
-            if (qtail - qdone >= 64u) {
-                do {
-                    batch(64u);
-                } while (qtail - qdone >= 64u);
-                if (has || sp > bot) best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
-            }
-        }
-    }
-    if (qtail > qdone) batch(qtail - qdone);
-    __builtin_amdgcn_wave_barrier();
-    if (want) {
-        const unsigned long long key = W.key[lane];
-        if (key != ~0ull) {
-            const uint32_t k = tri_orig[2 * (base + (uint32_t)(key & 0xFFFFFFFFu)) + 1];
-            h.merge(__uint_as_float((uint32_t)(key >> 32)), order, false, obj, (int32_t)k);
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-}
-#endif
-
-#ifndef RT_BVH_PAIRS
-#define RT_BVH_PAIRS 1  // mesh BVHs traversed over child-pair records (0: node records, A/B)
-#endif
-#if RT_BVH_PAIRS && RT_LEAF_BATCH && RT_MESH_RUN
 // The batched mesh traversal over child-pair records (rt_scene.cpp build_mesh_pairs). A lane
 // holds one reference word instead of a node: a pair index, whose 64 B record carries both
 // children's boxes and references, or a leaf reference (first triangle, count). An inner
 // step is one aligned 64 B load and two box tests; the nearer hit child becomes the lane's
 // reference and the farther one is pushed as a word. Popping, stealing and reaching a leaf
 // load nothing: a leaf's triangles are queued for the wave's batched tests (up to three per
-// trip, as in the node-record traversal) in the same trip that reached it. The node-record
-// version re-loaded and re-tested every popped node before loading its children - two
-// dependent loads per pop. A popped entry is not re-tested against the improved bound
+// trip; a larger leaf keeps its lane for more trips) in the same trip that reached it, and
+// whenever 64 pairs are queued the whole wave tests them at once - one pair per lane, the
+// triangle loads of all 64 in flight together - merging each accepted hit into its ray's LDS
+// minimum of (t, mesh-local index); lanes then re-read their ray's minimum as the pruning
+// bound. (Superseded in round 3 and removed in round 4: per-lane traversal, node records
+// re-tested at every pop, per-lane leaf loops) A popped entry is not re-tested against the improved bound
 // (its children are, on their pair load); pruning stays conservative, so the candidate set
 // still contains the sequential scan's winner and the (t, index) minimum picks it.
 __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
@@ -941,7 +448,6 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
     }
     __builtin_amdgcn_wave_barrier();
 }
-#endif
 
 // One object record (64 B) as a single wave-uniform scalar load; the same
 // helper serves per-lane loads of sphere-group members.
@@ -968,13 +474,12 @@ __device__ __forceinline__ ObjRec load_obj(const ObjRec* __restrict__ objs, int 
     return r;
 }
 
-#if RT_MESH_RUN
 // A run of g consecutive brute-force meshes with the same triangle count m (instances
 // of one model; rt_scene.cpp stores g in the first record's f[7], 0 in the others)
 // compacted together: the rays wanting each mesh (box early-out, TriangleMesh.cu:34-38)
 // are listed one after the other as ray slots (lane, the mesh's triangle base), and the
-// slot x triangle pairs of the whole run are packed over the 64 lanes as in
-// mesh_compact. One partial batch per run instead of one per mesh. Triangles of
+// slot x triangle pairs of the whole run are packed densely over the 64 lanes,
+// backface-culled, then fully tested in batches of 64. One partial batch per run instead of one per mesh. Triangles of
 // consecutive meshes are consecutive in `tris` (their bases rise with scan order), so
 // the per-lane minimum of (t, global triangle index) over the run is the candidate the
 // sequential hit() keeps: smallest t, then the earliest mesh, then its lowest triangle.
@@ -1000,7 +505,7 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
     __builtin_amdgcn_wave_barrier();
     const uint32_t total = nslot * m;
     const float t0 = h.t;
-    uint32_t queued = 0, tested = 0;  // wave-uniform ring positions (two phases as in mesh_compact)
+    uint32_t queued = 0, tested = 0;  // wave-uniform ring positions (phase 1: cull, phase 2: full test)
     auto full_test = [&](uint32_t count) {
         const uint32_t i = tested + (uint32_t)lane;
         const bool act = (uint32_t)lane < count;
@@ -1050,7 +555,6 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
     }
     __builtin_amdgcn_wave_barrier();
 }
-#endif
 
 // Candidate root of a (moving) sphere independent of closestSoFar: the near
 // root if >= tMin, else the far root (Sphere.cu:20-31 with tMax = +inf; the
@@ -1064,69 +568,9 @@ __device__ __forceinline__ float sphere_candidate(const ObjRec& ob, v3 o, v3 d, 
     return sphere_root(o, d, c, r, kTMin, kInf, t) ? t : __builtin_nanf("");
 }
 
-// Sphere group: per-lane traversal of the object BVH over the scene's spheres
-// (members are ObjRecs stored after the scan list, in leaf order).
-[[maybe_unused]] __device__ __forceinline__ void sphere_group(const ObjRec* __restrict__ objs,
-                                             const BvhNode* __restrict__ nodes, uint32_t root,
-                                             bool live, const Ray& ray, v3 inv, Hit& h,
-                                             uint32_t* stack, Counters& cnt, int cap) {
-    if (!live) return;
-    const v3 o = ray.o, d = ray.d;
-    BvhNode cur = nodes[root];
-    ++cnt.node_visits;
-    bool has = true;
-    int sp = 0;
-    for (;;) {  // ordered as mesh_bvh
-        if (!has) {
-            if (sp == 0) break;
-            cur = nodes[stack[(--sp) * 64]];
-            ++cnt.node_visits;
-            float tn;
-            if (!node_hit(cur, o, inv, h.t, tn)) continue;
-            has = true;
-        }
-        if (cur.b & 0x80000000u) {
-            const uint32_t n = cur.b & 0x7FFFFFFFu;
-            for (uint32_t k = cur.a; k < cur.a + n; ++k) {
-                const ObjRec ob = load_obj(objs, (int)k);
-                cnt.grp += ob.type == kObjMovingSphere ? 0x10000u : 1u;
-                h.merge(sphere_candidate(ob, o, d, ray.time), ob.order, true, (int32_t)k, -1);
-            }
-            has = false;
-            continue;
-        }
-        const uint32_t il = cur.a, ir = cur.b;
-        const BvhNode nl = nodes[il], nr = nodes[ir];
-        cnt.node_visits += 2;
-        float tl, tr;
-        const bool hl = node_hit(nl, o, inv, h.t, tl);
-        const bool hr = node_hit(nr, o, inv, h.t, tr);
-        if (hl && hr) {
-            if (sp + 1 > cap) {
-                cnt.overflow();
-                break;
-            }
-            const bool left_first = tl <= tr;
-            stack[(sp++) * 64] = left_first ? ir : il;
-            cur = left_first ? nl : nr;
-        } else if (hl) {
-            cur = nl;
-        } else if (hr) {
-            cur = nr;
-        } else {
-            has = false;
-        }
-    }
-}
-
-#ifndef RT_SG_BATCH
-#define RT_SG_BATCH 1  // sphere groups' leaf tests deferred to wave-wide batches (0: per-lane loops, A/B)
-#endif
-#ifndef RT_SG_PAIRS
-#define RT_SG_PAIRS 1  // ... over child-pair records (as mesh_bvh_pairs; 0: node records, A/B)
-#endif
-#if RT_SG_BATCH && RT_MESH_RUN
-// sphere_group with deferred leaf tests (as mesh_bvh_coop, without stealing): the traversal
+// Sphere group: the object BVH over the scene's spheres (members are ObjRecs stored after the
+// scan list, in leaf order), over child-pair records with deferred leaf tests (as
+// mesh_bvh_pairs, without stealing): the traversal
 // loop is wave-uniform, and lanes at a leaf queue (member, ray owner) pairs that the wave tests
 // 64 at a time. Every group member is a sphere, and among spheres at the same t the sequential
 // hit() keeps the one of highest scan order (the inclusive test, Sphere.cu:25), which also
@@ -1142,12 +586,7 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
     key_reset(W.key[lane]);
     const v3 o = ray.o;
     float best = h.t;  // pruning bound: the ray's closestSoFar, then its best member so far
-#if RT_SG_PAIRS
     uint32_t cur = root;  // pair index or leaf reference (root: the group's root pair)
-#else
-    BvhNode cur = nodes[root];
-    if (live) ++cnt.node_visits;
-#endif
     bool has = live;
     int sp = 0;
     uint32_t qtail = 0, qdone = 0;
@@ -1178,7 +617,6 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
     };
     for (;;) {
         if (__ballot(has || sp > 0) == 0) break;
-#if RT_SG_PAIRS
         if (!has && sp > 0) {
             cur = wstack[(--sp) * 64 + lane];
             has = true;
@@ -1217,52 +655,6 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
             else
                 has = false;
         }
-#else
-        if (!has && sp > 0) {
-            cur = nodes[wstack[(--sp) * 64 + lane]];
-            ++cnt.node_visits;
-            float tn;
-            has = node_hit(cur, o, inv, best, tn);  // best improved since the push?
-        }
-        uint32_t lk = 0, ln = 0;
-        if (has) {
-            if (cur.b & 0x80000000u) {
-                const uint32_t nt = cur.b & 0x7FFFFFFFu;
-                ln = nt < 3u ? nt : 3u;
-                lk = cur.a;
-                if (nt > 3u) {
-                    cur.a += 3u;
-                    cur.b -= 3u;
-                } else {
-                    has = false;
-                }
-            } else {
-                const uint32_t il = cur.a, ir = cur.b;
-                const BvhNode nl = nodes[il], nr = nodes[ir];
-                cnt.node_visits += 2;
-                float tl, tr;
-                const bool hl = node_hit(nl, o, inv, best, tl);
-                const bool hr = node_hit(nr, o, inv, best, tr);
-                if (hl && hr) {
-                    if (sp + 1 > cap) {
-                        cnt.overflow();
-                        has = false;
-                        sp = 0;
-                    } else {
-                        const bool left_first = tl <= tr;
-                        wstack[(sp++) * 64 + lane] = left_first ? ir : il;
-                        cur = left_first ? nl : nr;
-                    }
-                } else if (hl) {
-                    cur = nl;
-                } else if (hr) {
-                    cur = nr;
-                } else {
-                    has = false;
-                }
-            }
-        }
-#endif
         const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
         if (b1) {
             const uint32_t at = qtail + (uint32_t)(lane_rank(b1) + lane_rank(b2) + lane_rank(b3));
@@ -1288,7 +680,6 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
     }
     __builtin_amdgcn_wave_barrier();
 }
-#endif
 
 // Constant medium bounded by a cube (rt_constant_medium, rtmi.h; "Ray Tracing:
 // The Next Week" ConstantMedium::hit with the boundary = the six two-sided faces
@@ -1365,21 +756,6 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
 // wave active; `live` masks lanes without a path. Records are fetched one
 // object ahead (scalar loads overlap the current object's VALU work), and the
 // per-object tests are branch-free candidates merged with Hit's tie rule.
-#ifndef RT_ORDERED_MERGE
-#define RT_ORDERED_MERGE 1  // linear-scan kernels merge candidates with Hit::merge_seq<true> (0: A/B)
-#endif
-#ifndef RT_MED_MERGE1
-#define RT_MED_MERGE1 1  // the media variant merges once per object (0: per branch, A/B)
-#endif
-#ifndef RT_BVH_PARTS_VARIANT
-#define RT_BVH_PARTS_VARIANT 1  // BVH scenes with only mesh BVHs / only sphere groups take the kParts 1 / 2 kernels
-#endif
-#ifndef RT_NOSPH_VARIANT
-#define RT_NOSPH_VARIANT 1  // sphere-free scenes without BVHs or media take render_kernel<false, *, false, false>
-#endif
-#ifndef RT_MED_VARIANT
-#define RT_MED_VARIANT 1  // media scenes without BVHs take render_kernel<false, *, true> (0: A/B)
-#endif
 // kMed: the scan-kernel variant for scenes with participating media (rt_capi.cpp picks it):
 // no record prefetch (the medium test is long and the next record's 16 SGPRs stay live
 // across it) and one merge per object (the type branches yield a candidate instead of
@@ -1397,12 +773,9 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
     Hit h{kInf, -1, -1, 0xFFFFFFFFu, -1, 0u};
     const v3 o = ray.o, d = ray.d;
     const int n = S.n_objs;
-#ifndef RT_OBJ_PREFETCH
-#define RT_OBJ_PREFETCH 1
-#endif
-    constexpr bool kPf = RT_OBJ_PREFETCH && !kMed;
+    constexpr bool kPf = !kMed;
     // no sphere groups: merges come in scan order (the media variant measured slower with it)
-    constexpr bool kOrd = RT_ORDERED_MERGE && !kBvh && !kMed;
+    constexpr bool kOrd = !kBvh && !kMed;
     ObjRec cur = load_obj(S.objs, 0);
     for (int i = 0; i < n; ++i) {
         const ObjRec ob = kPf ? cur : load_obj(S.objs, i);
@@ -1411,7 +784,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
         float tc = __builtin_nanf("");  // kMed: this object's candidate, merged once below
         bool tsph = false;
         auto cand = [&](float t, bool sphere) {
-            if constexpr (kMed && RT_MED_MERGE1) {
+            if constexpr (kMed) {
                 tc = t;
                 tsph = sphere;
             } else {
@@ -1446,57 +819,29 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             // TriangleMesh::hit (TriangleMesh.cu:34-117): the AABB early-out
             // gates the triangle scan exactly as in the reference.
             const uint32_t root = ob.u2;  // wave-uniform (scalar record)
-#if RT_MESH_RUN
             if (!kBvh || root == kNoBvh) {
                 const uint32_t g = __float_as_uint(ob.f[7]);  // run length (0: inside a run)
                 RT_STAMP(t_m0);
                 if (g != 0u)
                     mesh_run<kOrd>(S.objs, S.tris, i, g, ob.u1, __float_as_uint(ob.f[6]), live, o, d, inv, h, cnt, W,
-                             lane);
+                                   lane);
                 RT_STAMP(t_m1);
                 RT_ACC(3, t_m0, t_m1);
-            } else {
-                if constexpr ((kParts & 1) != 0) {
+            } else if constexpr ((kParts & 1) != 0) {
                 const bool want = live && box_hit(f, o, inv);
                 cnt.box_tests += (uint32_t)__popcll(__ballot(live));
-#else
-            const bool want = live && box_hit(f, o, inv);
-            cnt.box_tests += (uint32_t)__popcll(__ballot(live));
-            if (root == kNoBvh) cnt.tri_wave += (uint32_t)__popcll(__ballot(want)) * ob.u1;
-            if (!kBvh || root == kNoBvh) {
-                RT_STAMP(t_m0);
-                mesh_compact(S.tris, ob.u0, ob.u1, __float_as_uint(ob.f[6]), want, o, d, h, i, ob.order, W, lane);
-                RT_STAMP(t_m1);
-                RT_ACC(3, t_m0, t_m1);
-            } else {
-#endif
-#if RT_BVH_STEAL && RT_BVH_PAIRS && RT_LEAF_BATCH && RT_MESH_RUN
                 mesh_bvh_pairs(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0, want, o, d, inv, h, i,
                                ob.order, stack - lane, W, lane, cnt, S.stack_cap);
-#elif RT_BVH_STEAL
-                mesh_bvh_coop(S.tris, S.tri_orig, S.nodes, root, ob.u0, want, o, d, inv, h, i, ob.order,
-                              stack - lane, W, lane, cnt, S.stack_cap);
-#else
-                mesh_bvh(S.tris, S.tri_orig, S.nodes, root, want, o, d, inv, h, i, ob.order, stack, cnt,
-                         S.stack_cap);
-#endif
-#if RT_MESH_RUN
-                }
-#endif
             }
-        } else if ((kMed || (kBvh && kSph) || !RT_MED_VARIANT) && ob.type == kObjMedium) {
+        } else if ((kMed || (kBvh && kSph)) && ob.type == kObjMedium) {
             // (the general linear-scan kernel never sees a medium: launch_render sends scenes with
             // media to the kMed variant, so its register allocation need not cover this test)
             cand(live ? medium_candidate(ob, o, d, rng) : __builtin_nanf(""), false);
         } else if (kBvh && (kParts & 2) != 0) {  // kObjSphereGroup
-#if RT_SG_BATCH && RT_MESH_RUN
-            sphere_group_batched(S.objs, S.nodes, RT_SG_PAIRS ? __float_as_uint(ob.f[8]) : ob.u2, live, ray, inv, h,
-                                 stack - lane, W, lane, cnt, S.stack_cap);
-#else
-            sphere_group(S.objs, S.nodes, ob.u2, live, ray, inv, h, stack, cnt, S.stack_cap);
-#endif
+            sphere_group_batched(S.objs, S.nodes, __float_as_uint(ob.f[8]), live, ray, inv, h, stack - lane, W, lane,
+                                 cnt, S.stack_cap);
         }
-        if constexpr (kMed && RT_MED_MERGE1) h.merge_seq<kOrd>(tc, ob.order, tsph, i, -1);  // NaN: no candidate
+        if constexpr (kMed) h.merge_seq<kOrd>(tc, ob.order, tsph, i, -1);  // NaN: no candidate
     }
     h.finish();
     return h;
@@ -1720,12 +1065,6 @@ __global__ __launch_bounds__(256) void combine_kernel(RenderLaunch L, float* __r
     write_pixel(L, out, ((size_t)lrow * (size_t)L.cols + (size_t)(px - L.col0)) * 3, acc, (float)L.spp);
 }
 
-#ifndef RT_TAIL_STEAL
-#define RT_TAIL_STEAL 1  // lanes idle at the end of the queue take other lanes' last samples
-#endif
-#ifndef RT_CAM_SLOTS
-#define RT_CAM_SLOTS 1  // linear-scan kernels prepare each lane's next camera sample in LDS (0: A/B)
-#endif
 #ifndef RT_CAM_BATCH
 #define RT_CAM_BATCH 32  // lanes lacking a prepared next sample that start a camera pass on their own
 #endif
@@ -1770,7 +1109,7 @@ __device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, i
 // and holds its radiance; the owner, once its own samples are done, folds the
 // held values in sample order and writes the partial sum. The partial sums are
 // therefore bit-identical; only the tail of the launch gets shorter.
-[[maybe_unused]] __device__ __forceinline__ void tail_steal(const RenderLaunch& L, WaveLds& W, int lane, int SP, bool& alive,
+__device__ __forceinline__ void tail_steal(const RenderLaunch& L, WaveLds& W, int lane, int SP, bool& alive,
                                            bool& waiting, bool& held, int& towner, uint32_t& tl_pack,
                                            int& own_end, int& s, uint32_t& item, v3& sum, v3& thr,
                                            bool& need_cam) {
@@ -1833,9 +1172,6 @@ __device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, i
     __builtin_amdgcn_wave_barrier();
 }
 
-#ifndef RT_LK
-#define RT_LK 1  // the render loops read their launch parameters from the kernarg segment at their use
-#endif
 // The megakernels' launch parameters (their FIRST argument: kernarg offset 0) behind an
 // opaque pointer. Each loop trip re-reads the fields it uses with scalar loads at their
 // use, instead of the compiler holding ~40 of them in SGPRs across the persistent loop
@@ -1865,7 +1201,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
     const SceneArgs S{objs, tris, mats, nodes, tri_orig, n_objs, 0, kBvh, L.stack_depth};
     __shared__ WaveLds lds[kWavesPerBlock];
     // camera slots: the linear-scan kernels only (the traversal kernels' LDS holds their stacks)
-    constexpr bool kCamPf = RT_CAM_SLOTS && !kBvh;
+    constexpr bool kCamPf = !kBvh;
     __shared__ CamSlots cslots[kCamPf ? kWavesPerBlock : 1];
     // traversal stacks (kBvh): kWavesPerBlock x L.stack_depth x 64 lanes, sized per scene at launch
     extern __shared__ uint32_t dyn_stacks[];
@@ -1917,10 +1253,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
     uint64_t tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
     for (;;) {
-#if RT_LK
         const RenderLaunch& L = launch_args();  // this trip's view of the launch parameters
         const int SP = L.lanes_per_pixel;
-#endif
         RT_STAMP(t_q);
         if (kQueue) {
             // lanes without work take the next items once enough lanes are idle
@@ -1952,10 +1286,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                 }
             });
         }
-#if RT_TAIL_STEAL
         if (kQueue && exhausted)
             tail_steal(L, W, lane, SP, alive, waiting, held, towner, tl_pack, own_end, s, item, sum, thr, need_cam);
-#endif
         if (__ballot(alive || waiting || held || (kQueue && !exhausted)) == 0) break;  // wave-uniform exit
         RT_STAMP(t_a);
         RT_ACC(7, t_q, t_a);
@@ -2048,7 +1380,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             v3 p = add(ray.o, scale(ray.d, h.t));  // ray.at(t)
             v3 outward;
             constexpr bool kAnySph = kSph || kMed;
-            if ((kMed || (kBvh && kSph) || !RT_MED_VARIANT) && ob.type == kObjMedium) {
+            if ((kMed || (kBvh && kSph)) && ob.type == kObjMedium) {
                 outward = v3{1.0f, 0.0f, 0.0f};  // arbitrary; isotropic scatter ignores it
             } else if (ob.type == kObjPlane) {
                 outward = v3{f[3], f[4], f[5]};
@@ -2321,291 +1653,17 @@ struct PtBest {
     v3 hit;
 };
 
-// Kuchkuda triangle tests of one leaf (CUDAPathTracer.cu:258-345).
-__device__ __forceinline__ void pt_leaf(const KTri* __restrict__ ktris,
-                                        const int32_t* __restrict__ tri_list, uint32_t u0,
-                                        uint32_t u1, const PtRay& r, int avoid, PtBest& b,
-                                        Counters& cnt) {
-    const uint32_t n = u0 & 0x7FFFFFFFu;
-    cnt.tri_tests += n;
-    for (uint32_t i = u1; i < u1 + n; ++i) {
-        const int idx = tri_list[i];
-        if (avoid == idx) continue;
-        const float4* T = reinterpret_cast<const float4*>(ktris + idx);
-        const float4 q0 = T[0], q1 = T[1], q2 = T[2], q3 = T[3];
-        const v3 nn{q0.x, q0.y, q0.z};
-        const float k = dot(nn, r.d);
-        if (k == 0.0f) continue;
-        const float sd = fdiv(q0.w - dot(nn, r.o), k);
-        if (sd <= 0.0f) continue;
-        if (sd <= 1e-3f) continue;  // NUDGE_FACTOR
-        const v3 hit = add(scale(r.d, sd), r.o);
-        if (dot(v3{q1.x, q1.y, q1.z}, hit) - q1.w < 0.0f) continue;
-        if (dot(v3{q2.x, q2.y, q2.z}, hit) - q2.w < 0.0f) continue;
-        if (dot(v3{q3.x, q3.y, q3.z}, hit) - q3.w < 0.0f) continue;
-        const v3 df = sub(r.o, hit);
-        const float hz = df.x * df.x + df.y * df.y + df.z * df.z;  // distancesq
-        if (hz < b.hz || (hz == b.hz && (int)i < b.i)) {
-            b.hz = hz;
-            b.dist = fsqrt(hz);
-            b.i = (int)i;
-            b.idx = idx;
-            b.hit = hit;
-        }
-    }
-}
-
-// BVH_IntersectTriangles (CUDAPathTracer.cu:192-352) as an ordered traversal.
-// The result is the minimum over (distance^2, DFS list position) of the
-// triangles in the leaves the reference reaches: every inner node gets the
-// reference's exact box decision, leaves are never box-tested, and a subtree
-// is skipped only when every point of its eps-widened box lies beyond the
-// best hit. Children are tested at their parent and the nearer is descended
-// first, which changes the order but not the set of candidates that can win.
-[[maybe_unused]] __device__ __forceinline__ void pt_traverse(const KTri* __restrict__ ktris,
-                                            const CFNode* __restrict__ nodes,
-                                            const int32_t* __restrict__ tri_list,
-                                            uint32_t* stack, const PtRay& r, int avoid,
-                                            float len_d, float eps, PtBest& b, Counters& cnt, int cap) {
-    auto pruned = [&](float tw) { return tw > 0.0f && tw * len_d > b.dist * 1.0001f + eps; };
-    CFNode cur = nodes[0];
-    ++cnt.node_visits;
-    bool has_cur = true;
-    if (!(cur.u0 & 0x80000000u)) {
-        float tw, od;
-        has_cur = pt_box_decide(cur, r, tw, od);
-    }
-    int sp = 0;
-    for (;;) {
-        if (!has_cur) {
-            if (sp == 0) break;
-            const uint32_t ni = stack[(--sp) * 64];
-            cur = nodes[ni];
-            ++cnt.node_visits;
-            float tw, od;
-            pt_box_bounds(cur, r, tw, od);
-            if (pruned(tw)) continue;  // the best hit improved since the push
-            has_cur = true;
-        }
-        if (cur.u0 & 0x80000000u) {
-            pt_leaf(ktris, tri_list, cur.u0, cur.u1, r, avoid, b, cnt);
-            has_cur = false;
-            continue;
-        }
-        const uint32_t i0 = cur.u0, i1 = cur.u1;
-        const CFNode c0 = nodes[i0], c1 = nodes[i1];
-        cnt.node_visits += 2;
-        float w0, o0, w1, o1;
-        bool h0, h1;
-        if (c0.u0 & 0x80000000u) {
-            pt_box_bounds(c0, r, w0, o0);
-            h0 = true;
-        } else {
-            h0 = pt_box_decide(c0, r, w0, o0);
-        }
-        if (c1.u0 & 0x80000000u) {
-            pt_box_bounds(c1, r, w1, o1);
-            h1 = true;
-        } else {
-            h1 = pt_box_decide(c1, r, w1, o1);
-        }
-        h0 = h0 && !pruned(w0);
-        h1 = h1 && !pruned(w1);
-        if (h0 && h1) {
-            if (sp + 1 > cap) {
-                cnt.overflow();
-                break;
-            }
-            const bool first0 = o0 <= o1;
-            stack[(sp++) * 64] = first0 ? i1 : i0;
-            cur = first0 ? c0 : c1;
-        } else if (h0) {
-            cur = c0;
-        } else if (h1) {
-            cur = c1;
-        } else {
-            has_cur = false;
-        }
-    }
-}
-
-// Cooperative BVH_IntersectTriangles (all lanes of the wave that reach it; the
-// same work stealing as mesh_bvh_coop). Lanes without a subtree take the oldest
-// pending subtree of a lane that has a spare one, with its ray and pruning bound;
-// per-ray minima of (distance^2, DFS list position), the reference's tie rule,
-// merge through 64-bit LDS atomic-min. Every subtree is traversed once with the
-// reference's exact box decisions and a bound no tighter than the owner's, so
-// the winner is the one BVH_IntersectTriangles finds. The owner recomputes the
-// winner's hit point with pt_leaf's operations.
-[[maybe_unused]] __device__ __forceinline__ void pt_traverse_coop(const KTri* __restrict__ ktris,
-                                                 const CFNode* __restrict__ nodes,
-                                                 const int32_t* __restrict__ tri_list, uint32_t* wstack,
-                                                 unsigned long long* keys, int32_t* vlist, int lane, bool want,
-                                                 const PtRay& ray, int avoid_in, float len_in, float eps_in,
-                                                 PtBest& out, Counters& cnt, int cap) {
-    const uint64_t wm = __ballot(want);
-    if (wm == 0) return;
-    key_reset(keys[lane]);
-    int owner = lane;
-    PtRay r = ray;
-    int avoid = avoid_in;
-    float len_d = len_in, eps = eps_in;
-    PtBest b{3.40282347e+38f, 3.40282347e+38f, 0x7FFFFFFF, -1, v3{0.0f, 0.0f, 0.0f}};
-    auto pruned = [&](float tw) { return tw > 0.0f && tw * len_d > b.dist * 1.0001f + eps; };
-    auto flush = [&]() {
-        if (b.i != 0x7FFFFFFF)
-            atomicMin(&keys[owner], ((unsigned long long)__float_as_uint(b.hz) << 32) | (uint32_t)b.i);
-        b.i = 0x7FFFFFFF;
-    };
-    auto refresh = [&]() {  // the ray's best over all lanes (NaN while none)
-        const float g = __uint_as_float((uint32_t)(keys[owner] >> 32));
-        if (g < b.hz) {
-            b.hz = g;
-            b.dist = fsqrt(g);
-        }
-    };
-    CFNode cur = nodes[0];
-    bool has = want;
-    if (want) {
-        ++cnt.node_visits;
-        if (!(cur.u0 & 0x80000000u)) {
-            float tw, od;
-            has = pt_box_decide(cur, r, tw, od);
-        }
-    }
-    int sp = 0, bot = 0;
-    __builtin_amdgcn_wave_barrier();
-    for (;;) {
-        if (__ballot(has || sp > bot) == 0) break;
-        const bool idle = !has && sp == bot;
-        const bool spare = sp - bot >= (has ? 1 : 2);
-        const uint64_t im = __ballot(idle), vm = __ballot(spare);
-        if (im != 0 && vm != 0) {
-            const int nv = __popcll(vm), ni = __popcll(im);
-            if (spare) vlist[lane_rank(vm)] = lane;
-            __builtin_amdgcn_wave_barrier();
-            int vic = lane;
-            const bool thief = idle && lane_rank(im) < nv;
-            if (thief) vic = vlist[lane_rank(im)];
-            const int vb = __shfl(bot, vic, 64);
-            const int v_owner = __shfl(owner, vic, 64), v_avoid = __shfl(avoid, vic, 64);
-            PtRay vr;
-            vr.o = v3{__shfl(r.o.x, vic, 64), __shfl(r.o.y, vic, 64), __shfl(r.o.z, vic, 64)};
-            vr.d = v3{__shfl(r.d.x, vic, 64), __shfl(r.d.y, vic, 64), __shfl(r.d.z, vic, 64)};
-            vr.inv = v3{__shfl(r.inv.x, vic, 64), __shfl(r.inv.y, vic, 64), __shfl(r.inv.z, vic, 64)};
-            vr.pad_t = v3{__shfl(r.pad_t.x, vic, 64), __shfl(r.pad_t.y, vic, 64), __shfl(r.pad_t.z, vic, 64)};
-            vr.exact = __shfl((int)r.exact, vic, 64) != 0;
-            const float v_len = __shfl(len_d, vic, 64), v_eps = __shfl(eps, vic, 64);
-            const float v_hz = __shfl(b.hz, vic, 64), v_dist = __shfl(b.dist, vic, 64);
-            if (thief) {
-                const uint32_t entry = wstack[vb * 64 + vic];
-                flush();
-                owner = v_owner;
-                r = vr;
-                avoid = v_avoid;
-                len_d = v_len;
-                eps = v_eps;
-                b.hz = v_hz;
-                b.dist = v_dist;
-                refresh();
-                sp = bot = 0;
-                cur = nodes[entry];
-                ++cnt.node_visits;
-                float tw, od;
-                pt_box_bounds(cur, r, tw, od);
-                has = !pruned(tw);
-            }
-            if (spare && lane_rank(vm) < ni) ++bot;  // robbed
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (!has) {
-            if (sp > bot) {
-                cur = nodes[wstack[(--sp) * 64 + lane]];
-                ++cnt.node_visits;
-                refresh();
-                float tw, od;
-                pt_box_bounds(cur, r, tw, od);
-                has = !pruned(tw);  // the best hit improved since the push
-            }
-            if (sp == bot) sp = bot = 0;
-            if (!has) continue;
-        }
-        if (cur.u0 & 0x80000000u) {
-            pt_leaf(ktris, tri_list, cur.u0, cur.u1, r, avoid, b, cnt);
-            flush();
-            has = false;
-            continue;
-        }
-        const uint32_t i0 = cur.u0, i1 = cur.u1;
-        const CFNode c0 = nodes[i0], c1 = nodes[i1];
-        cnt.node_visits += 2;
-        float w0, o0, w1, o1;
-        bool h0, h1;
-        if (c0.u0 & 0x80000000u) {
-            pt_box_bounds(c0, r, w0, o0);
-            h0 = true;
-        } else {
-            h0 = pt_box_decide(c0, r, w0, o0);
-        }
-        if (c1.u0 & 0x80000000u) {
-            pt_box_bounds(c1, r, w1, o1);
-            h1 = true;
-        } else {
-            h1 = pt_box_decide(c1, r, w1, o1);
-        }
-        h0 = h0 && !pruned(w0);
-        h1 = h1 && !pruned(w1);
-        if (h0 && h1) {
-            if (sp + 1 > cap) {
-                cnt.overflow();
-                has = false;
-                sp = bot = 0;
-                continue;
-            }
-            const bool first0 = o0 <= o1;
-            wstack[(sp++) * 64 + lane] = first0 ? i1 : i0;
-            cur = first0 ? c0 : c1;
-        } else if (h0) {
-            cur = c0;
-        } else if (h1) {
-            cur = c1;
-        } else {
-            has = false;
-        }
-    }
-    flush();
-    __builtin_amdgcn_wave_barrier();
-    if (want) {
-        const unsigned long long key = keys[lane];
-        if (key != ~0ull) {
-            // the winner's hit point with pt_leaf's operations on the owner's ray
-            const int i = (int)(uint32_t)(key & 0xFFFFFFFFu);
-            const int idx = tri_list[i];
-            const float4 q0 = reinterpret_cast<const float4*>(ktris + idx)[0];
-            const v3 nn{q0.x, q0.y, q0.z};
-            const float k = dot(nn, ray.d);
-            const float sd = fdiv(q0.w - dot(nn, ray.o), k);
-            const float hz = __uint_as_float((uint32_t)(key >> 32));
-            out.hz = hz;
-            out.dist = fsqrt(hz);
-            out.i = i;
-            out.idx = idx;
-            out.hit = add(scale(ray.d, sd), ray.o);
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-}
-
-#ifndef RT_PT_DERIVE
-#define RT_PT_DERIVE 1  // pathTrace queue mode derives the pixel from the work item at the camera (0: kept, A/B)
-#endif
-#ifndef RT_PT_PAIRS
-#define RT_PT_PAIRS 1  // pathTrace traversal over child-pair records (cf_child_pairs; 0: node records, A/B)
-#endif
-#if RT_LEAF_BATCH
-// pt_traverse_coop with deferred leaf tests (as mesh_bvh_coop): leaves append (DFS list
+// BVH_IntersectTriangles (CUDAPathTracer.cu:192-352) as a cooperative ordered traversal over
+// child-pair records (rt_bvh.cpp cf_child_pairs). The result is the minimum over (distance^2,
+// DFS list position) of the triangles in the leaves the reference reaches: every inner box gets
+// the reference's exact decision (pt_box_decide), leaf boxes are never box-tested (the child
+// record says which boxes are leaves'), and a subtree is skipped only when every point of its
+// eps-widened box lies beyond the best hit. Children are tested at their parent and the nearer
+// is descended first, which changes the order but not the set of candidates that can win.
+// Lanes without a subtree take the oldest pending subtree of a lane that has a spare one, with
+// its ray and pruning bound (as mesh_bvh_pairs). Leaves append (DFS list
 // position, ray owner) pairs to a per-wave LDS queue, three per lane and trip, and the wave
-// runs pt_leaf's Kuchkuda test on 64 queued pairs at once, one per lane, each merged into its
+// runs the Kuchkuda triangle test (CUDAPathTracer.cu:258-345) on 64 queued pairs at once, one per lane, each merged into its
 // ray's LDS minimum of (distance^2, list position) - the reference's first-in-DFS tie rule.
 // Pairs take their ray (origin, direction, avoidSelf) from the owner lane's registers.
 __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict__ ktris,
@@ -2630,12 +1688,7 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
             bdist = fsqrt(g);
         }
     };
-#if RT_PT_PAIRS
     uint32_t cur = root_ref;  // pair index or leaf reference
-#else
-    (void)root_ref;
-    CFNode cur = nodes[0];
-#endif
     bool has = want;
     if (want) {
         ++cnt.node_visits;
@@ -2657,7 +1710,7 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
         const v3 pd{__shfl(ray.d.x, own, 64), __shfl(ray.d.y, own, 64), __shfl(ray.d.z, own, 64)};
         const int pav = __shfl(avoid_in, own, 64);
         if (act) {
-            // pt_leaf's test for list position i (CUDAPathTracer.cu:258-345)
+            // the Kuchkuda test for list position i (CUDAPathTracer.cu:258-345)
             const int idx = tri_list[i];
             if (pav != idx) {
                 const float4* T = reinterpret_cast<const float4*>(ktris + idx);
@@ -2716,21 +1769,12 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
                 const uint32_t entry = wstack[vb * 64 + vic];
                 refresh();
                 sp = bot = 0;
-#if RT_PT_PAIRS
                 cur = entry;
                 has = true;
-#else
-                cur = nodes[entry];
-                ++cnt.node_visits;
-                float tw, od;
-                pt_box_bounds(cur, r, tw, od);
-                has = !pruned(tw);
-#endif
             }
             if (spare && lane_rank(vm) < ni) ++bot;  // robbed
             __builtin_amdgcn_wave_barrier();
         }
-#if RT_PT_PAIRS
         if (!has && sp > bot) {
             cur = wstack[(--sp) * 64 + lane];
             refresh();
@@ -2785,69 +1829,6 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
                 has = false;
             cnt.tri_tests += ln;
         }
-#else
-        if (!has && sp > bot) {
-            cur = nodes[wstack[(--sp) * 64 + lane]];
-            ++cnt.node_visits;
-            refresh();
-            float tw, od;
-            pt_box_bounds(cur, r, tw, od);
-            has = !pruned(tw);  // the best hit improved since the push
-        }
-        if (!has && sp == bot) sp = bot = 0;
-        uint32_t lk = 0, ln = 0;  // this trip's leaf pairs: list positions lk .. lk + ln - 1
-        if (has) {
-            if (cur.u0 & 0x80000000u) {
-                const uint32_t nt = cur.u0 & 0x7FFFFFFFu;
-                ln = nt < 3u ? nt : 3u;
-                lk = cur.u1;
-                if (nt > 3u) {  // a larger leaf keeps this lane for more trips
-                    cur.u1 += 3u;
-                    cur.u0 -= 3u;
-                } else {
-                    has = false;
-                }
-                cnt.tri_tests += ln;
-            } else {
-                const uint32_t i0 = cur.u0, i1 = cur.u1;
-                const CFNode c0 = nodes[i0], c1 = nodes[i1];
-                cnt.node_visits += 2;
-                float w0, o0, w1, o1;
-                bool h0, h1;
-                if (c0.u0 & 0x80000000u) {
-                    pt_box_bounds(c0, r, w0, o0);
-                    h0 = true;
-                } else {
-                    h0 = pt_box_decide(c0, r, w0, o0);
-                }
-                if (c1.u0 & 0x80000000u) {
-                    pt_box_bounds(c1, r, w1, o1);
-                    h1 = true;
-                } else {
-                    h1 = pt_box_decide(c1, r, w1, o1);
-                }
-                h0 = h0 && !pruned(w0);
-                h1 = h1 && !pruned(w1);
-                if (h0 && h1) {
-                    if (sp + 1 > cap) {
-                        cnt.overflow();
-                        has = false;
-                        sp = bot = 0;
-                    } else {
-                        const bool first0 = o0 <= o1;
-                        wstack[(sp++) * 64 + lane] = first0 ? i1 : i0;
-                        cur = first0 ? c0 : c1;
-                    }
-                } else if (h0) {
-                    cur = c0;
-                } else if (h1) {
-                    cur = c1;
-                } else {
-                    has = false;
-                }
-            }
-        }
-#endif
         const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
         if (b1) {
             const uint32_t at = qtail + (uint32_t)(lane_rank(b1) + lane_rank(b2) + lane_rank(b3));
@@ -2867,7 +1848,7 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
     if (want) {
         const unsigned long long key = keys[lane];
         if (key != ~0ull) {
-            // the winner's hit point with pt_leaf's operations on the owner's ray
+            // the winner's hit point with the batch test's operations on the owner's ray
             const int i = (int)(uint32_t)(key & 0xFFFFFFFFu);
             const int idx = tri_list[i];
             const float4 q0 = reinterpret_cast<const float4*>(ktris + idx)[0];
@@ -2884,7 +1865,6 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
     }
     __builtin_amdgcn_wave_barrier();
 }
-#endif
 
 }  // namespace
 
@@ -2896,9 +1876,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
     extern __shared__ uint32_t dyn_stacks[];  // kWavesPerBlock x L.stack_depth x 64, sized at launch
     __shared__ unsigned long long pt_keys[kWavesPerBlock][64];  // per-ray minima (cooperative traversal)
     __shared__ int32_t pt_vlist[kWavesPerBlock][64];            // victims of a steal round
-#if RT_LEAF_BATCH
     __shared__ uint32_t pt_queue[kWavesPerBlock][256];          // deferred leaf pairs
-#endif
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     uint32_t* stack = dyn_stacks + (size_t)wave * L.stack_depth * 64 + lane;
@@ -2928,27 +1906,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
     Rng rng{1u, 0u, 0u, 0u};
 
     for (;;) {
-#if RT_LK
         const RenderLaunch& L = launch_args();  // this trip's view of the launch parameters
         const int SP = L.lanes_per_pixel;
-#endif
         const bool has_mesh = L.pt_has_mesh != 0;
         if (kQueue) {
             queue_refill(L, lane, alive, exhausted, shard, shards_tried, [&](uint32_t it) {
-#if RT_PT_DERIVE
                 // only `item` is kept across the traversal: the pixel is derived from it at the
                 // camera (as render_kernel does), which frees four VGPRs for the traversal
                 int ic, ipx, ilr;
                 if (!queue_item(L, it, ic, ipx, ilr)) return;  // past the frame edge: ask again
                 item = it;
                 s = ic;
-#else
-                if (!queue_item(L, it, c, px, lrow)) return;  // past the frame edge: ask again
-                item = it;
-                y = global_row_of(L, lrow);
-                pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
-                s = c;
-#endif
                 sum = v3{0.0f, 0.0f, 0.0f};
                 alive = s < L.spp;
                 // a sub-stream with no samples (S > spp) still owns its partial-sum slot
@@ -2958,14 +1926,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
         }
         if (__ballot(alive || (kQueue && !exhausted)) == 0) break;
         if (alive && need_cam) {
-#if RT_PT_DERIVE
             if (kQueue) {
                 int ic, ilr;
                 queue_item(L, item, ic, px, ilr);
                 y = global_row_of(L, ilr);
                 pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
             }
-#endif
             const Ray r = camera_sample(cam, L, rng, pixel, px, y, s, (float)(L.width - 1), (float)(L.height - 1));
             o = r.o;
             d = r.d;
@@ -2993,19 +1959,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
             // coordinates involved), with a 10x margin.
             const float eps = 1e-5f * (1.0f + fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) + L.pt_scale);
             r.pad_t = v3{eps * fabsf(r.inv.x), eps * fabsf(r.inv.y), eps * fabsf(r.inv.z)};
-#if RT_BVH_STEAL
-#if RT_LEAF_BATCH
             pt_traverse_coop_batched(ktris, nodes, tri_list, stack - lane, pt_keys[wave], pt_vlist[wave], pt_queue[wave],
                                      lane, alive, r, avoid, fsqrt(dot(d, d)), eps, best, cnt, L.stack_depth,
                                      L.pt_root_ref);
-#else
-            pt_traverse_coop(ktris, nodes, tri_list, stack - lane, pt_keys[wave], pt_vlist[wave], lane, alive, r,
-                             avoid, fsqrt(dot(d, d)), eps, best, cnt, L.stack_depth);
-#endif
-#else
-            if (alive)
-                pt_traverse(ktris, nodes, tri_list, stack, r, avoid, fsqrt(dot(d, d)), eps, best, cnt, L.stack_depth);
-#endif
         }
         cnt.segs += (uint32_t)__popcll(__ballot(alive));
         if (!alive) continue;
@@ -3217,17 +2173,17 @@ uint32_t select_variant(bool pathtrace, bool queue, bool bvh, bool media, bool f
     if (pathtrace) return queue ? RT_VARIANT_PATHTRACE_QUEUE : RT_VARIANT_PATHTRACE_STATIC;
     if (!queue) {
         if (bvh) return RT_VARIANT_BVH_STATIC;
-        if (media && RT_MED_VARIANT) return RT_VARIANT_SCAN_MEDIA_STATIC;
-        if (!full && RT_NOSPH_VARIANT) return RT_VARIANT_SCAN_SIMPLE_STATIC;
+        if (media) return RT_VARIANT_SCAN_MEDIA_STATIC;
+        if (!full) return RT_VARIANT_SCAN_SIMPLE_STATIC;
         return RT_VARIANT_SCAN_STATIC;
     }
-    if (bvh && bvh_parts == 1 && !full && !media && RT_BVH_PARTS_VARIANT && RT_NOSPH_VARIANT)
+    if (bvh && bvh_parts == 1 && !full && !media)
         return RT_VARIANT_BVH_MESH_SIMPLE_QUEUE;
-    if (bvh && bvh_parts == 1 && RT_BVH_PARTS_VARIANT) return RT_VARIANT_BVH_MESH_QUEUE;
-    if (bvh && bvh_parts == 2 && RT_BVH_PARTS_VARIANT) return RT_VARIANT_BVH_GROUP_QUEUE;
+    if (bvh && bvh_parts == 1) return RT_VARIANT_BVH_MESH_QUEUE;
+    if (bvh && bvh_parts == 2) return RT_VARIANT_BVH_GROUP_QUEUE;
     if (bvh) return RT_VARIANT_BVH_QUEUE;
-    if (media && RT_MED_VARIANT) return RT_VARIANT_SCAN_MEDIA_QUEUE;
-    if (!full && RT_NOSPH_VARIANT) return RT_VARIANT_SCAN_SIMPLE_QUEUE;
+    if (media) return RT_VARIANT_SCAN_MEDIA_QUEUE;
+    if (!full) return RT_VARIANT_SCAN_SIMPLE_QUEUE;
     return RT_VARIANT_SCAN_QUEUE;
 }
 
@@ -3277,9 +2233,9 @@ uint32_t kernel_build_flags() {
 #ifdef RT_STAMPS
     f |= 2u;  // RT_BUILD_STAMPS
 #endif
-#if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || !RT_MESH_TWO_PHASE || !RT_BVH_STEAL || \
-    !RT_TAIL_STEAL || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || RT_PT_WAVES != 6 || \
-    defined(RT_U01_MULADD) || !RT_OBJ_PREFETCH || !RT_MED_VARIANT || !RT_MED_MERGE1 || !RT_MESH_RUN || !RT_ORDERED_MERGE || !RT_NOSPH_VARIANT || !RT_BVH_PARTS_VARIANT || !RT_LEAF_BATCH || !RT_SG_BATCH || !RT_BVH_PAIRS || !RT_SG_PAIRS || !RT_PT_PAIRS || !RT_CAM_SLOTS || RT_CAM_BATCH != 32 || !RT_PT_DERIVE
+#if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
+    RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
+    RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;

@@ -70,14 +70,20 @@ def test_hostile_ply_headers_are_handled(tmp_path):
 
 def test_fast_split_search_equals_reference_search():
     # the builder's O(N log N) split search (sorted prefix/suffix boxes) must give
-    # Recurse's tree byte for byte; RTMI_BVH_REFERENCE_SEARCH=1 runs the
-    # reference's own O(N x bins) loop for comparison (bun_zipper, 69,451 triangles)
+    # Recurse's tree byte for byte; the oracle restates the reference's own
+    # O(N x bins) loop (BVH.cpp:94-333) for comparison (bun_zipper, 69,451 triangles,
+    # which the reference ships no `.bvh` cache for)
+    from oracle import oracle as O
     path = os.path.join(S.MODELS, "bunny", "bun_zipper.ply")
     fast = bvh_image(path, (0.0, -0.15, -0.1), 0.35)
-    os.environ["RTMI_BVH_REFERENCE_SEARCH"] = "1"
-    try:
-        ref = bvh_image(path, (0.0, -0.15, -0.1), 0.35)
-    finally:
-        del os.environ["RTMI_BVH_REFERENCE_SEARCH"]
+    ref = O.bvh_image(O.load_ply(path, (0.0, -0.15, -0.1), 0.35))
     assert fast == ref
     assert int.from_bytes(fast[4:8], "little") == 69451
+
+
+def test_oracle_builder_reproduces_reference_cache():
+    # the oracle's Recurse restatement (the checker of the test above) is itself
+    # pinned by a cache the reference ships: bunny.ply.bvh, byte for byte
+    from oracle import oracle as O
+    soup = O.load_ply(os.path.join(S.MODELS, "bunny", "bunny.ply"))
+    assert O.bvh_image(soup) == open(os.path.join(S.GOLDEN, "bvh", "bunny.ply.bvh"), "rb").read()

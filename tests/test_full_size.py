@@ -39,7 +39,25 @@ CONFIGS = {
     "C5_media": ("cornell_box_media", "cornellbox_media.yaml", 2048, 2048, 1024, 16, 2048, (300, 1555)),
     # Suzanne box (the geometry of the images.MD:44-53 timing image): 512^2, 32 spp, 10 bounces
     "suzanne_published": ("suzanne_cornell_box", "suzanne_cornellbox.yaml", 512, 512, 32, 10, 128, (3, 77)),
+    # the headline frame exactly as bench.py times it: three frames in flight
+    # (RT_RENDER_FRAMES_IN_FLIGHT), whose auto layout bench.py reports as config.lanes_per_pixel
+    "C2_cornellbox1_bench_layout": ("cornell_box1", "cornellbox1.yaml", 512, 512, 128, 8, 32, (0, 21)),
 }
+IN_FLIGHT = {"C2_cornellbox1_bench_layout"}
+
+
+def _bench_lanes(w, h, spp, depth):
+    """The sub-stream layout bench.py's default (N = 1) line renders with, from its own params."""
+    import bench
+    import raytracingthenextweekcuda_amd as rtmi
+
+    assert (bench.SCENES["cornellbox1"][1:5]) == (w, h, spp, depth)
+    with rtmi.Renderer(0) as r:
+        rtmi.cornell_box1(r, w, h)
+        # bench.measure()'s params (seed 1984, row_block 2, rank 0 of 1, lanes 0 = auto, rayColor),
+        # frames_in_flight as when three contexts overlap (the default for CB1 at N = 1)
+        r.render(w, h, spp, depth, 1984, 0, 2, 0, 1, 0, "rayColor", frames_in_flight=True)
+        return int(r.stats()["lanes_per_pixel"])
 
 
 def _oracle_scene(name, w, h):
@@ -69,11 +87,14 @@ def test_full_frame_spot_rows_and_sharding(cfg):
 
     loader, scene_file, w, h, spp, depth, K, ranks = CONFIGS[cfg]
     oracle = _oracle_scene(scene_file, w, h)
+    fif = cfg in IN_FLIGHT
     with rtmi.Renderer(0) as r:
         getattr(rtmi, loader)(r, w, h)
-        full = r.render(w, h, spp, depth, lanes_per_pixel=0)
+        full = r.render(w, h, spp, depth, lanes_per_pixel=0, frames_in_flight=fif)
         st = r.stats()
         lanes = int(st["lanes_per_pixel"])
+        if fif:  # the layout checked here is the one the bench line times and reports
+            assert lanes == _bench_lanes(w, h, spp, depth), lanes
         assert st["samples"] == w * h * spp and st["overflow"] == 0
         assert np.isfinite(full).all() and (full >= 0).all()
 

@@ -3,7 +3,9 @@
 #   TESTS=1   pytest -m gpu + smoke()
 #   BENCH=1   the default bench line (config 2, frame overlap, CPU baseline)
 #   SCENES    bench lines of these workloads (no CPU baseline); ALT = A/B libraries run after each
-#   VALU      SQ_INSTS_VALU passes of these workloads (--no-overlap), for profiles/valu_issue.json
+#   VALU      SQ_INSTS_VALU (+ lane utilisation, wait shares) passes of these workloads (--no-overlap,
+#             BENCH_ARGS appended: --in-flight-layout for the timed layout), for profiles/valu_issue.json
+#   PROBE=1   tools/valu_probe under SQ counters with 64 and 16 active lanes (lane-utilisation calibration)
 #   TRAFFIC   FETCH_SIZE and WRITE_SIZE passes (separate runs), for profiles/pmc_traffic.json
 #   PROF      rocprofv3 --kernel-trace --stats of these workloads (--no-overlap)
 #   MULTI=1   examples/multigpu (RCCL through the C ABI, N = 1 on this box)
@@ -13,6 +15,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${TAG:-session}
 mkdir -p "$O"
+# the passes profile the layout the timed line uses: CB1's line keeps three frames in flight
+lay() { if [ "$1" = "cornellbox1" ]; then echo "--in-flight-layout"; fi; }
 stop_if_fatal() { rc=$1; name=$2; echo "$name rc=$rc"; if [ "$rc" -ne 0 ]; then echo "fatal in $name"; exit "$rc"; fi; }
 export TMPDIR=/tmp
 if [ "${TESTS:-0}" = "1" ]; then
@@ -33,18 +37,24 @@ for sc in ${SCENES:-}; do
     stop_if_fatal $? bench_${sc}_$alt
   done
 done
+if [ "${PROBE:-0}" = "1" ] && [ -x ./tools/valu_probe ]; then  # lane-utilisation calibration (64 / 16 lanes)
+  for a in 64 16; do
+    timeout -s KILL 60 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU --output-format csv -d "$O/probe_lanes_$a" -o pmc -- ./tools/valu_probe 10000 4 0 $a > "$O/probe_lanes_$a.log" 2>&1
+    stop_if_fatal $? probe_lanes_$a
+  done
+fi
 for sc in ${VALU:-}; do
-  timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --output-format csv -d "$O/pmc_valu_$sc" -o pmc -- python3 bench.py --scene $sc --steps 2 --warmup 1 --no-cpu-baseline --no-overlap > "$O/pmc_valu_$sc.log" 2>&1
+  timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_ANY --output-format csv -d "$O/pmc_valu_$sc" -o pmc -- python3 bench.py --scene $sc --steps 2 --warmup 1 --no-cpu-baseline --no-overlap $(lay $sc) > "$O/pmc_valu_$sc.log" 2>&1
   stop_if_fatal $? pmc_valu_$sc
 done
 for sc in ${TRAFFIC:-}; do
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_${sc}_$c" -o pmc -- python3 bench.py --scene $sc --steps 1 --warmup 1 --no-cpu-baseline --no-overlap > "$O/pmc_${sc}_$c.log" 2>&1
+    timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_${sc}_$c" -o pmc -- python3 bench.py --scene $sc --steps 1 --warmup 1 --no-cpu-baseline --no-overlap $(lay $sc) > "$O/pmc_${sc}_$c.log" 2>&1
     stop_if_fatal $? pmc_${sc}_$c
   done
 done
 for sc in ${PROF:-}; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$sc" -o run --output-format csv -- python3 bench.py --scene $sc --steps ${PROF_STEPS:-10} --warmup ${PROF_WARMUP:-2} --no-cpu-baseline --no-overlap > "$O/prof_$sc.log" 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$sc" -o run --output-format csv -- python3 bench.py --scene $sc --steps ${PROF_STEPS:-10} --warmup ${PROF_WARMUP:-2} --no-cpu-baseline --no-overlap $(lay $sc) > "$O/prof_$sc.log" 2>&1
   stop_if_fatal $? prof_$sc
 done
 if [ "${MULTI:-0}" = "1" ] && [ -x ./examples/multigpu ]; then

@@ -6,13 +6,17 @@
 // which calibrates rocprofv3's SQ_INSTS_VALU (is it the whole chip? per XCD?), and the
 // timed run gives the chip's sustained VALU issue rate against the spec peak
 // (1024 SIMDs x 2.4 GHz / 2 cycles per wave64 v_fma_f32, MI355X_MICROARCH.md).
-//   ./valu_probe [iters=20000] [waves_per_simd=4] [inline_constants=0]
+// With active_lanes < 64 only lanes [0, active_lanes) of each wave run the loop: the same
+// instruction count at a known lane utilisation (active_lanes / 64), which calibrates the
+// lane-utilisation counter ratio SQ_THREAD_CYCLES_VALU / 64 / SQ_ACTIVE_INST_VALU.
+//   ./valu_probe [iters=20000] [waves_per_simd=4] [inline_constants=0] [active_lanes=64]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
 
-__global__ __launch_bounds__(256) void valu_probe(float* out, int iters) {
+__global__ __launch_bounds__(256) void valu_probe(float* out, int iters, int active) {
+    if ((int)(threadIdx.x & 63) >= active) iters = 0;
     float a0 = threadIdx.x * 1e-3f, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;
     float a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
     const float x = 0.999f, y = 1e-4f;
@@ -34,7 +38,8 @@ __global__ __launch_bounds__(256) void valu_probe(float* out, int iters) {
 
 // The same count with inline-constant operands: each v_fma_f32 reads ONE VGPR (no
 // register-bank pressure from shared source operands), the issue-rate ceiling.
-__global__ __launch_bounds__(256) void valu_probe_k(float* out, int iters) {
+__global__ __launch_bounds__(256) void valu_probe_k(float* out, int iters, int active) {
+    if ((int)(threadIdx.x & 63) >= active) iters = 0;
     float a0 = threadIdx.x * 1e-3f, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;
     float a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
     for (int i = 0; i < iters; ++i) {
@@ -56,6 +61,7 @@ int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 20000;
     const int wps = argc > 2 ? atoi(argv[2]) : 4;
     const int konst = argc > 3 ? atoi(argv[3]) : 0;  // 1: the inline-constant kernel
+    const int active = argc > 4 ? atoi(argv[4]) : 64;  // lanes per wave that run the loop
     auto kern = konst ? valu_probe_k : valu_probe;
     int dev = 0, n_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -66,11 +72,11 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, nullptr, out, iters);  // warm-up
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, nullptr, out, iters, active);  // warm-up
     float best = 1e30f;
     for (int rep = 0; rep < 5; ++rep) {
         hipEventRecord(e0, nullptr);
-        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, nullptr, out, iters);
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, nullptr, out, iters, active);
         hipEventRecord(e1, nullptr);
         hipEventSynchronize(e1);
         float ms = 0;
@@ -80,9 +86,9 @@ int main(int argc, char** argv) {
     const double waves = (double)blocks * 4;
     const double insts = waves * 8.0 * iters;  // loop body only; the prologue/epilogue add a few per wave
     const double peak = (double)n_cu * 4 * 2.4e9 / 2.0;
-    printf("{\"kernel\": \"%s\", \"iters\": %d, \"waves_per_simd\": %d, \"cus\": %d, \"waves\": %.0f, \"loop_valu_insts\": %.6g, \"best_ms\": %.4f, "
+    printf("{\"kernel\": \"%s\", \"iters\": %d, \"active_lanes\": %d, \"waves_per_simd\": %d, \"cus\": %d, \"waves\": %.0f, \"loop_valu_insts\": %.6g, \"best_ms\": %.4f, "
            "\"inst_per_s\": %.6g, \"spec_peak_inst_per_s\": %.6g, \"frac_of_spec\": %.4f, \"launches\": 6}\n",
-           konst ? "valu_probe_k (inline constants)" : "valu_probe (VGPR operands)", iters, wps, n_cu, waves, insts, best, insts / (best * 1e-3), peak, insts / (best * 1e-3) / peak);
+           konst ? "valu_probe_k (inline constants)" : "valu_probe (VGPR operands)", iters, active, wps, n_cu, waves, insts, best, insts / (best * 1e-3), peak, insts / (best * 1e-3) / peak);
     hipFree(out);
     return 0;
 }

@@ -3,6 +3,9 @@
   python tools/valu_summary.py calibrate <probe_dir_10000> <probe_dir_20000> [valu_probe.json]
       -> profiles/<round>/valu_probe.json: SQ_INSTS_VALU of tools/valu_probe at two trip
          counts; their difference must be waves x 8 x d_iters (the whole chip, exactly).
+  python tools/valu_summary.py lanes <probe_dir_64> <probe_dir_16>
+      -> the lane-utilisation counter ratio SQ_THREAD_CYCLES_VALU / 64 / SQ_ACTIVE_INST_VALU of
+         tools/valu_probe with 64 and 16 active lanes per wave (expected 1 and 0.25).
   python tools/valu_summary.py workload <pmc_dir> <bench_log> [out_json]
       -> merges {workload: valu_insts_per_segment, ...} into profiles/valu_issue.json, from
          the render/pathtrace kernel dispatches of a `--pmc SQ_INSTS_VALU SQ_WAVES
@@ -51,6 +54,24 @@ def calibrate(d1, d2, probe_json=None):
     return res
 
 
+def lane_util(c):
+    """Mean active lanes per issued wave64 VALU instruction, as a fraction of 64."""
+    if not c.get("SQ_ACTIVE_INST_VALU") or "SQ_THREAD_CYCLES_VALU" not in c:
+        return None
+    return c["SQ_THREAD_CYCLES_VALU"] / 64.0 / c["SQ_ACTIVE_INST_VALU"]
+
+
+def lanes(d64, d16):
+    out = {"probe": "tools/valu_probe: the same VALU loop run by 64 or 16 lanes of each wave"}
+    for name, d, want in (("active_64", d64, 1.0), ("active_16", d16, 0.25)):
+        ds = dispatches(d, ["valu_probe"])
+        v = list(ds.values())[-1]["counters"]
+        out[name] = {"sq_thread_cycles_valu": v.get("SQ_THREAD_CYCLES_VALU"),
+                     "sq_active_inst_valu": v.get("SQ_ACTIVE_INST_VALU"),
+                     "sq_insts_valu": v.get("SQ_INSTS_VALU"), "lane_util": lane_util(v), "expected": want}
+    return out
+
+
 def workload(pmc_dir, bench_log, out_json):
     line = next(json.loads(s) for s in open(bench_log) if s.startswith("{"))
     wl = line["config"]["workload"]
@@ -64,11 +85,19 @@ def workload(pmc_dir, bench_log, out_json):
     # every dispatch of the pass renders the same frame (warm-up + timed): take their mean
     per_launch = sum(insts) / len(insts)
     clk = [v["counters"]["GRBM_GUI_ACTIVE"] / 8 / (v["ns"] * 1e-9) / 1e9 for v in ds.values() if v["ns"] > 0]
+    tot = collections.Counter()
+    for v in ds.values():
+        tot.update(v["counters"])
     ent = {"kernel": next(iter(ds.values()))["kernel"].split("(")[0],
            "valu_insts_per_launch": per_launch, "spread": (max(insts) - min(insts)) / per_launch,
            "segments_per_launch": segs, "valu_insts_per_segment": per_launch / segs,
            "effective_clock_ghz": sum(clk) / len(clk) if clk else None,
            "dispatches": len(insts), "source": os.path.relpath(pmc_dir, REPO),
+           # VALU lane utilisation (SQ_THREAD_CYCLES_VALU / 64 / SQ_ACTIVE_INST_VALU, calibrated with
+           # tools/valu_probe's active-lane mode) and the wave-cycle shares, summed over the dispatches
+           "valu_lane_util": lane_util(tot),
+           "wait_inst_any_share": (tot["SQ_WAIT_INST_ANY"] / tot["SQ_WAVE_CYCLES"]) if tot.get("SQ_WAVE_CYCLES") else None,
+           "wait_any_share": (tot["SQ_WAIT_ANY"] / tot["SQ_WAVE_CYCLES"]) if tot.get("SQ_WAVE_CYCLES") else None,
            # what bench.py checks before using the entry: the launched symbol and the kernel sources
            "variant": variant, "kernel_source_sha": line["config"].get("kernel_source_sha")}
     d = json.load(open(out_json)) if os.path.exists(out_json) else {}
@@ -84,6 +113,8 @@ def workload(pmc_dir, bench_log, out_json):
 if __name__ == "__main__":
     if sys.argv[1] == "calibrate":
         print(json.dumps(calibrate(*sys.argv[2:5]), indent=1))
+    elif sys.argv[1] == "lanes":
+        print(json.dumps(lanes(*sys.argv[2:4]), indent=1))
     else:
         out = sys.argv[4] if len(sys.argv) > 4 else os.path.join(REPO, "profiles", "valu_issue.json")
         print(workload(sys.argv[2], sys.argv[3], out))
