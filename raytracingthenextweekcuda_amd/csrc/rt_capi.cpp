@@ -749,9 +749,8 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
             }
         }
         if (have) {
-            const int waves =
-                rt::variant_waves(rt::select_variant(pathtrace, true, bvh, c->has_media, c->full_scan, c->bvh_parts));
-            L.queue = rt::queue_blocks(c->n_cu, waves);
+            L.queue = rt::queue_blocks(
+                c->n_cu, rt::select_variant(pathtrace, true, bvh, c->has_media, c->full_scan, c->bvh_parts), L);
             L.n_items = (uint32_t)items;
             L.n_pix = (uint32_t)(items >> L.sp_log2);
             // refill threshold (idle lanes a wave collects before one dequeue): 4 for long

@@ -137,8 +137,9 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
                             float* out, unsigned long long* counters, hipStream_t stream,
                             hipEvent_t main_done);
 
-// Workgroups of the persistent work-queue grid (n_cu x resident 4-wave blocks per CU).
-int queue_blocks(int n_cu, int waves_per_simd);
+// Workgroups of the persistent work-queue grid (n_cu x resident 4-wave blocks per CU: the
+// variant's occupancy, capped by the LDS its tables and L's traversal stacks take).
+int queue_blocks(int n_cu, uint32_t variant, const RenderLaunch& L);
 // The kernel instantiation of a launch (rtmi.h RT_VARIANT_*) from the integrator, the
 // schedule and the committed scene's content; the occupancy it is compiled for (waves per
 // SIMD); its symbol as rocprofv3 prints it (nullptr for an unknown id).

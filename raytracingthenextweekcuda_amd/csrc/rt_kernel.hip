@@ -309,6 +309,12 @@ __device__ __forceinline__ int lane_rank(uint64_t mask) {
 // re-tested at every pop, per-lane leaf loops) A popped entry is not re-tested against the improved bound
 // (its children are, on their pair load); pruning stays conservative, so the candidate set
 // still contains the sequential scan's winner and the (t, index) minimum picks it.
+// kWide: the same traversal over 4-wide nodes (rt_scene.h WideNode): an inner step is one
+// aligned 128 B load and four box tests; the hit children are sorted by entry distance, the
+// nearest becomes the lane's reference and the others are pushed farthest first, so the next
+// nearest is popped first. Half the dependent loads per ray of the child-pair records; the
+// stack bound is the builder's max over paths of sum (children - 1).
+template <bool kWide>
 __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
                                                const uint32_t* __restrict__ tri_orig,
                                                const BvhNode* __restrict__ nodes, uint32_t root, uint32_t base,
@@ -386,7 +392,54 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
         }
         if (!has && sp == bot) sp = bot = 0;
-        if (has && !(cur & kLeafRef)) {
+        if (kWide && has && !(cur & kLeafRef)) {
+            const float4* q = reinterpret_cast<const float4*>(nodes + 4 * (size_t)cur);
+            const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
+            const uint4 rf = reinterpret_cast<const uint4*>(q)[6];
+            cnt.node_visits += 4;
+            // entry distance of each child, +inf when missed (the sort keys)
+            const float bound = best * 1.00001f + 1e-30f;
+            auto test = [&](float x0, float y0, float z0, float x1, float y1, float z1) {
+                const float tx0 = (x0 - ro.x) * ri.x, tx1 = (x1 - ro.x) * ri.x;
+                const float ty0 = (y0 - ro.y) * ri.y, ty1 = (y1 - ro.y) * ri.y;
+                const float tz0 = (z0 - ro.z) * ri.z, tz1 = (z1 - ro.z) * ri.z;
+                const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+                const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+                return tn <= fminf(tf, bound) ? tn : kInf;
+            };
+            float k0 = test(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x), k1 = test(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y);
+            float k2 = test(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z), k3 = test(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w);
+            uint32_t r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
+            // sorting network (0,1) (2,3) (0,2) (1,3) (1,2): ascending entry distance
+            auto cx = [](float& ka, uint32_t& ra, float& kb, uint32_t& rb) {
+                const bool sw = kb < ka;
+                const float kt = sw ? kb : ka;
+                kb = sw ? ka : kb;
+                ka = kt;
+                const uint32_t rt = sw ? rb : ra;
+                rb = sw ? ra : rb;
+                ra = rt;
+            };
+            cx(k0, r0, k1, r1);
+            cx(k2, r2, k3, r3);
+            cx(k0, r0, k2, r2);
+            cx(k1, r1, k3, r3);
+            cx(k1, r1, k2, r2);
+            const int nh = (k0 < kInf) + (k1 < kInf) + (k2 < kInf) + (k3 < kInf);
+            if (nh == 0) {
+                has = false;
+            } else if (sp + nh - 1 > cap) {
+                cnt.overflow();
+                has = false;
+                sp = bot = 0;
+            } else {
+                if (nh > 3) wstack[(sp++) * 64 + lane] = r3;
+                if (nh > 2) wstack[(sp++) * 64 + lane] = r2;
+                if (nh > 1) wstack[(sp++) * 64 + lane] = r1;
+                cur = r0;
+            }
+        }
+        if (!kWide && has && !(cur & kLeafRef)) {
             const BvhNode nl = nodes[2 * (size_t)cur], nr = nodes[2 * (size_t)cur + 1];
             cnt.node_visits += 2;
             float tl, tr;
@@ -830,8 +883,9 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             } else if constexpr ((kParts & 1) != 0) {
                 const bool want = live && box_hit(f, o, inv);
                 cnt.box_tests += (uint32_t)__popcll(__ballot(live));
-                mesh_bvh_pairs(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0, want, o, d, inv, h, i,
-                               ob.order, stack - lane, W, lane, cnt, S.stack_cap);
+                mesh_bvh_pairs<RT_MESH_WIDE != 0>(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0,
+                                                  want, o, d, inv, h, i, ob.order, stack - lane, W, lane, cnt,
+                                                  S.stack_cap);
             }
         } else if ((kMed || (kBvh && kSph)) && ob.type == kObjMedium) {
             // (the general linear-scan kernel never sees a medium: launch_render sends scenes with
@@ -2163,8 +2217,26 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
     return hipGetLastError();
 }
 
-// A persistent grid fills the resident waves: waves per SIMD x 4 SIMDs / 4-wave blocks per CU.
-int queue_blocks(int n_cu, int waves_per_simd) { return n_cu * waves_per_simd; }
+// A persistent grid fills the resident waves: waves per SIMD x 4 SIMDs / 4-wave blocks per CU,
+// capped by what fits the CU's 160 KB of LDS (the variant's static tables + the launch's
+// traversal stacks): blocks beyond it would only start once others retire, after the queue ran dry.
+int queue_blocks(int n_cu, uint32_t variant, const RenderLaunch& L) {
+    const int waves = variant_waves(variant);
+    size_t lds = 0;
+    switch (variant) {
+        case RT_VARIANT_PATHTRACE_QUEUE: case RT_VARIANT_PATHTRACE_STATIC:
+            lds = (size_t)kWavesPerBlock * 64 * (8 + 4 + 4 * 4) + stack_bytes(L);
+            break;
+        case RT_VARIANT_SCAN_QUEUE: case RT_VARIANT_SCAN_STATIC: case RT_VARIANT_SCAN_MEDIA_QUEUE:
+        case RT_VARIANT_SCAN_MEDIA_STATIC: case RT_VARIANT_SCAN_SIMPLE_QUEUE: case RT_VARIANT_SCAN_SIMPLE_STATIC:
+            lds = (size_t)kWavesPerBlock * (sizeof(WaveLds) + sizeof(CamSlots));
+            break;
+        default:
+            lds = (size_t)kWavesPerBlock * sizeof(WaveLds) + stack_bytes(L);
+    }
+    const int fit = (int)((size_t)160 * 1024 / (lds ? lds : 1));
+    return n_cu * std::max(1, std::min(waves, fit));
+}
 
 // The instantiation a launch runs (rtmi.h RT_VARIANT_*). This is the only place that maps
 // scene content + schedule to a kernel: launch_render / launch_pathtrace dispatch on the id,
@@ -2235,7 +2307,7 @@ uint32_t kernel_build_flags() {
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
-    RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32
+    RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_MESH_WIDE != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;
