@@ -151,6 +151,7 @@ void rt_destroy(rt_ctx* c) {
         (void)hipFree(c->d_u8);
         (void)hipFree(c->d_queue);
         (void)hipFree(c->d_partial);
+        (void)hipFree(c->d_stack_spill);
         (void)hipFree(c->d_stage);
         (void)hipFree(c->d_frame);
         rtc::destroy_multi(c);
@@ -711,6 +712,8 @@ rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& 
     const int depth = p->integrator == RT_INTEGRATOR_PATHTRACE ? std::max(c->pt_bvh.max_depth, c->pt_pair_depth)
                                                                 : c->scene.bvh_max_depth;
     L.stack_depth = depth > 0 ? depth : 1;
+    L.stack_lds = L.stack_depth;  // rtc::launch may move the wide traversal's deepest entries out of LDS
+    L.stack_spill = nullptr;
     L.pt_scale = c->pt_scale;
     L.pt_root_ref = c->pt_root_ref;
     return RT_OK;
@@ -749,8 +752,28 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
             }
         }
         if (have) {
-            L.queue = rt::queue_blocks(
-                c->n_cu, rt::select_variant(pathtrace, true, bvh, c->has_media, c->full_scan, c->bvh_parts), L);
+            const uint32_t qv = rt::select_variant(pathtrace, true, bvh, c->has_media, c->full_scan, c->bvh_parts);
+            // The 4-wide mesh traversal may hold more stack entries than the variant's occupancy leaves
+            // room for in the CU's LDS (bunny: 27 per lane, 22 fit at 5 waves/SIMD). Its deepest
+            // entries, which few lanes ever reach, then live in a per-wave HBM area instead of
+            // lowering the occupancy for every lane; the other traversals stay in LDS.
+            if (RT_WIDE_SPLIT && !pathtrace && c->scene.wide_bound > 0) {
+                const int lds = std::max(std::max(std::min(L.stack_depth, rt::stack_lds_fit(qv)), c->scene.group_bound), 1);
+                if (lds < L.stack_depth) {
+                    L.stack_lds = lds;
+                    const size_t sb = (size_t)rt::queue_blocks(c->n_cu, qv, L) * 4 * (size_t)(L.stack_depth - lds) * 64 *
+                                      sizeof(uint32_t);
+                    if (sb > c->d_stack_spill_bytes) {
+                        (void)hipFree(c->d_stack_spill);
+                        c->d_stack_spill = nullptr;
+                        c->d_stack_spill_bytes = 0;
+                        RT_HIP(c, hipMalloc((void**)&c->d_stack_spill, sb));
+                        c->d_stack_spill_bytes = sb;
+                    }
+                    L.stack_spill = c->d_stack_spill;
+                }
+            }
+            L.queue = rt::queue_blocks(c->n_cu, qv, L);
             L.n_items = (uint32_t)items;
             L.n_pix = (uint32_t)(items >> L.sp_log2);
             // refill threshold (idle lanes a wave collects before one dequeue): 4 for long

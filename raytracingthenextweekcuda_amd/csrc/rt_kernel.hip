@@ -295,6 +295,17 @@ __device__ __forceinline__ int lane_rank(uint64_t mask) {
                                           __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// The megakernels' launch parameters (their FIRST argument: kernarg offset 0) behind an
+// opaque pointer. Each loop trip re-reads the fields it uses with scalar loads at their
+// use, instead of the compiler holding ~40 of them in SGPRs across the persistent loop
+// (SGPRs are the scarce resource: their spills take VGPR lanes, whose spills go to scratch).
+__device__ __forceinline__ const RenderLaunch& launch_args() {
+    const __attribute__((address_space(4))) char* p =
+        (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *reinterpret_cast<const RenderLaunch*>((const char*)p);
+}
+
 // The batched mesh traversal over child-pair records (rt_scene.cpp build_mesh_pairs). A lane
 // holds one reference word instead of a node: a pair index, whose 64 B record carries both
 // children's boxes and references, or a leaf reference (first triangle, count). An inner
@@ -313,7 +324,9 @@ __device__ __forceinline__ int lane_rank(uint64_t mask) {
 // aligned 128 B load and four box tests; the hit children are sorted by entry distance, the
 // nearest becomes the lane's reference and the others are pushed farthest first, so the next
 // nearest is popped first. Half the dependent loads per ray of the child-pair records; the
-// stack bound is the builder's max over paths of sum (children - 1).
+// stack bound is the builder's max over paths of sum (children - 1). Its entries at and above
+// L.stack_lds (the deepest, which few lanes reach) live in the wave's L.stack_spill area in HBM
+// instead of LDS (rt_capi.cpp launch); only LDS entries are stolen.
 template <bool kWide>
 __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
                                                const uint32_t* __restrict__ tri_orig,
@@ -330,6 +343,23 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
     uint32_t cur = root;  // pair index or leaf reference
     bool has = want;
     int sp = 0, bot = 0;            // pending references: wstack[k * 64 + lane], bot <= k < sp
+    // kWide: entries k >= L.stack_lds in the wave's HBM spill area. Nothing about it is held
+    // across the loop: the launch fields are scalar loads at the use, the wave's slot is scalar.
+    auto spill_at = [&](int k) -> uint32_t* {
+        const RenderLaunch& LA = launch_args();
+        const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+        return LA.stack_spill +
+               ((size_t)w * (size_t)(LA.stack_depth - LA.stack_lds) + (size_t)(k - LA.stack_lds)) * 64 + lane;
+    };
+    auto in_lds = [&](int k) { return !kWide || k < launch_args().stack_lds; };
+    auto put = [&](int k, uint32_t v) {
+        if (in_lds(k)) wstack[k * 64 + lane] = v;
+        else *spill_at(k) = v;
+    };
+    auto get = [&](int k) -> uint32_t {
+        if (in_lds(k)) return wstack[k * 64 + lane];
+        return *spill_at(k);
+    };
     uint32_t qtail = 0, qdone = 0;  // wave-uniform positions in the pair queue W.slot (256 entries)
     constexpr uint32_t kQ = (uint32_t)kMaxRun * 64u;
     static_assert(kQ >= 256, "the pair queue holds 63 + 3 x 64 pairs");
@@ -355,7 +385,7 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
         if (__ballot(has || sp > bot) == 0) break;
         // steal: pair the r-th idle lane with the r-th lane that has a spare reference
         const bool idle = !has && sp == bot;
-        const bool spare = sp - bot >= (has ? 1 : 2);
+        const bool spare = sp - bot >= (has ? 1 : 2) && in_lds(bot);
         const uint64_t im = __ballot(idle), vm = __ballot(spare);
         if (im != 0 && vm != 0) {
             const int nv = __popcll(vm), ni = __popcll(im);
@@ -386,7 +416,7 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             __builtin_amdgcn_wave_barrier();
         }
         if (!has && sp > bot) {
-            cur = wstack[(--sp) * 64 + lane];
+            cur = get(--sp);
             has = true;
             // the ray's best so far over all lanes (NaN while none: fminf keeps ours)
             best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
@@ -433,9 +463,9 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
                 has = false;
                 sp = bot = 0;
             } else {
-                if (nh > 3) wstack[(sp++) * 64 + lane] = r3;
-                if (nh > 2) wstack[(sp++) * 64 + lane] = r2;
-                if (nh > 1) wstack[(sp++) * 64 + lane] = r1;
+                if (nh > 3) put(sp++, r3);
+                if (nh > 2) put(sp++, r2);
+                if (nh > 1) put(sp++, r1);
                 cur = r0;
             }
         }
@@ -1226,17 +1256,6 @@ __device__ __forceinline__ void tail_steal(const RenderLaunch& L, WaveLds& W, in
     __builtin_amdgcn_wave_barrier();
 }
 
-// The megakernels' launch parameters (their FIRST argument: kernarg offset 0) behind an
-// opaque pointer. Each loop trip re-reads the fields it uses with scalar loads at their
-// use, instead of the compiler holding ~40 of them in SGPRs across the persistent loop
-// (SGPRs are the scarce resource: their spills take VGPR lanes, whose spills go to scratch).
-__device__ __forceinline__ const RenderLaunch& launch_args() {
-    const __attribute__((address_space(4))) char* p =
-        (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(p));
-    return *reinterpret_cast<const RenderLaunch*>((const char*)p);
-}
-
 __device__ __forceinline__ int global_row_of(const RenderLaunch& L, int lr) {
     const int lb = (int)udiv((uint32_t)lr, L.row_block_div);
     return (lb * L.row_world + L.row_rank) * L.row_block + (lr - lb * L.row_block);
@@ -1267,7 +1286,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         W.grp_s[lane] = 0;
         W.grp_m[lane] = 0;
     }
-    uint32_t* stack = kBvh ? dyn_stacks + (size_t)wave * L.stack_depth * 64 + lane : nullptr;
+    uint32_t* stack = kBvh ? dyn_stacks + (size_t)wave * L.stack_lds * 64 + lane : nullptr;
 
     // Lane layout: SP = lanes_per_pixel adjacent lanes share one pixel and split
     // its samples (sub-lane c takes samples c, c+SP, c+2SP, ...). A wave covers
@@ -1638,7 +1657,7 @@ __device__ __forceinline__ bool pt_box(const CFNode& n, v3 o, v3 d, float& tnear
 struct PtRay {
     v3 o, d;
     v3 inv;        // v_rcp_f32(d) per axis (1 ulp)
-    v3 pad_t;      // eps * |inv|: widens each slab by eps for the pruning bound
+    float eps;     // pruning margin: eps * |inv| widens each slab (computed at each use: no VGPRs held)
     bool exact;    // a direction component is tiny but non-zero: always divide
 };
 
@@ -1654,7 +1673,8 @@ __device__ __forceinline__ bool pt_box_decide(const CFNode& n, const PtRay& r, f
     float tn = -3.40282347e+38f, tf = 3.40282347e+38f, tw = -3.40282347e+38f;
     bool miss = false;
     const float oo[3] = {r.o.x, r.o.y, r.o.z}, dd[3] = {r.d.x, r.d.y, r.d.z};
-    const float iv[3] = {r.inv.x, r.inv.y, r.inv.z}, pt[3] = {r.pad_t.x, r.pad_t.y, r.pad_t.z};
+    const float iv[3] = {r.inv.x, r.inv.y, r.inv.z};
+    const float pt[3] = {r.eps * fabsf(r.inv.x), r.eps * fabsf(r.inv.y), r.eps * fabsf(r.inv.z)};
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         const float lo = n.bottom[c], hi = n.top[c];
@@ -1684,7 +1704,8 @@ __device__ __forceinline__ void pt_box_bounds(const CFNode& n, const PtRay& r, f
                                               float& order) {
     float tn = -3.40282347e+38f, tw = -3.40282347e+38f;
     const float oo[3] = {r.o.x, r.o.y, r.o.z}, dd[3] = {r.d.x, r.d.y, r.d.z};
-    const float iv[3] = {r.inv.x, r.inv.y, r.inv.z}, pt[3] = {r.pad_t.x, r.pad_t.y, r.pad_t.z};
+    const float iv[3] = {r.inv.x, r.inv.y, r.inv.z};
+    const float pt[3] = {r.eps * fabsf(r.inv.x), r.eps * fabsf(r.inv.y), r.eps * fabsf(r.inv.z)};
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         if (dd[c] != 0.0f && !r.exact) {
@@ -1732,9 +1753,10 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
     key_reset(keys[lane]);
     int owner = lane;
     PtRay r = ray;
-    float len_d = len_in, eps = eps_in;
+    float len_d = len_in;
+    (void)eps_in;  // = ray.eps
     float bhz = 3.40282347e+38f, bdist = 3.40282347e+38f;  // the current ray's best (pruning bound)
-    auto pruned = [&](float tw) { return tw > 0.0f && tw * len_d > bdist * 1.0001f + eps; };
+    auto pruned = [&](float tw) { return tw > 0.0f && tw * len_d > bdist * 1.0001f + r.eps; };
     auto refresh = [&]() {  // the ray's best over all lanes (NaN while none)
         const float g = __uint_as_float((uint32_t)(keys[owner] >> 32));
         if (g < bhz) {
@@ -1817,8 +1839,7 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
             take(r.o.x); take(r.o.y); take(r.o.z);
             take(r.d.x); take(r.d.y); take(r.d.z);
             take(r.inv.x); take(r.inv.y); take(r.inv.z);
-            take(r.pad_t.x); take(r.pad_t.y); take(r.pad_t.z);
-            take(len_d); take(eps); take(bhz); take(bdist);
+            take(len_d); take(r.eps); take(bhz); take(bdist);
             if (thief) {
                 const uint32_t entry = wstack[vb * 64 + vic];
                 refresh();
@@ -1922,6 +1943,9 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
 
 }  // namespace
 
+#ifndef RT_PT_GSUM
+#define RT_PT_GSUM 1  // pathTrace work-queue launches fold a sub-stream's sum in its partial-sum slot (0: registers)
+#endif
 template <bool kQueue>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES))) void pathtrace_kernel(
     RenderLaunch L, const KTri* __restrict__ ktris, const CFNode* __restrict__ nodes,
@@ -1933,7 +1957,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
     __shared__ uint32_t pt_queue[kWavesPerBlock][256];          // deferred leaf pairs
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    uint32_t* stack = dyn_stacks + (size_t)wave * L.stack_depth * 64 + lane;
+    uint32_t* stack = dyn_stacks + (size_t)wave * L.stack_lds * 64 + lane;
 
     const int SP = L.lanes_per_pixel;
     int c = lane & (SP - 1);
@@ -1971,10 +1995,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
                 if (!queue_item(L, it, ic, ipx, ilr)) return;  // past the frame edge: ask again
                 item = it;
                 s = ic;
-                sum = v3{0.0f, 0.0f, 0.0f};
                 alive = s < L.spp;
+#if RT_PT_GSUM
+                // the item's sample sum lives in its partial-sum slot: zero it (a sub-stream with no
+                // samples, S > spp, keeps the zero)
+                const float z = fresh_f32(0.0f);  // materialised here, not kept live (and spilled)
+                store_partial(L, item, v3{z, z, z});
+#else
+                sum = v3{0.0f, 0.0f, 0.0f};
                 // a sub-stream with no samples (S > spp) still owns its partial-sum slot
                 if (!alive) store_partial(L, item, sum);
+#endif
                 need_cam = true;
             }, []() {});
         }
@@ -2012,7 +2043,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
             // outside its triangle's box (rounding at the scale of the
             // coordinates involved), with a 10x margin.
             const float eps = 1e-5f * (1.0f + fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) + L.pt_scale);
-            r.pad_t = v3{eps * fabsf(r.inv.x), eps * fabsf(r.inv.y), eps * fabsf(r.inv.z)};
+            r.eps = eps;
             pt_traverse_coop_batched(ktris, nodes, tri_list, stack - lane, pt_keys[wave], pt_vlist[wave], pt_queue[wave],
                                      lane, alive, r, avoid, fsqrt(dot(d, d)), eps, best, cnt, L.stack_depth,
                                      L.pt_root_ref);
@@ -2155,12 +2186,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
             }
         }
         if (done) {
+#if RT_PT_GSUM
+            if (kQueue) {  // ((0 + c0) + c1) + ...: the register fold's order, through the slot
+                const float* q = L.partial + ((size_t)(item & (uint32_t)(SP - 1)) * L.n_pix + (item >> L.sp_log2)) * 3;
+                store_partial(L, item, add(v3{q[0], q[1], q[2]}, contrib));
+            } else {
+                sum = add(sum, contrib);
+            }
+#else
             sum = add(sum, contrib);
+#endif
             need_cam = true;
             s += SP;
             if (s >= L.spp) {
                 alive = false;
+#if !RT_PT_GSUM
                 if (kQueue) store_partial(L, item, sum);
+#endif
             }
         }
     }
@@ -2190,7 +2232,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
 
 // Dynamic LDS of a traversal kernel: the per-lane stacks of its 4 waves.
 static size_t stack_bytes(const RenderLaunch& L) {
-    return (size_t)kWavesPerBlock * (size_t)(L.stack_depth > 0 ? L.stack_depth : 1) * 64 * sizeof(uint32_t);
+    return (size_t)kWavesPerBlock * (size_t)(L.stack_lds > 0 ? L.stack_lds : 1) * 64 * sizeof(uint32_t);
 }
 
 hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const RenderLaunch& L,
@@ -2220,6 +2262,13 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
 // A persistent grid fills the resident waves: waves per SIMD x 4 SIMDs / 4-wave blocks per CU,
 // capped by what fits the CU's 160 KB of LDS (the variant's static tables + the launch's
 // traversal stacks): blocks beyond it would only start once others retire, after the queue ran dry.
+int stack_lds_fit(uint32_t variant) {
+    const int waves = variant_waves(variant);
+    const size_t budget = (size_t)160 * 1024 / (size_t)(waves > 0 ? waves : 1);  // per 4-wave block
+    const size_t fixed = (size_t)kWavesPerBlock * sizeof(WaveLds);
+    return budget > fixed ? (int)((budget - fixed) / ((size_t)kWavesPerBlock * 64 * sizeof(uint32_t))) : 1;
+}
+
 int queue_blocks(int n_cu, uint32_t variant, const RenderLaunch& L) {
     const int waves = variant_waves(variant);
     size_t lds = 0;
@@ -2307,7 +2356,7 @@ uint32_t kernel_build_flags() {
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
-    RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_MESH_WIDE != 1
+    RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_MESH_WIDE != 1 || RT_WIDE_SPLIT != 1 || RT_PT_GSUM != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;

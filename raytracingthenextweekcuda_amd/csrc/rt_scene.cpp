@@ -561,6 +561,7 @@ std::string HostScene::build_mesh_pairs() {
     if (nodes.size() & 1u) nodes.push_back(BvhNode{});
     // the LDS stacks are sized by what the traversals below may push (not the binary depth)
     bvh_max_depth = 0;
+    wide_bound = group_bound = 0;
     for (int k = 0; k < n_scan; ++k) {
         ObjRec& r = objs[k];
         if (!tree(r)) continue;
@@ -572,6 +573,7 @@ std::string HostScene::build_mesh_pairs() {
                 return "wide BVH stack bound " + std::to_string(wb.max_push) + " exceeds the traversal stack (" +
                        std::to_string(kWideStackMax) + ")";
             bvh_max_depth = std::max(bvh_max_depth, std::max(wb.max_push, 1));
+            wide_bound = std::max(wide_bound, std::max(wb.max_push, 1));
             memcpy(&r.f[8], &root, 4);
             continue;
         }
@@ -583,6 +585,7 @@ std::string HostScene::build_mesh_pairs() {
             return "BVH pair depth " + std::to_string(pb.max_pairs) + " exceeds the traversal stack (" +
                    std::to_string(kBvhStackDepth) + ")";
         bvh_max_depth = std::max(bvh_max_depth, pb.max_pairs);
+        group_bound = std::max(group_bound, pb.max_pairs);
         memcpy(&r.f[8], &root, 4);
     }
     return "";

@@ -100,6 +100,9 @@ struct alignas(16) WideNode {
     uint32_t n, pad[3];
 };
 static_assert(sizeof(WideNode) == 128, "WideNode must be 128 B");
+#ifndef RT_WIDE_SPLIT
+#define RT_WIDE_SPLIT 1  // the wide traversal's deepest stack entries in HBM when LDS would lower occupancy (0: A/B)
+#endif
 #ifndef RT_MESH_WIDE
 #define RT_MESH_WIDE 1  // rayColor mesh BVHs as 4-wide nodes (0: child-pair records; A/B)
 #endif
@@ -167,6 +170,8 @@ struct HostScene {
     std::vector<BvhNode> nodes;
     std::vector<uint32_t> tri_orig;  // 2 per triangle: (mesh-local index, inverse map), see flatten()
     int bvh_max_depth = 0;
+    int wide_bound = 0;   // stack entries the 4-wide mesh traversals may push (0: none)
+    int group_bound = 0;  // ... the sphere-group and child-pair mesh traversals (LDS-resident)
 
     // BVH builder (rt_set_bvh_builder): host Recurse, or its GPU restatement on
     // `bvh_device` (byte-identical; falls back to the host when it declines).
