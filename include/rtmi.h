@@ -82,10 +82,11 @@ typedef struct rt_render_params {
                                after many launches, no per-launch host sync).
                                RT_RENDER_FRAMES_IN_FLIGHT: the caller keeps three or more
                                launches in flight on other contexts/streams (frame overlap);
-                               the auto layout (lanes_per_pixel = 0) of a linear-scan rayColor
-                               work-queue launch then takes at most 16 sub-streams per pixel
-                               (items of more samples, whose longer tail the next frames fill).
-                               The image is that of lanes_per_pixel = the reported value. */
+                               a linear-scan rayColor work-queue launch then hands out work
+                               items of several sub-streams (at most 16 items per pixel:
+                               longer items, whose longer tail the next frames fill). The
+                               sub-streams, and so the image, are those of lanes_per_pixel:
+                               the flag never changes a pixel. */
     /* Column window of every owned row: columns [col_begin, col_begin + col_count);
      * col_count = 0 = the whole width. Output rows are col_count wide. The pixels are
      * those of the full frame (camera and RNG keyed by the frame position). */
@@ -145,7 +146,8 @@ typedef struct rt_render_stats {
     uint32_t launches;      /* launches summed in these counters (RT_RENDER_KEEP_COUNTERS chains; else 1) */
     double kernel_ms_sum;   /* render-kernel time summed over those launches (one event pair each) */
     uint32_t variant;       /* RT_VARIANT_* of the last launch */
-    uint32_t reserved;
+    uint32_t substreams_per_item; /* sub-streams a work item runs in sequence (work queue; 1 on the static
+                                     grid): the schedule's item length, which does not change the image */
 } rt_render_stats;
 
 #define RT_GATHER_RCCL 1 /* one ncclGather over the contexts' devices */

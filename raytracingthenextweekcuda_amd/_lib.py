@@ -91,7 +91,7 @@ class RenderStats(C.Structure):
         ("group_sphere_tests", C.c_uint64), ("group_moving_sphere_tests", C.c_uint64),
         ("debug", C.c_uint64 * 8),
         ("refill", C.c_uint32), ("queue_blocks", C.c_uint32), ("gather", C.c_uint32), ("launches", C.c_uint32),
-        ("kernel_ms_sum", C.c_double), ("variant", C.c_uint32), ("reserved", C.c_uint32),
+        ("kernel_ms_sum", C.c_double), ("variant", C.c_uint32), ("substreams_per_item", C.c_uint32),
     ]
 
 

@@ -688,18 +688,22 @@ rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& 
         return fail(c, RT_ERR_INVALID, "lanes_per_pixel must be 0 (auto) or a power of two <= 128 (64 static)");
     const bool bvh = p->integrator == RT_INTEGRATOR_PATHTRACE || !c->scene.nodes.empty();
     rt::choose_layout(L, s, queue, bvh);
-    // Frames in flight: with three launches overlapped, CornellBox1 runs faster at S = 16 than at
-    // the auto S = 32 (N = 1 5.55 vs 5.68 ms/frame, N = 8 shard 0.816 vs 0.834) and slower alone
-    // (5.85 vs 5.83): larger items cut the dequeues, and the next frames fill their longer tail
-    // (profiles/r03/lanes/). BVH launches keep their S (Suzanne, materialball: slower).
-    if (s == 0 && queue && !bvh && (p->flags & RT_RENDER_FRAMES_IN_FLIGHT) && L.lanes_per_pixel > 16)
-        rt::choose_layout(L, 16, queue, bvh);
+    // Work items of several sub-streams (the image is that of S regardless). Frames in flight: with
+    // three launches overlapped, CornellBox1 ran faster with items of 8 samples (round 3, as S = 16:
+    // N = 1 5.55 vs 5.68 ms/frame, N = 8 shard 0.816 vs 0.834) and slower alone (5.85 vs 5.83):
+    // longer items cut the dequeues, and the next frames fill their longer tail (DESIGN §7,
+    // profiles/r03/lanes/). Here the same item length comes from groups of S' = 16 sub-streams of
+    // the auto S, so the flag no longer changes the image. BVH launches keep one sub-stream per item.
+    L.grp_log2 = 0;
+    if (queue && !bvh && (p->flags & RT_RENDER_FRAMES_IN_FLIGHT))
+        while ((L.lanes_per_pixel >> L.grp_log2) > 16) ++L.grp_log2;
     L.accumulate = 0;
     L.accum_scale = 0.0f;
     L.u8 = nullptr;
     L.queue = 0;
     L.tiles_x = (L.cols + 7) / 8;
     L.n_items = 0;
+    L.n_qitems = 0;
     L.n_pix = 0;
     L.tiles_x_div = rt::make_udiv((uint32_t)L.tiles_x);
     L.row_block_div = rt::make_udiv((uint32_t)L.row_block);
@@ -775,6 +779,7 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
             }
             L.queue = rt::queue_blocks(c->n_cu, qv, L);
             L.n_items = (uint32_t)items;
+            L.n_qitems = L.n_items >> L.grp_log2;
             L.n_pix = (uint32_t)(items >> L.sp_log2);
             // refill threshold (idle lanes a wave collects before one dequeue): 4 for long
             // items (>= 16 samples each: waiting for 8 idle lanes wastes lane time), else 8
@@ -782,13 +787,14 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
             // media (128) 1798 / 1846 (profiles/r01/ab_refill*.log); N = 8 shards (4 samples/item,
             // profiles/r02/refill_shards.log) CB1 1.205 / 1.207, spheres 10.86 / 10.81, Suzanne
             // 0.876 / 0.860 - round 1's extra "short shard -> 4" rule is not supported there.
-            const int per_item = (L.spp + L.lanes_per_pixel - 1) / L.lanes_per_pixel;
+            const int per_item = ((L.spp + L.lanes_per_pixel - 1) / L.lanes_per_pixel) << L.grp_log2;
             L.refill = per_item >= 16 ? 4 : 8;
             L.partial = c->d_partial;
             RT_HIP(c, hipMemsetAsync(c->d_queue, 0, rt::kQueueHeadWords * sizeof(uint32_t), st));
         }
     }
     const uint32_t variant = rt::select_variant(pathtrace, L.queue != 0, bvh, c->has_media, c->full_scan, c->bvh_parts);
+    if (L.queue == 0 || pathtrace) L.grp_log2 = 0;  // the static grid and pathTrace: one sub-stream per item
     if (L.queue == 0 && L.lanes_per_pixel > 64)  // the static grid keeps a pixel's sub-streams in one wave
         return fail(c, RT_ERR_INVALID, "lanes_per_pixel > 64 needs the work queue, which this frame does not fit");
     const bool keep = (p->flags & RT_RENDER_KEEP_COUNTERS) != 0;
@@ -844,6 +850,7 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
     c->last.refill = L.queue ? (uint32_t)L.refill : 0u;
     c->last.queue_blocks = (uint32_t)L.queue;
     c->last.variant = variant;
+    c->last.substreams_per_item = L.queue ? 1u << L.grp_log2 : 1u;
     c->stats_pending = true;
     return RT_OK;
 }

@@ -70,6 +70,11 @@ struct RenderLaunch {
     int32_t queue;
     int32_t tiles_x;
     uint32_t n_items;
+    // A work item is a group of 1 << grp_log2 sub-streams of one pixel, c, c + S', c + 2S', ...
+    // with S' = S >> grp_log2: the lane runs them one after the other and stores each one's
+    // partial sum. The image depends on S only; the group size is the schedule's item length.
+    int32_t grp_log2;
+    uint32_t n_qitems;        // n_items >> grp_log2: what the queue hands out
     uint32_t n_pix;           // n_items / S: the pixels of the launch (one partial-sum plane)
     UDiv tiles_x_div;         // tile -> (tile row, tile column)
     UDiv row_block_div;       // local row -> local row block

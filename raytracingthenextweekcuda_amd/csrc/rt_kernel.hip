@@ -1098,17 +1098,34 @@ constexpr int kQueueStride = 32;  // u32 words between heads
 #define RT_REFILL_AT(L) ((L).refill)
 #endif
 
-// Wave-wide dequeue from shard `sh`: every lane in `need` gets an item index,
-// or ~0u if the shard ran out (one atomic per wave).
+// Wave-wide dequeue from shard `sh`: every lane in `need` gets the item index of its group's
+// first sub-stream, or ~0u if the shard ran out (one atomic per wave).
 __device__ __forceinline__ uint32_t queue_take(const RenderLaunch& L, int sh, uint64_t need, int lane) {
-    const uint32_t lo = (uint32_t)(((uint64_t)L.n_items * (uint64_t)sh) / kQueueShards);
-    const uint32_t hi = (uint32_t)(((uint64_t)L.n_items * (uint64_t)(sh + 1)) / kQueueShards);
+    const uint32_t lo = (uint32_t)(((uint64_t)L.n_qitems * (uint64_t)sh) / kQueueShards);
+    const uint32_t hi = (uint32_t)(((uint64_t)L.n_qitems * (uint64_t)(sh + 1)) / kQueueShards);
     const int first = __builtin_ctzll(need);
     uint32_t base = 0;
     if (lane == first) base = atomicAdd(L.q_counter + sh * kQueueStride, (unsigned)__popcll(need));
     base = (uint32_t)__shfl((int)base, first, 64);
     const uint32_t it = lo + base + (uint32_t)lane_rank(need);
-    return it < hi ? it : ~0u;
+    if (it >= hi) return ~0u;
+    // group it -> (pixel, first sub-stream c < S'): item = pixel << sp_log2 | c
+    const uint32_t gs = (uint32_t)(L.sp_log2 - L.grp_log2);
+    return ((it >> gs) << L.sp_log2) | (it & ((1u << gs) - 1u));
+}
+
+// The next sub-stream of an item's group after c (S' = S >> grp_log2 apart), or -1.
+__device__ __forceinline__ int next_member(const RenderLaunch& L, int c, int SP) {
+    const int cn = c + (SP >> L.grp_log2);
+    return cn < SP ? cn : -1;
+}
+
+// Partial sums of the group members from c on that have no samples (c >= spp, possible when
+// S > spp): their slots hold zero.
+__device__ __forceinline__ void zero_members(const RenderLaunch& L, uint32_t item, int SP) {
+    const float z = fresh_f32(0.0f);
+    for (int c = (int)(item & (uint32_t)(SP - 1)); c >= 0; c = next_member(L, c, SP))
+        store_partial(L, (item & ~(uint32_t)(SP - 1)) | (uint32_t)c, v3{z, z, z});
 }
 
 // Refill of a wave's idle lanes (wave-uniform: called by all 64 lanes). A lane
@@ -1153,7 +1170,7 @@ __global__ __launch_bounds__(256) void combine_kernel(RenderLaunch L, float* __r
 #define RT_CAM_BATCH 32  // lanes lacking a prepared next sample that start a camera pass on their own
 #endif
 // Camera slots: bit 31 of a lane's work-queue item is set while its slot holds the lane's next
-// sample (s if need_cam, else s + SP): a flag in a VGPR already live, not a lane mask in SGPRs (the
+// sample (s if need_cam, else s + SP or the first sample of its group's next member): a flag in a VGPR already live, not a lane mask in SGPRs (the
 // megakernels' scarce registers). Item indices stay below 2^31 (rt_capi.cpp caps them).
 constexpr uint32_t kPrepared = 0x80000000u;
 
@@ -1165,7 +1182,9 @@ __device__ __forceinline__ int sub_end(int spp, int c, int SP, int sp_log2) {
 // A sample's path finished with radiance `contrib`. Owners fold it into the
 // item's sum in sample order (((p0 + p1) + p2) + ...); a thief holds it in `thr`
 // until its owner folds it in (tail_steal).
-__device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, int SP, uint32_t item, int own_end,
+// `item` may carry kPrepared; at the end of a group member's samples the owner stores its partial
+// sum and goes on with the next member (tail stealing happens only in the last member).
+__device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, int SP, uint32_t& item, int& own_end,
                                             int& s, v3& sum, v3& thr, bool& alive, bool& need_cam, int towner,
                                             bool& held, bool& waiting, uint32_t tl_pack) {
     need_cam = true;
@@ -1178,10 +1197,24 @@ __device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, i
     sum = add(sum, contrib);
     s += SP;
     if (s >= own_end) {
+        const int cn = L.queue ? next_member(L, (int)(item & (uint32_t)(SP - 1)), SP) : -1;
+        if (cn >= 0) {
+            store_partial(L, item & ~kPrepared, sum);
+            item += (uint32_t)(SP >> L.grp_log2);  // kPrepared (bit 31) is kept: the slot may hold s = cn
+            s = cn;
+            own_end = sub_end(L.spp, cn, SP, L.sp_log2);
+            const float z = fresh_f32(0.0f);
+            sum = v3{z, z, z};
+            if (cn >= L.spp) {
+                zero_members(L, item & ~kPrepared, SP);
+                alive = false;
+            }
+            return;
+        }
         alive = false;
         if (L.queue) {
             if (tl_pack) waiting = true;  // its last samples were taken by other lanes
-            else store_partial(L, item, sum);
+            else store_partial(L, item & ~kPrepared, sum);
         }
     }
 }
@@ -1228,7 +1261,8 @@ __device__ __forceinline__ void tail_steal(const RenderLaunch& L, WaveLds& W, in
     // 2. pair the r-th idle lane with the r-th lane that has a spare (unstarted, not
     //    current) sample; items of at most 4 samples (one byte per position in tl_pack)
     const bool idle = !alive && !waiting && !held;
-    const bool spare = alive && towner < 0 && s + SP < own_end && sub_end(L.spp, c, SP, L.sp_log2) - c <= 4 * SP;
+    const bool spare = alive && towner < 0 && s + SP < own_end && sub_end(L.spp, c, SP, L.sp_log2) - c <= 4 * SP &&
+                       next_member(L, c, SP) < 0;  // the group's last member
     const uint64_t im = __ballot(idle), vm = __ballot(spare);
     if (im == 0 || vm == 0) return;
     const int nv = __popcll(vm), ni = __popcll(im);
@@ -1342,8 +1376,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                 sum = v3{z, z, z};
                 alive = s < L.spp;
                 own_end = sub_end(L.spp, ic, SP, L.sp_log2);
-                // a sub-stream with no samples (S > spp) still owns its partial-sum slot
-                if (!alive) store_partial(L, item, sum);
+                // sub-streams with no samples (S > spp) still own their partial-sum slots
+                if (!alive) zero_members(L, item, SP);
                 need_cam = true;
             }, [&]() {
                 // the wave-uniform event counts are 32-bit: at a dequeue, flush them to the 64-bit
@@ -1373,7 +1407,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             // same whichever pass computes them (the stream is keyed by pixel and sample).
             CamSlots& C = cslots[wave];
             const bool now = alive && need_cam && !(item & kPrepared);
-            const bool nxt = alive && !need_cam && !(item & kPrepared) && towner < 0 && s + SP < own_end;
+            // the lane's next sample: the member's next one, or the first of the group's next member
+            int ns = s + SP;
+            if (ns >= own_end) {
+                const int cn = towner < 0 ? next_member(L, (int)(item & (uint32_t)(SP - 1)), SP) : -1;
+                ns = cn >= 0 && cn < L.spp ? cn : -1;
+            }
+            const bool nxt = alive && !need_cam && !(item & kPrepared) && towner < 0 && ns >= 0;
             if (__ballot(now) != 0 || __popcll(__ballot(nxt)) >= RT_CAM_BATCH) {
                 if (now || nxt) {
                     if (kQueue) {
@@ -1383,7 +1423,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                         pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
                     }
                     Rng r2{1u, 0u, 0u, 0u};
-                    const Ray cr = camera_sample(cam, L, r2, pixel, px, y, now ? s : s + SP, (float)(L.width - 1),
+                    const Ray cr = camera_sample(cam, L, r2, pixel, px, y, now ? s : ns, (float)(L.width - 1),
                                                  (float)(L.height - 1));
                     C.a[lane] = float4{cr.o.x, cr.o.y, cr.o.z, cr.d.x};
                     C.b[lane] = float4{cr.d.y, cr.d.z, cr.time, __uint_as_float(r2.s0)};
@@ -1402,7 +1442,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                 thr = v3{1.0f, 1.0f, 1.0f};
                 depth = 0;
                 if (L.max_depth <= 0)  // rayColor with BOUNCES = 0 returns black
-                    sample_done(L, v3{0.0f, 0.0f, 0.0f}, SP, item & ~kPrepared, own_end, s, sum, thr, alive, need_cam,
+                    sample_done(L, v3{0.0f, 0.0f, 0.0f}, SP, item, own_end, s, sum, thr, alive, need_cam,
                                 towner, held, waiting, tl_pack);
             }
         } else if (alive && need_cam) {
@@ -1417,7 +1457,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             depth = 0;
             need_cam = false;
             if (L.max_depth <= 0)  // rayColor with BOUNCES = 0 returns black
-                sample_done(L, v3{0.0f, 0.0f, 0.0f}, SP, item & ~kPrepared, own_end, s, sum, thr, alive, need_cam, towner,
+                sample_done(L, v3{0.0f, 0.0f, 0.0f}, SP, item, own_end, s, sum, thr, alive, need_cam, towner,
                             held, waiting, tl_pack);
         }
         const bool live = alive && !need_cam;
@@ -1540,7 +1580,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             done = true;
         }
         if (done)
-            sample_done(L, contrib, SP, item & ~kPrepared, own_end, s, sum, thr, alive, need_cam, towner, held, waiting,
+            sample_done(L, contrib, SP, item, own_end, s, sum, thr, alive, need_cam, towner, held, waiting,
                         tl_pack);
 #ifdef RT_STAMPS
         {
@@ -1997,14 +2037,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
                 s = ic;
                 alive = s < L.spp;
 #if RT_PT_GSUM
-                // the item's sample sum lives in its partial-sum slot: zero it (a sub-stream with no
-                // samples, S > spp, keeps the zero)
-                const float z = fresh_f32(0.0f);  // materialised here, not kept live (and spilled)
-                store_partial(L, item, v3{z, z, z});
+                // the group's sample sums live in their partial-sum slots: zero them (a sub-stream with
+                // no samples, S > spp, keeps the zero)
+                zero_members(L, item, SP);
 #else
                 sum = v3{0.0f, 0.0f, 0.0f};
-                // a sub-stream with no samples (S > spp) still owns its partial-sum slot
-                if (!alive) store_partial(L, item, sum);
+                // sub-streams with no samples (S > spp) still own their partial-sum slots
+                if (!alive) zero_members(L, item, SP);
 #endif
                 need_cam = true;
             }, []() {});
@@ -2198,7 +2237,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
 #endif
             need_cam = true;
             s += SP;
-            if (s >= L.spp) {
+            if (s >= L.spp) {  // (pathTrace launches run one sub-stream per work item: grp_log2 = 0)
                 alive = false;
 #if !RT_PT_GSUM
                 if (kQueue) store_partial(L, item, sum);

@@ -383,7 +383,7 @@ class Renderer:
     def stats(self) -> dict:
         s = RenderStats()
         self._check(self.L.rt_sync_stats(self.ctx, C.byref(s)))
-        d = {k: getattr(s, k) for k, _ in RenderStats._fields_ if k != "reserved"}
+        d = {k: getattr(s, k) for k, _ in RenderStats._fields_}
         d["debug"] = list(s.debug)
         d["variant_name"] = variant_name(s.variant)  # the kernel symbol, as rocprofv3 prints it
         return d

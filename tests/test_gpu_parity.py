@@ -223,23 +223,33 @@ def test_auto_lane_layout(rtmi):
 
 
 def test_frames_in_flight_layout(rtmi):
-    # RT_RENDER_FRAMES_IN_FLIGHT: the auto layout of linear-scan work-queue launches takes at
-    # most 16 sub-streams (rt_capi.cpp validate); the image is that of the reported S, and the
-    # hint leaves explicit layouts, small S and BVH launches alone
+    # RT_RENDER_FRAMES_IN_FLIGHT: linear-scan work-queue launches hand out items of several
+    # sub-streams (at most 16 items per pixel, rt_capi.cpp validate); the sub-streams, and so the
+    # image, stay those of lanes_per_pixel, byte for byte - with the flag or without, auto or explicit,
+    # and against the oracle (the full-size C2 case in test_full_size.py checks the bench's frame)
+    from oracle import oracle as orc
+
     with rtmi.Renderer(0) as r:
         rtmi.cornell_box1(r, 48, 32)
         img = r.render(48, 32, 64, 4, lanes_per_pixel=0, frames_in_flight=True)
-        assert r.stats()["lanes_per_pixel"] == 16
-        assert np.array_equal(img, r.render(48, 32, 64, 4, lanes_per_pixel=16))
-        assert r.stats()["lanes_per_pixel"] == 16
-        r.render(48, 32, 64, 4, lanes_per_pixel=32, frames_in_flight=True)
-        assert r.stats()["lanes_per_pixel"] == 32
+        st = r.stats()
+        assert st["lanes_per_pixel"] == 32 and st["substreams_per_item"] == 2
+        assert np.array_equal(img, r.render(48, 32, 64, 4, lanes_per_pixel=0))
+        assert r.stats()["substreams_per_item"] == 1
+        assert np.array_equal(img, r.render(48, 32, 64, 4, lanes_per_pixel=32, frames_in_flight=True))
+        sc = orc.yaml_scene(os.path.join(S.SCENES, "cornellbox1.yaml"), S.MODELS, 48, 32)
+        want, ost = sc.render(48, 32, 64, 4, lanes_per_pixel=32)
+        assert np.array_equal(img, want) and st["segments"] == ost["segments"]
+        # 128 sub-streams for 64 samples: the groups' second halves have no samples (zero partials)
+        img = r.render(48, 32, 64, 4, lanes_per_pixel=128, frames_in_flight=True)
+        assert r.stats()["substreams_per_item"] == 8
+        assert np.array_equal(img, r.render(48, 32, 64, 4, lanes_per_pixel=128))
         r.render(48, 32, 8, 4, lanes_per_pixel=0, frames_in_flight=True)
-        assert r.stats()["lanes_per_pixel"] == 8
+        assert r.stats()["lanes_per_pixel"] == 8 and r.stats()["substreams_per_item"] == 1
     with rtmi.Renderer(0) as r:
         rtmi.suzanne_cornell_box(r, 64, 64)
         r.render(64, 64, 32, 3, lanes_per_pixel=0, frames_in_flight=True)
-        assert r.stats()["lanes_per_pixel"] == 32
+        assert r.stats()["lanes_per_pixel"] == 32 and r.stats()["substreams_per_item"] == 1
 
 
 def test_auto_lane_layout_bvh(rtmi):
