@@ -151,7 +151,6 @@ void rt_destroy(rt_ctx* c) {
         (void)hipFree(c->d_u8);
         (void)hipFree(c->d_queue);
         (void)hipFree(c->d_partial);
-        (void)hipFree(c->d_stack_spill);
         (void)hipFree(c->d_stage);
         (void)hipFree(c->d_frame);
         rtc::destroy_multi(c);
@@ -695,8 +694,13 @@ rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& 
     // profiles/r03/lanes/). Here the same item length comes from groups of S' = 16 sub-streams of
     // the auto S, so the flag no longer changes the image. BVH launches keep one sub-stream per item.
     L.grp_log2 = 0;
-    if (queue && !bvh && (p->flags & RT_RENDER_FRAMES_IN_FLIGHT))
+#ifndef RT_FIF_GROUPS
+#define RT_FIF_GROUPS 1  // 0 (A/B only): frames in flight lower the auto S to 16 instead (round 3)
+#endif
+    if (RT_FIF_GROUPS && queue && !bvh && (p->flags & RT_RENDER_FRAMES_IN_FLIGHT))
         while ((L.lanes_per_pixel >> L.grp_log2) > 16) ++L.grp_log2;
+    if (!RT_FIF_GROUPS && s == 0 && queue && !bvh && (p->flags & RT_RENDER_FRAMES_IN_FLIGHT) && L.lanes_per_pixel > 16)
+        rt::choose_layout(L, 16, queue, bvh);
     L.accumulate = 0;
     L.accum_scale = 0.0f;
     L.u8 = nullptr;
@@ -716,8 +720,6 @@ rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& 
     const int depth = p->integrator == RT_INTEGRATOR_PATHTRACE ? std::max(c->pt_bvh.max_depth, c->pt_pair_depth)
                                                                 : c->scene.bvh_max_depth;
     L.stack_depth = depth > 0 ? depth : 1;
-    L.stack_lds = L.stack_depth;  // rtc::launch may move the wide traversal's deepest entries out of LDS
-    L.stack_spill = nullptr;
     L.pt_scale = c->pt_scale;
     L.pt_root_ref = c->pt_root_ref;
     return RT_OK;
@@ -757,26 +759,6 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
         }
         if (have) {
             const uint32_t qv = rt::select_variant(pathtrace, true, bvh, c->has_media, c->full_scan, c->bvh_parts);
-            // The 4-wide mesh traversal may hold more stack entries than the variant's occupancy leaves
-            // room for in the CU's LDS (bunny: 27 per lane, 22 fit at 5 waves/SIMD). Its deepest
-            // entries, which few lanes ever reach, then live in a per-wave HBM area instead of
-            // lowering the occupancy for every lane; the other traversals stay in LDS.
-            if (RT_WIDE_SPLIT && !pathtrace && c->scene.wide_bound > 0) {
-                const int lds = std::max(std::max(std::min(L.stack_depth, rt::stack_lds_fit(qv)), c->scene.group_bound), 1);
-                if (lds < L.stack_depth) {
-                    L.stack_lds = lds;
-                    const size_t sb = (size_t)rt::queue_blocks(c->n_cu, qv, L) * 4 * (size_t)(L.stack_depth - lds) * 64 *
-                                      sizeof(uint32_t);
-                    if (sb > c->d_stack_spill_bytes) {
-                        (void)hipFree(c->d_stack_spill);
-                        c->d_stack_spill = nullptr;
-                        c->d_stack_spill_bytes = 0;
-                        RT_HIP(c, hipMalloc((void**)&c->d_stack_spill, sb));
-                        c->d_stack_spill_bytes = sb;
-                    }
-                    L.stack_spill = c->d_stack_spill;
-                }
-            }
             L.queue = rt::queue_blocks(c->n_cu, qv, L);
             L.n_items = (uint32_t)items;
             L.n_qitems = L.n_items >> L.grp_log2;

@@ -48,8 +48,6 @@ struct rt_ctx {
     uint32_t* d_queue = nullptr;  // work-queue head
     float* d_partial = nullptr;   // work-queue partial sums
     size_t d_partial_bytes = 0;
-    uint32_t* d_stack_spill = nullptr;  // the 4-wide mesh traversal's deepest stack entries (RenderLaunch)
-    size_t d_stack_spill_bytes = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool have_events = false;
     // one (start, end-of-megakernel) event pair per launch since the counters were last

@@ -50,9 +50,6 @@ struct RenderLaunch {
     int32_t stack_depth;      // BVH traversal stack entries per lane = the scene's BVH depth (>= 1): an
                               // ordered traversal holds at most one pending subtree per level below the
                               // root, so the LDS stacks are sized per scene (dynamic LDS)
-    int32_t stack_lds;        // of which the first stack_lds live in LDS; entries stack_lds .. stack_depth - 1
-                              // (the 4-wide mesh traversal's rare deep ones) in stack_spill
-    uint32_t* stack_spill;    // per wave of the persistent grid: (stack_depth - stack_lds) x 64 lanes, or null
     float pt_scale;           // pathTrace: max |coordinate| of the triangles
     uint32_t pt_root_ref;     // pathTrace: the root's child-pair reference (rt_bvh.h cf_child_pairs)
     // Pixel output (Canvas.h:58-98): accumulate = 0 writes the mean color/spp to
@@ -148,8 +145,6 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
 // Workgroups of the persistent work-queue grid (n_cu x resident 4-wave blocks per CU: the
 // variant's occupancy, capped by the LDS its tables and L's traversal stacks take).
 int queue_blocks(int n_cu, uint32_t variant, const RenderLaunch& L);
-// Traversal-stack entries per lane that fit in LDS with the variant at its compiled occupancy.
-int stack_lds_fit(uint32_t variant);
 // The kernel instantiation of a launch (rtmi.h RT_VARIANT_*) from the integrator, the
 // schedule and the committed scene's content; the occupancy it is compiled for (waves per
 // SIMD); its symbol as rocprofv3 prints it (nullptr for an unknown id).

@@ -320,14 +320,6 @@ __device__ __forceinline__ const RenderLaunch& launch_args() {
 // re-tested at every pop, per-lane leaf loops) A popped entry is not re-tested against the improved bound
 // (its children are, on their pair load); pruning stays conservative, so the candidate set
 // still contains the sequential scan's winner and the (t, index) minimum picks it.
-// kWide: the same traversal over 4-wide nodes (rt_scene.h WideNode): an inner step is one
-// aligned 128 B load and four box tests; the hit children are sorted by entry distance, the
-// nearest becomes the lane's reference and the others are pushed farthest first, so the next
-// nearest is popped first. Half the dependent loads per ray of the child-pair records; the
-// stack bound is the builder's max over paths of sum (children - 1). Its entries at and above
-// L.stack_lds (the deepest, which few lanes reach) live in the wave's L.stack_spill area in HBM
-// instead of LDS (rt_capi.cpp launch); only LDS entries are stolen.
-template <bool kWide>
 __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
                                                const uint32_t* __restrict__ tri_orig,
                                                const BvhNode* __restrict__ nodes, uint32_t root, uint32_t base,
@@ -343,23 +335,6 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
     uint32_t cur = root;  // pair index or leaf reference
     bool has = want;
     int sp = 0, bot = 0;            // pending references: wstack[k * 64 + lane], bot <= k < sp
-    // kWide: entries k >= L.stack_lds in the wave's HBM spill area. Nothing about it is held
-    // across the loop: the launch fields are scalar loads at the use, the wave's slot is scalar.
-    auto spill_at = [&](int k) -> uint32_t* {
-        const RenderLaunch& LA = launch_args();
-        const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-        return LA.stack_spill +
-               ((size_t)w * (size_t)(LA.stack_depth - LA.stack_lds) + (size_t)(k - LA.stack_lds)) * 64 + lane;
-    };
-    auto in_lds = [&](int k) { return !kWide || k < launch_args().stack_lds; };
-    auto put = [&](int k, uint32_t v) {
-        if (in_lds(k)) wstack[k * 64 + lane] = v;
-        else *spill_at(k) = v;
-    };
-    auto get = [&](int k) -> uint32_t {
-        if (in_lds(k)) return wstack[k * 64 + lane];
-        return *spill_at(k);
-    };
     uint32_t qtail = 0, qdone = 0;  // wave-uniform positions in the pair queue W.slot (256 entries)
     constexpr uint32_t kQ = (uint32_t)kMaxRun * 64u;
     static_assert(kQ >= 256, "the pair queue holds 63 + 3 x 64 pairs");
@@ -385,7 +360,7 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
         if (__ballot(has || sp > bot) == 0) break;
         // steal: pair the r-th idle lane with the r-th lane that has a spare reference
         const bool idle = !has && sp == bot;
-        const bool spare = sp - bot >= (has ? 1 : 2) && in_lds(bot);
+        const bool spare = sp - bot >= (has ? 1 : 2);
         const uint64_t im = __ballot(idle), vm = __ballot(spare);
         if (im != 0 && vm != 0) {
             const int nv = __popcll(vm), ni = __popcll(im);
@@ -416,60 +391,13 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             __builtin_amdgcn_wave_barrier();
         }
         if (!has && sp > bot) {
-            cur = get(--sp);
+            cur = wstack[(--sp) * 64 + lane];
             has = true;
             // the ray's best so far over all lanes (NaN while none: fminf keeps ours)
             best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
         }
         if (!has && sp == bot) sp = bot = 0;
-        if (kWide && has && !(cur & kLeafRef)) {
-            const float4* q = reinterpret_cast<const float4*>(nodes + 4 * (size_t)cur);
-            const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
-            const uint4 rf = reinterpret_cast<const uint4*>(q)[6];
-            cnt.node_visits += 4;
-            // entry distance of each child, +inf when missed (the sort keys)
-            const float bound = best * 1.00001f + 1e-30f;
-            auto test = [&](float x0, float y0, float z0, float x1, float y1, float z1) {
-                const float tx0 = (x0 - ro.x) * ri.x, tx1 = (x1 - ro.x) * ri.x;
-                const float ty0 = (y0 - ro.y) * ri.y, ty1 = (y1 - ro.y) * ri.y;
-                const float tz0 = (z0 - ro.z) * ri.z, tz1 = (z1 - ro.z) * ri.z;
-                const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-                const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-                return tn <= fminf(tf, bound) ? tn : kInf;
-            };
-            float k0 = test(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x), k1 = test(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y);
-            float k2 = test(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z), k3 = test(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w);
-            uint32_t r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
-            // sorting network (0,1) (2,3) (0,2) (1,3) (1,2): ascending entry distance
-            auto cx = [](float& ka, uint32_t& ra, float& kb, uint32_t& rb) {
-                const bool sw = kb < ka;
-                const float kt = sw ? kb : ka;
-                kb = sw ? ka : kb;
-                ka = kt;
-                const uint32_t rt = sw ? rb : ra;
-                rb = sw ? ra : rb;
-                ra = rt;
-            };
-            cx(k0, r0, k1, r1);
-            cx(k2, r2, k3, r3);
-            cx(k0, r0, k2, r2);
-            cx(k1, r1, k3, r3);
-            cx(k1, r1, k2, r2);
-            const int nh = (k0 < kInf) + (k1 < kInf) + (k2 < kInf) + (k3 < kInf);
-            if (nh == 0) {
-                has = false;
-            } else if (sp + nh - 1 > cap) {
-                cnt.overflow();
-                has = false;
-                sp = bot = 0;
-            } else {
-                if (nh > 3) put(sp++, r3);
-                if (nh > 2) put(sp++, r2);
-                if (nh > 1) put(sp++, r1);
-                cur = r0;
-            }
-        }
-        if (!kWide && has && !(cur & kLeafRef)) {
+        if (has && !(cur & kLeafRef)) {
             const BvhNode nl = nodes[2 * (size_t)cur], nr = nodes[2 * (size_t)cur + 1];
             cnt.node_visits += 2;
             float tl, tr;
@@ -913,9 +841,8 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             } else if constexpr ((kParts & 1) != 0) {
                 const bool want = live && box_hit(f, o, inv);
                 cnt.box_tests += (uint32_t)__popcll(__ballot(live));
-                mesh_bvh_pairs<RT_MESH_WIDE != 0>(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0,
-                                                  want, o, d, inv, h, i, ob.order, stack - lane, W, lane, cnt,
-                                                  S.stack_cap);
+                mesh_bvh_pairs(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0, want, o, d, inv, h, i,
+                               ob.order, stack - lane, W, lane, cnt, S.stack_cap);
             }
         } else if ((kMed || (kBvh && kSph)) && ob.type == kObjMedium) {
             // (the general linear-scan kernel never sees a medium: launch_render sends scenes with
@@ -959,6 +886,34 @@ __device__ __forceinline__ Ray camera_sample(const CamRec* camp, const RenderLau
     dir = normalize(dir);
     const float tm = random_range(rng, cam.time0, cam.time1);
     return Ray{add(cam.origin, offset), dir, tm};
+}
+
+// The Ray ctor's inverse direction (Ray.h:10-16), 1.0f / d per component, correctly rounded.
+// v_rcp_f32 + one Newton step is RN(1/x) for every x with 2^-126 <= |x| < 2^126 (exhaustive
+// GPU check over all 4.2e9 such floats, tools/div_check.hip, profiles/r02/div_check.json): 3 VALU
+// per component instead of the IEEE division's 11. A wave with any component outside that range
+// (zero, subnormal, huge, inf or NaN: practically never, for normalized directions) takes the IEEE
+// division for its lanes. Called by all lanes of the wave (wave-uniform branch).
+#ifndef RT_RCP_NR
+#define RT_RCP_NR 1  // 0: IEEE divisions (A/B)
+#endif
+__device__ __forceinline__ v3 rcp_exact(v3 d) {
+#if RT_RCP_NR
+    auto nr = [](float b) {
+        const float y0 = __builtin_amdgcn_rcpf(b);
+        return __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
+    };
+    v3 r{nr(d.x), nr(d.y), nr(d.z)};
+    const float lo = fminf(fminf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
+    const float hi = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
+    const bool ok = lo >= 0x1p-126f && hi < 0x1p126f;  // false for NaN (fminf / fmaxf skip NaNs:
+    const bool nan = (d.x != d.x) | (d.y != d.y) | (d.z != d.z);  // checked on their own)
+    if (__builtin_expect(__ballot(!ok || nan) != 0, 0))
+        if (!ok || nan) r = rcp(d);
+    return r;
+#else
+    return rcp(d);
+#endif
 }
 
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
@@ -1320,7 +1275,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         W.grp_s[lane] = 0;
         W.grp_m[lane] = 0;
     }
-    uint32_t* stack = kBvh ? dyn_stacks + (size_t)wave * L.stack_lds * 64 + lane : nullptr;
+    uint32_t* stack = kBvh ? dyn_stacks + (size_t)wave * L.stack_depth * 64 + lane : nullptr;
 
     // Lane layout: SP = lanes_per_pixel adjacent lanes share one pixel and split
     // its samples (sub-lane c takes samples c, c+SP, c+2SP, ...). A wave covers
@@ -1469,7 +1424,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         tm[6] += (uint64_t)__popcll(__ballot(valid)); // lanes that own a pixel
 #endif
 
-        const v3 inv = rcp(ray.d);
+        const v3 inv = rcp_exact(ray.d);
         const Hit h = closest_hit<kBvh, kMed, kSph, kParts>(S, ray, inv, live, rng, W, stack, lane, cnt
 #ifdef RT_STAMPS
                                         , tm
@@ -1983,9 +1938,6 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
 
 }  // namespace
 
-#ifndef RT_PT_GSUM
-#define RT_PT_GSUM 1  // pathTrace work-queue launches fold a sub-stream's sum in its partial-sum slot (0: registers)
-#endif
 template <bool kQueue>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES))) void pathtrace_kernel(
     RenderLaunch L, const KTri* __restrict__ ktris, const CFNode* __restrict__ nodes,
@@ -1997,7 +1949,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
     __shared__ uint32_t pt_queue[kWavesPerBlock][256];          // deferred leaf pairs
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    uint32_t* stack = dyn_stacks + (size_t)wave * L.stack_lds * 64 + lane;
+    uint32_t* stack = dyn_stacks + (size_t)wave * L.stack_depth * 64 + lane;
 
     const int SP = L.lanes_per_pixel;
     int c = lane & (SP - 1);
@@ -2036,15 +1988,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
                 item = it;
                 s = ic;
                 alive = s < L.spp;
-#if RT_PT_GSUM
-                // the group's sample sums live in their partial-sum slots: zero them (a sub-stream with
-                // no samples, S > spp, keeps the zero)
-                zero_members(L, item, SP);
-#else
-                sum = v3{0.0f, 0.0f, 0.0f};
+                const float z = fresh_f32(0.0f);  // materialised here, not kept live (and spilled)
+                sum = v3{z, z, z};
                 // sub-streams with no samples (S > spp) still own their partial-sum slots
                 if (!alive) zero_members(L, item, SP);
-#endif
                 need_cam = true;
             }, []() {});
         }
@@ -2225,23 +2172,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
             }
         }
         if (done) {
-#if RT_PT_GSUM
-            if (kQueue) {  // ((0 + c0) + c1) + ...: the register fold's order, through the slot
-                const float* q = L.partial + ((size_t)(item & (uint32_t)(SP - 1)) * L.n_pix + (item >> L.sp_log2)) * 3;
-                store_partial(L, item, add(v3{q[0], q[1], q[2]}, contrib));
-            } else {
-                sum = add(sum, contrib);
-            }
-#else
             sum = add(sum, contrib);
-#endif
             need_cam = true;
             s += SP;
             if (s >= L.spp) {  // (pathTrace launches run one sub-stream per work item: grp_log2 = 0)
                 alive = false;
-#if !RT_PT_GSUM
                 if (kQueue) store_partial(L, item, sum);
-#endif
             }
         }
     }
@@ -2271,7 +2207,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
 
 // Dynamic LDS of a traversal kernel: the per-lane stacks of its 4 waves.
 static size_t stack_bytes(const RenderLaunch& L) {
-    return (size_t)kWavesPerBlock * (size_t)(L.stack_lds > 0 ? L.stack_lds : 1) * 64 * sizeof(uint32_t);
+    return (size_t)kWavesPerBlock * (size_t)(L.stack_depth > 0 ? L.stack_depth : 1) * 64 * sizeof(uint32_t);
 }
 
 hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const RenderLaunch& L,
@@ -2301,13 +2237,6 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
 // A persistent grid fills the resident waves: waves per SIMD x 4 SIMDs / 4-wave blocks per CU,
 // capped by what fits the CU's 160 KB of LDS (the variant's static tables + the launch's
 // traversal stacks): blocks beyond it would only start once others retire, after the queue ran dry.
-int stack_lds_fit(uint32_t variant) {
-    const int waves = variant_waves(variant);
-    const size_t budget = (size_t)160 * 1024 / (size_t)(waves > 0 ? waves : 1);  // per 4-wave block
-    const size_t fixed = (size_t)kWavesPerBlock * sizeof(WaveLds);
-    return budget > fixed ? (int)((budget - fixed) / ((size_t)kWavesPerBlock * 64 * sizeof(uint32_t))) : 1;
-}
-
 int queue_blocks(int n_cu, uint32_t variant, const RenderLaunch& L) {
     const int waves = variant_waves(variant);
     size_t lds = 0;
@@ -2395,7 +2324,7 @@ uint32_t kernel_build_flags() {
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
-    RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_MESH_WIDE != 1 || RT_WIDE_SPLIT != 1 || RT_PT_GSUM != 1
+    RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;

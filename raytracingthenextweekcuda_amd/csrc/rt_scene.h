@@ -44,8 +44,7 @@ struct alignas(16) ObjRec {
     //        orientation's axes a, b (XY: x, y; YZ: y, z; XZ: x, z)
     // mesh: boundsMin xyz, boundsMax xyz (computeMeshAABB, main.cu:261-281), f[6] = the bits of
     //       ceil(2^32 / triangle count) (the brute-force compaction's division), f[7] = mesh-run
-    //       length (brute force), f[8] = root reference (BVH meshes: a WideNode index or a leaf
-    //       reference; sphere groups: a child-pair reference)
+    //       length (brute force), f[8] = root child-pair reference (BVH meshes)
     float f[10];
 };
 constexpr uint32_t kNoBvh = 0xFFFFFFFFu;
@@ -57,10 +56,6 @@ constexpr uint32_t kSphereBvhMin = 16;
 // Per-lane LDS traversal stack depth; the builder rejects deeper trees, like
 // the reference's BVH_STACK_SIZE check (BVH.cpp:490-496, CUDAPathTracer.h:43).
 constexpr int kBvhStackDepth = 32;
-// The 4-wide mesh traversal may hold up to (children - 1) pending entries per wide level: its
-// bound (WideBuilder::max_push, the max over paths) is checked against this, and the launch
-// sizes the LDS stacks (and the persistent grid's blocks per CU) by the scene's bound.
-constexpr int kWideStackMax = 48;  // 48 KB of stacks per 4-wave block: within the 64 KB default dynamic LDS
 static_assert(sizeof(ObjRec) == 64, "ObjRec must be 64 B");
 
 // Triangle as prepared by prepareTriangleData (main.cu:334-349): v0, E1, E2.
@@ -86,26 +81,6 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 32, "BvhNode must be 32 B");
 
-// 4-wide BVH node of the rayColor mesh traversal (rt_kernel.hip mesh_bvh_wide; built by
-// HostScene::build_mesh_pairs from the binary SAH tree, whose adjacent levels it collapses):
-// up to four children's boxes as SoA rows (lo x, lo y, lo z, hi x, hi y, hi z; four floats
-// each), their references (a wide node index, or a leaf reference as in the child-pair
-// records: kLeafRef | (count - 1) << 27 | first), and the child count. One aligned 128 B
-// line = four BvhNode slots of the node table from an index divisible by four. An empty slot
-// has the box lo = hi = +inf on every axis, which node_hit rejects for any ray.
-struct alignas(16) WideNode {
-    float lo[3][4];
-    float hi[3][4];
-    uint32_t ref[4];
-    uint32_t n, pad[3];
-};
-static_assert(sizeof(WideNode) == 128, "WideNode must be 128 B");
-#ifndef RT_WIDE_SPLIT
-#define RT_WIDE_SPLIT 1  // the wide traversal's deepest stack entries in HBM when LDS would lower occupancy (0: A/B)
-#endif
-#ifndef RT_MESH_WIDE
-#define RT_MESH_WIDE 1  // rayColor mesh BVHs as 4-wide nodes (0: child-pair records; A/B)
-#endif
 
 struct alignas(16) MatRec {
     uint32_t type;  // RT_LAMBERTIAN..RT_ISOTROPIC
@@ -170,8 +145,6 @@ struct HostScene {
     std::vector<BvhNode> nodes;
     std::vector<uint32_t> tri_orig;  // 2 per triangle: (mesh-local index, inverse map), see flatten()
     int bvh_max_depth = 0;
-    int wide_bound = 0;   // stack entries the 4-wide mesh traversals may push (0: none)
-    int group_bound = 0;  // ... the sphere-group and child-pair mesh traversals (LDS-resident)
 
     // BVH builder (rt_set_bvh_builder): host Recurse, or its GPU restatement on
     // `bvh_device` (byte-identical; falls back to the host when it declines).

@@ -30,12 +30,15 @@ if [ "${BENCH:-0}" = "1" ]; then
   stop_if_fatal $? bench
 fi
 for sc in ${SCENES:-}; do
-  timeout -k 10 300 python bench.py --scene $sc --no-cpu-baseline ${BENCH_ARGS:-} > "$O/bench_$sc.log" 2>&1
-  stop_if_fatal $? bench_$sc
+ for rep in $(seq 1 ${REPS:-1}); do  # REPS > 1: the A/B round repeated, logs suffixed _r<rep>
+  sfx=""; [ "${REPS:-1}" -gt 1 ] && sfx="_r$rep"
+  timeout -k 10 300 python bench.py --scene $sc --no-cpu-baseline ${BENCH_ARGS:-} > "$O/bench_$sc$sfx.log" 2>&1
+  stop_if_fatal $? bench_$sc$sfx
   for alt in ${ALT:-}; do  # A/B libraries of the same sources (RTMI_LIB), same box, interleaved
-    RTMI_LIB=raytracingthenextweekcuda_amd/$alt timeout -k 10 300 python bench.py --scene $sc --no-cpu-baseline ${BENCH_ARGS:-} > "$O/bench_${sc}_${alt%.so}.log" 2>&1
-    stop_if_fatal $? bench_${sc}_$alt
+    RTMI_LIB=raytracingthenextweekcuda_amd/$alt timeout -k 10 300 python bench.py --scene $sc --no-cpu-baseline ${BENCH_ARGS:-} > "$O/bench_${sc}_${alt%.so}$sfx.log" 2>&1
+    stop_if_fatal $? bench_${sc}_$alt$sfx
   done
+ done
 done
 if [ "${PROBE:-0}" = "1" ] && [ -x ./tools/valu_probe ]; then  # lane-utilisation calibration (64 / 16 lanes)
   for a in 64 16; do

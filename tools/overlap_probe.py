@@ -1,7 +1,7 @@
 """Does overlapping consecutive frames fill the SIMDs that a launch's tail leaves idle?
 Renders K frames (rank 0's shard of a world-W row tiling) back to back on one context and
 stream, then rotating over n contexts on n streams, and prints ms per frame of each.
-Usage: [SCENE=cornellbox1] [CTX="1 2"] [LANES=0] python tools/overlap_probe.py W [K]"""
+Usage: [SCENE=cornellbox1] [CTX="1 2"] [LANES=0] [FIF=1] python tools/overlap_probe.py W [K]"""
 import os
 import sys
 import time
@@ -24,7 +24,9 @@ for r in rs:
 outs = [torch.empty((H, W, 3), dtype=torch.float32, device="cuda") for _ in rs]
 streams = [torch.cuda.Stream() for _ in rs]
 LANES = int(os.environ.get("LANES", "0"))  # sub-streams per pixel (0 = auto)
-p = rs[0].params(W, H, SPP, DEPTH, 1984, 0, 2, 0, world, LANES, bench.INTEGRATOR.get(SCENE, "rayColor"))
+FIF = os.environ.get("FIF", "1") == "1"  # RT_RENDER_FRAMES_IN_FLIGHT, as bench.py sets it with 3 contexts
+p = rs[0].params(W, H, SPP, DEPTH, 1984, 0, 2, 0, world, LANES, bench.INTEGRATOR.get(SCENE, "rayColor"),
+                 frames_in_flight=FIF)
 
 
 def run(n_ctx):
