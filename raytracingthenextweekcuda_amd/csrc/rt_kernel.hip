@@ -281,6 +281,28 @@ __device__ __forceinline__ float fresh_f32(float v) {
     return v;
 }
 
+// Correctly rounded reciprocal and quotient without the IEEE division expansion (11 VALU):
+// v_rcp_f32 + one Newton step is RN(1/b) for every b with 2^-126 <= |b| < 2^126 (exhaustive GPU
+// check over all 4.2e9 such floats, tools/div_check.hip, profiles/r02/div_check.json), and
+// Markstein's correction q0 + r y with that y is RN(a/b) for |a|, |b| in [2^-100, 2^101) and
+// |a/b| in [2^-121, 2^125) (Markstein's theorem; the same check draws 4.3e9 random pairs of that
+// domain: no mismatch). Callers use them only where their operands provably lie in these domains,
+// or fall back to the IEEE division for the wave.
+#ifndef RT_RCP_NR
+#define RT_RCP_NR 1  // 0: IEEE divisions for the inverse direction (A/B)
+#endif
+#ifndef RT_DIV_NR
+#define RT_DIV_NR 1  // 0: IEEE divisions in the plane test and Lambertian's normalize (A/B)
+#endif
+__device__ __forceinline__ float rcp_nr(float b) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
+}
+__device__ __forceinline__ float div_y(float a, float b, float y) {
+    const float q0 = a * y;
+    return __builtin_fmaf(__builtin_fmaf(-b, q0, a), y, q0);
+}
+
 // Sets an LDS 64-bit minimum slot to +inf (all ones).
 __device__ __forceinline__ void key_reset(unsigned long long& k) {
     const uint32_t ones = fresh_u32(~0u);
@@ -807,7 +829,19 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             const v3 nrm{f[3], f[4], f[5]};
             const float den = dot(nrm, d);
             const bool proceed = ob.u1 ? (fabsf(den) > kTMin) : (den > kTMin);
-            const float t = fdiv(dot(sub(v3{f[0], f[1], f[2]}, o), nrm), den);
+            const float num = dot(sub(v3{f[0], f[1], f[2]}, o), nrm);
+#if RT_DIV_NR
+            // t matters only where `proceed` holds, i.e. |den| > tMin, and then only through
+            // t >= tMin and the comparisons after it. Markstein's quotient is exact for |num|, |den| in
+            // [2^-100, 2^100) and |t| >= 2^-121; a smaller |num| or |t| is below tMin either way. A
+            // wave with a proceeding lane whose |num| or |den| is >= 2^100, inf or NaN takes the
+            // IEEE division.
+            float t = div_y(num, den, rcp_nr(den));
+            if (__builtin_expect(__ballot(proceed && !(fmaxf(fabsf(num), fabsf(den)) < 0x1p100f)) != 0, 0))
+                t = fdiv(num, den);
+#else
+            const float t = fdiv(num, den);
+#endif
             // the hit point's two in-plane coordinates (ray.at(t) per component), tested
             // against the bounds rt_scene.cpp precomputed with Plane::hit's float ops
             float pa, pb;
@@ -876,8 +910,15 @@ __device__ __forceinline__ Ray camera_sample(const CamRec* camp, const RenderLau
     rng.begin(L.seed, pixel, L.sample_offset + (uint32_t)s);
     const float rx = rng.next();
     const float ry = rng.next();
+#if RT_DIV_NR
+    // (px + rx) / (W - 1): the numerator is in [2^-33, 2^31] (rx is a u01 draw), the divisor an
+    // integer in [1, 2^31], so the quotient is >= 2^-64: Markstein's domain, exact without a guard
+    const float dx = div_y((float)px + rx, fw, rcp_nr(fw));
+    const float dy = div_y((float)y + ry, fh, rcp_nr(fh));
+#else
     const float dx = fdiv((float)px + rx, fw);
     const float dy = fdiv((float)y + ry, fh);
+#endif
     const v3 disk = random_in_unit_disk(rng);
     const v3 rnd = scale(disk, cam.lens_radius);
     const v3 offset = add(scale(cam.right, rnd.x), scale(cam.true_up, rnd.y));
@@ -894,16 +935,9 @@ __device__ __forceinline__ Ray camera_sample(const CamRec* camp, const RenderLau
 // per component instead of the IEEE division's 11. A wave with any component outside that range
 // (zero, subnormal, huge, inf or NaN: practically never, for normalized directions) takes the IEEE
 // division for its lanes. Called by all lanes of the wave (wave-uniform branch).
-#ifndef RT_RCP_NR
-#define RT_RCP_NR 1  // 0: IEEE divisions (A/B)
-#endif
 __device__ __forceinline__ v3 rcp_exact(v3 d) {
 #if RT_RCP_NR
-    auto nr = [](float b) {
-        const float y0 = __builtin_amdgcn_rcpf(b);
-        return __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
-    };
-    v3 r{nr(d.x), nr(d.y), nr(d.z)};
+    v3 r{rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z)};
     const float lo = fminf(fminf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
     const float hi = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
     const bool ok = lo >= 0x1p-126f && hi < 0x1p126f;  // false for NaN (fminf / fmaxf skip NaNs:
@@ -1474,7 +1508,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             if (m.type == 0u || (kSph && (m.type == 1u || m.type == 4u))) rp = random_in_unit_sphere(rng);
             if (m.type == 0u) {
                 // Lambertian::scatter (Material.cu:3-19).
+#if RT_DIV_NR
+                // normalize(rp) of a randomInUnitSphere draw: each component is 2u - 1 of a u01 draw, so
+                // +0 or at least 2^-24 in magnitude, and |rp| < 1: inside Markstein's domain (a +0
+                // component gives +0, as the IEEE division does) unless rp = 0 (all three draws 1/2,
+                // p = 2^-72), which takes the IEEE division
+                const float nrp = fsqrt(rp.x * rp.x + rp.y * rp.y + rp.z * rp.z);
+                const float yrp = rcp_nr(nrp);
+                v3 u{div_y(rp.x, nrp, yrp), div_y(rp.y, nrp, yrp), div_y(rp.z, nrp, yrp)};
+                if (__builtin_expect(__ballot(!(nrp > 0.0f)) != 0, 0))
+                    if (!(nrp > 0.0f)) u = normalize(rp);
+#else
                 v3 u = normalize(rp);
+#endif
                 v3 sd = add(n, u);
                 if ((fabsf(sd.x) < 1e-8f) && (fabsf(sd.y) < 1e-8f) && (fabsf(sd.z) < 1e-8f)) sd = n;
                 nd = normalize(sd);
@@ -2324,7 +2370,7 @@ uint32_t kernel_build_flags() {
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
-    RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1
+    RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
     return f;
