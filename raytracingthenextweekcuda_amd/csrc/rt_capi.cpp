@@ -697,8 +697,11 @@ rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& 
 #ifndef RT_FIF_GROUPS
 #define RT_FIF_GROUPS 1  // 0 (A/B only): frames in flight lower the auto S to 16 instead (round 3)
 #endif
+#ifndef RT_FIF_ITEMS
+#define RT_FIF_ITEMS 16  // work items per pixel with frames in flight (A/B builds only)
+#endif
     if (RT_FIF_GROUPS && queue && !bvh && (p->flags & RT_RENDER_FRAMES_IN_FLIGHT))
-        while ((L.lanes_per_pixel >> L.grp_log2) > 16) ++L.grp_log2;
+        while ((L.lanes_per_pixel >> L.grp_log2) > RT_FIF_ITEMS) ++L.grp_log2;
     if (!RT_FIF_GROUPS && s == 0 && queue && !bvh && (p->flags & RT_RENDER_FRAMES_IN_FLIGHT) && L.lanes_per_pixel > 16)
         rt::choose_layout(L, 16, queue, bvh);
     L.accumulate = 0;

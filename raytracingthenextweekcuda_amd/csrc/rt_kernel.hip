@@ -2373,6 +2373,9 @@ uint32_t kernel_build_flags() {
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
+#if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)
+    f |= 4u;  // (host-side layout switches of rt_capi.cpp, passed to every TU through EXTRA)
+#endif
     return f;
 }
 
