@@ -402,6 +402,7 @@ def measure(args, world, rank, local, rehearsal):
         "frame_ms_isolated": float(np.mean(iso_frame)),
         "launch_ms": float(np.mean(launch_ms)),
         "lanes_per_pixel": int(st["lanes_per_pixel"]), "refill": int(st["refill"]),
+        "substreams_per_item": int(st.get("substreams_per_item", 1)),
         "queue_blocks": int(st["queue_blocks"]), "variant": st["variant_name"],
         "object_bytes_per_segment": object_bytes_per_segment(r) if integrator != "pathTrace" else 0,
         "n_cu": n_cu, "overlap": overlap, "contexts": len(rs), "frames_in_flight": in_flight,
@@ -510,6 +511,7 @@ def build_line(args, agg: dict, world: int, cpu=None) -> dict:
             "scene": SCENES[args.scene][5],
             "width": W, "height": H, "spp": args.spp, "depth": args.depth,
             "row_block": args.row_block, "lanes_per_pixel": agg["lanes_per_pixel"],
+            "substreams_per_item": agg.get("substreams_per_item", 1),
             "variant": agg["variant"], "queue": agg["queue_blocks"] > 0,
             "refill": agg["refill"], "queue_blocks": agg["queue_blocks"], "contexts": agg.get("contexts", 1),
             "frames_in_flight": bool(agg.get("frames_in_flight", False)),
