@@ -46,7 +46,16 @@ namespace rt {
 namespace {
 
 constexpr float kInf = __builtin_huge_valf();
-constexpr int kWavesPerBlock = 4;
+constexpr int kWavesPerBlock = 4;  // static-grid blocks: 2 x 2 wave tiles
+// Waves per block of the persistent work-queue grid. A block's LDS is released only when all its
+// waves have retired, so at the end of a launch a block with one long wave holds the LDS of all;
+// smaller blocks hand SIMD resources to the next launch in flight wave by wave.
+#ifndef RT_QUEUE_BLOCK_WAVES
+#define RT_QUEUE_BLOCK_WAVES 4
+#endif
+constexpr int kQueueBlockWaves = RT_QUEUE_BLOCK_WAVES;
+static_assert(kQueueBlockWaves == 1 || kQueueBlockWaves == 2 || kQueueBlockWaves == 4, "queue block waves");
+constexpr int block_waves(bool queue) { return queue ? kQueueBlockWaves : kWavesPerBlock; }
 
 struct Ray {
     v3 o, d;
@@ -1295,11 +1304,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
     const uint32_t* __restrict__ tri_orig, int n_objs, const CamRec* __restrict__ cam,
     float* __restrict__ out, unsigned long long* __restrict__ counters) {
     const SceneArgs S{objs, tris, mats, nodes, tri_orig, n_objs, 0, kBvh, L.stack_depth};
-    __shared__ WaveLds lds[kWavesPerBlock];
+    constexpr int kBW = block_waves(kQueue);
+    __shared__ WaveLds lds[kBW];
     // camera slots: the linear-scan kernels only (the traversal kernels' LDS holds their stacks)
     constexpr bool kCamPf = !kBvh;
-    __shared__ CamSlots cslots[kCamPf ? kWavesPerBlock : 1];
-    // traversal stacks (kBvh): kWavesPerBlock x L.stack_depth x 64 lanes, sized per scene at launch
+    __shared__ CamSlots cslots[kCamPf ? kBW : 1];
+    // traversal stacks (kBvh): kBW x L.stack_depth x 64 lanes, sized per scene at launch
     extern __shared__ uint32_t dyn_stacks[];
 
     const int lane = threadIdx.x & 63;
@@ -1989,10 +1999,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
     RenderLaunch L, const KTri* __restrict__ ktris, const CFNode* __restrict__ nodes,
     const int32_t* __restrict__ tri_list, const CamRec* __restrict__ cam, float* __restrict__ out,
     unsigned long long* __restrict__ counters) {
-    extern __shared__ uint32_t dyn_stacks[];  // kWavesPerBlock x L.stack_depth x 64, sized at launch
-    __shared__ unsigned long long pt_keys[kWavesPerBlock][64];  // per-ray minima (cooperative traversal)
-    __shared__ int32_t pt_vlist[kWavesPerBlock][64];            // victims of a steal round
-    __shared__ uint32_t pt_queue[kWavesPerBlock][256];          // deferred leaf pairs
+    constexpr int kBW = block_waves(kQueue);
+    extern __shared__ uint32_t dyn_stacks[];  // kBW x L.stack_depth x 64, sized at launch
+    __shared__ unsigned long long pt_keys[kBW][64];  // per-ray minima (cooperative traversal)
+    __shared__ int32_t pt_vlist[kBW][64];            // victims of a steal round
+    __shared__ uint32_t pt_queue[kBW][256];          // deferred leaf pairs
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     uint32_t* stack = dyn_stacks + (size_t)wave * L.stack_depth * 64 + lane;
@@ -2251,21 +2262,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
     }
 }
 
-// Dynamic LDS of a traversal kernel: the per-lane stacks of its 4 waves.
-static size_t stack_bytes(const RenderLaunch& L) {
-    return (size_t)kWavesPerBlock * (size_t)(L.stack_depth > 0 ? L.stack_depth : 1) * 64 * sizeof(uint32_t);
+// Dynamic LDS of a traversal kernel: the per-lane stacks of the block's `bw` waves.
+static size_t stack_bytes(const RenderLaunch& L, int bw) {
+    return (size_t)bw * (size_t)(L.stack_depth > 0 ? L.stack_depth : 1) * 64 * sizeof(uint32_t);
 }
 
 hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const RenderLaunch& L,
                             float* out, unsigned long long* counters, hipStream_t stream, hipEvent_t main_done) {
-    dim3 block(64 * kWavesPerBlock);
     if (L.queue) {
         if (L.n_items == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
         const uint32_t waves = (L.n_items + 63u) / 64u;
-        const uint32_t blocks = std::min<uint32_t>((waves + kWavesPerBlock - 1) / kWavesPerBlock,
+        const uint32_t blocks = std::min<uint32_t>((waves + kQueueBlockWaves - 1) / kQueueBlockWaves,
                                                    (uint32_t)L.queue);
-        hipLaunchKernelGGL(pathtrace_kernel<true>, dim3(blocks), block, stack_bytes(L), stream, L, sc.ktris, sc.nodes,
-                           sc.tri_list, cam, out, counters);
+        hipLaunchKernelGGL(pathtrace_kernel<true>, dim3(blocks), dim3(64 * kQueueBlockWaves),
+                           stack_bytes(L, kQueueBlockWaves), stream, L, sc.ktris, sc.nodes, sc.tri_list, cam, out,
+                           counters);
         if (main_done) (void)hipEventRecord(main_done, stream);
         const uint32_t pixels = L.n_items / (uint32_t)L.lanes_per_pixel;
         hipLaunchKernelGGL(combine_kernel, dim3((pixels + 255u) / 256u), dim3(256), 0, stream, L, out);
@@ -2274,31 +2285,32 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
     dim3 grid((L.cols + 2 * L.tile_w - 1) / (2 * L.tile_w),
               (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
     if (grid.x == 0 || grid.y == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
-    hipLaunchKernelGGL(pathtrace_kernel<false>, grid, block, stack_bytes(L), stream, L, sc.ktris, sc.nodes,
-                       sc.tri_list, cam, out, counters);
+    hipLaunchKernelGGL(pathtrace_kernel<false>, grid, dim3(64 * kWavesPerBlock), stack_bytes(L, kWavesPerBlock),
+                       stream, L, sc.ktris, sc.nodes, sc.tri_list, cam, out, counters);
     if (main_done) (void)hipEventRecord(main_done, stream);
     return hipGetLastError();
 }
 
-// A persistent grid fills the resident waves: waves per SIMD x 4 SIMDs / 4-wave blocks per CU,
-// capped by what fits the CU's 160 KB of LDS (the variant's static tables + the launch's
-// traversal stacks): blocks beyond it would only start once others retire, after the queue ran dry.
+// A persistent grid fills the resident waves: waves per SIMD x 4 SIMDs per CU, in blocks of
+// kQueueBlockWaves, capped by what fits the CU's 160 KB of LDS (the variant's static tables + the
+// launch's traversal stacks): blocks beyond it would only start once others retire, after the queue
+// ran dry.
 int queue_blocks(int n_cu, uint32_t variant, const RenderLaunch& L) {
-    const int waves = variant_waves(variant);
+    const int waves = variant_waves(variant), bw = kQueueBlockWaves;
     size_t lds = 0;
     switch (variant) {
         case RT_VARIANT_PATHTRACE_QUEUE: case RT_VARIANT_PATHTRACE_STATIC:
-            lds = (size_t)kWavesPerBlock * 64 * (8 + 4 + 4 * 4) + stack_bytes(L);
+            lds = (size_t)bw * 64 * (8 + 4 + 4 * 4) + stack_bytes(L, bw);
             break;
         case RT_VARIANT_SCAN_QUEUE: case RT_VARIANT_SCAN_STATIC: case RT_VARIANT_SCAN_MEDIA_QUEUE:
         case RT_VARIANT_SCAN_MEDIA_STATIC: case RT_VARIANT_SCAN_SIMPLE_QUEUE: case RT_VARIANT_SCAN_SIMPLE_STATIC:
-            lds = (size_t)kWavesPerBlock * (sizeof(WaveLds) + sizeof(CamSlots));
+            lds = (size_t)bw * (sizeof(WaveLds) + sizeof(CamSlots));
             break;
         default:
-            lds = (size_t)kWavesPerBlock * sizeof(WaveLds) + stack_bytes(L);
+            lds = (size_t)bw * sizeof(WaveLds) + stack_bytes(L, bw);
     }
     const int fit = (int)((size_t)160 * 1024 / (lds ? lds : 1));
-    return n_cu * std::max(1, std::min(waves, fit));
+    return n_cu * std::max(1, std::min(4 * waves / bw, fit));
 }
 
 // The instantiation a launch runs (rtmi.h RT_VARIANT_*). This is the only place that maps
@@ -2370,7 +2382,8 @@ uint32_t kernel_build_flags() {
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
-    RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1
+    RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
+    RT_QUEUE_BLOCK_WAVES != 4
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)
@@ -2390,13 +2403,14 @@ void launch_rk(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const Rend
 
 hipError_t launch_render(uint32_t variant, const SceneArgs& sc, const CamRec* cam, const RenderLaunch& L, float* out,
                          unsigned long long* counters, hipStream_t stream, hipEvent_t main_done) {
-    const dim3 block(64 * kWavesPerBlock);
-    const size_t lds = stack_bytes(L);
+    const int bw = block_waves(L.queue != 0);
+    const dim3 block(64 * bw);
+    const size_t lds = stack_bytes(L, bw);
     dim3 grid;
     if (L.queue) {
         if (L.n_items == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
         const uint32_t waves_needed = (L.n_items + 63u) / 64u;
-        grid = dim3(std::min<uint32_t>((waves_needed + kWavesPerBlock - 1) / kWavesPerBlock, (uint32_t)L.queue), 1);
+        grid = dim3(std::min<uint32_t>((waves_needed + bw - 1) / bw, (uint32_t)L.queue), 1);
     } else {
         grid = dim3((L.cols + 2 * L.tile_w - 1) / (2 * L.tile_w), (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
         if (grid.x == 0 || grid.y == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
