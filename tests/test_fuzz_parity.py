@@ -251,3 +251,48 @@ def test_gpu_large_leaf_parity(seed, lanes):
     assert st["overflow"] == 0
     assert np.array_equal(got, want)
     assert st["segments"] == ost["segments"]
+
+
+def division_edge_spec():
+    """Planes whose quotient leaves the domain of the kernel's v_rcp + Newton / Markstein
+    division (rt_kernel.hip rcp_nr / div_y): a floor 1e31 below the scene (|num| >= 2^100) and a
+    wall with a huge, non-unit normal (|den| >= 2^100), next to ordinary objects. Waves that meet
+    them take the IEEE division; the image must stay bit-identical to the restatement's."""
+    mats = [("lambertian", 0, (0.7, 0.6, 0.5)), ("metal", 1, (0.9, 0.9, 0.9), 0.05),
+            ("emission", 2, (1.0, 0.9, 0.8), 3.0), ("lambertian", 3, (0.3, 0.5, 0.8))]
+    objs = [
+        ("plane", 0, (0.0, -1.0e31, 0.0), (0.0, 1.0, 0.0), (1.0e38, 1.0e38, 1.0e38), 0, 2, True),
+        ("plane", 1, (-1.5, 0.0, 0.0), (-3.0e31, 0.0, 0.0), (2.0, 2.0, 2.0), 2, 1, False),  # emissive: no scatter off a huge normal
+        ("sphere", 2, (0.0, 0.0, 0.0), 0.5, 1),
+        ("sphere", 3, (0.6, 0.9, -0.4), 0.3, 2),
+        ("plane", 4, (0.0, 0.0, -1.2), (0.0, 0.0, 1.0), (2.0, 2.0, 2.0), 0, 0, True),
+    ]
+    cam = ((0.3, 0.8, 2.4), (0.0, -0.2, 0.0), (0.0, 1.0, 0.0), 1.33, 60.0, 0.0, 2.5, 0.0, 1.0)
+    return {"camera": cam, "materials": mats, "objects": objs}
+
+
+def test_division_edge_spec_builds_on_host():
+    import raytracingthenextweekcuda_amd as rtmi
+
+    r = rtmi.Renderer(-1)
+    build_product(r, division_edge_spec())
+    r.close()
+    build_oracle(division_edge_spec())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lanes", [1, 8])
+def test_gpu_division_edge_parity(lanes):
+    import raytracingthenextweekcuda_amd as rtmi
+
+    spec = division_edge_spec()
+    w, h, spp, depth = 40, 30, 8, 6
+    r = rtmi.Renderer(0)
+    build_product(r, spec)
+    got = r.render(w, h, spp, depth, lanes_per_pixel=lanes)
+    st = r.stats()
+    r.close()
+    want, ost = build_oracle(spec).render(w, h, spp, depth, lanes_per_pixel=lanes)
+    assert np.isfinite(got).all()
+    assert np.array_equal(got, want)
+    assert st["segments"] == ost["segments"]
