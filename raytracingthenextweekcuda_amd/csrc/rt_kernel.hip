@@ -732,33 +732,33 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
 // or NaN.
 __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, Rng& rng) {
     const float* f = ob.f;
-    const v3 c{f[0], f[1], f[2]}, e{f[3], f[4], f[5]};
-    const v3 pos[6] = {{c.x - e.x, c.y, c.z}, {c.x + e.x, c.y, c.z}, {c.x, c.y + e.y, c.z},
-                       {c.x, c.y - e.y, c.z}, {c.x, c.y, c.z + e.z}, {c.x, c.y, c.z - e.z}};
+    // blo = center - extend, bhi = center + extend (rt_scene.cpp, the restatement's p.a -/+ e.a):
+    // faces at blo.x, bhi.x, bhi.y, blo.y, bhi.z, blo.z in createCube's order (kernels.h:139-154)
+    const v3 blo{f[0], f[1], f[2]}, bhi{f[3], f[4], f[5]};
     float tf[6];
     bool ok[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-        const v3 p = pos[k];
         // Plane::hit with the face's unit normal +-e_a (a = k / 2): dot(n, d) is +-d_a and
         // dot(p - o, n) is +-(p_a - o_a) - the zero terms only decide the sign of a zero,
         // which no test below can see (the faces count only when |d_a| > tMin; ray origins
         // and directions are finite, or all NaN) - and (-x) / (-y) = x / y, so
         // t = (p_a - o_a) / d_a is the restatement's quotient bit for bit.
         const int a = k >> 1;
+        const bool high = (k == 1) | (k == 2) | (k == 4);
         const float da = a == 0 ? d.x : (a == 1 ? d.y : d.z);
-        const float pa = a == 0 ? p.x : (a == 1 ? p.y : p.z);
         const float oa = a == 0 ? o.x : (a == 1 ? o.y : o.z);
+        const float pa = a == 0 ? (high ? bhi.x : blo.x) : (a == 1 ? (high ? bhi.y : blo.y) : (high ? bhi.z : blo.z));
         const float den = da;
         const float t = fdiv(pa - oa, da);
         const v3 q = add(o, scale(d, t));
         bool in;
         if (k < 2)  // YZ faces
-            in = (q.y > p.y - e.y) & (q.y < p.y + e.y) & (q.z > p.z - e.z) & (q.z < p.z + e.z);
+            in = (q.y > blo.y) & (q.y < bhi.y) & (q.z > blo.z) & (q.z < bhi.z);
         else if (k < 4)  // XZ faces
-            in = (q.x > p.x - e.x) & (q.x < p.x + e.x) & (q.z > p.z - e.z) & (q.z < p.z + e.z);
+            in = (q.x > blo.x) & (q.x < bhi.x) & (q.z > blo.z) & (q.z < bhi.z);
         else  // XY faces
-            in = (q.x > p.x - e.x) & (q.x < p.x + e.x) & (q.y > p.y - e.y) & (q.y < p.y + e.y);
+            in = (q.x > blo.x) & (q.x < bhi.x) & (q.y > blo.y) & (q.y < bhi.y);
         ok[k] = (fabsf(den) > kTMin) & in;
         tf[k] = t;
     }

@@ -318,6 +318,12 @@ std::string HostScene::flatten() {
         if (o.type == kObjMedium) {
             r.u0 = (uint32_t)i;             // slot: keys the free-flight draw
             r.f[6] = -1.0f / o.f[6];        // neg_inv_density
+            // the boundary's face coordinates and rectangle bounds, center -/+ extend per axis: the
+            // same floats the restatement computes per face (p.a -/+ e.a), evaluated once here
+            for (int a = 0; a < 3; ++a) {
+                r.f[a] = o.f[a] - o.f[3 + a];
+                r.f[3 + a] = o.f[a] + o.f[3 + a];
+            }
         } else if (o.type == kObjPlane) {
             r.u0 = o.orientation;
             r.u1 = o.two_side;

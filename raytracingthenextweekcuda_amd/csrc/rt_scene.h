@@ -25,7 +25,7 @@ enum ObjType : uint32_t {
     kObjPlane = 2,
     kObjMesh = 3,
     kObjSphereGroup = 4,  // BVH over (moving) spheres: u0 = first member, u1 = count, u2 = root, f[8] = root pair ref
-    kObjMedium = 5        // constant medium in a cube: f = center xyz, extend xyz, -1/density; u0 = slot
+    kObjMedium = 5        // constant medium in a cube: f = (center - extend) xyz, (center + extend) xyz, -1/density; u0 = slot
 };
 
 // One hitable (Sphere.h, Plane.h, TriangleMesh.h). Cube is flattened into its
