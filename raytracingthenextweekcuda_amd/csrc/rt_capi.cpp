@@ -549,11 +549,6 @@ static rt_status rt_process_triangle_data_impl(rt_ctx* c, const float offset[3],
     c->pt_scale = scale_max;
     c->pt_root_ref = root_ref;
     c->pt_pair_depth = pair_depth;
-    {  // stack entries: compact reference + the pushed child's truncated pruning distance
-        auto bits = [](size_t n) { int b = 0; while (((size_t)1 << b) < n) ++b; return b; };
-        const int rb = 1 + std::max(bits(dev_nodes.size() / 2 + 1), 4 + bits(b.tri_index.size() + 1));
-        c->pt_ref_bits = RT_POP_PRUNE && 32 - rb >= 6 ? rb : 32;
-    }
     c->pt_bvh = std::move(b);
     c->pt_ready = true;
     return RT_OK;
@@ -728,7 +723,7 @@ rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& 
     const int depth = p->integrator == RT_INTEGRATOR_PATHTRACE ? std::max(c->pt_bvh.max_depth, c->pt_pair_depth)
                                                                 : c->scene.bvh_max_depth;
     L.stack_depth = depth > 0 ? depth : 1;
-    L.ref_bits = p->integrator == RT_INTEGRATOR_PATHTRACE ? c->pt_ref_bits : c->scene.stack_ref_bits;
+    L.ref_bits = p->integrator == RT_INTEGRATOR_PATHTRACE ? 32 : c->scene.stack_ref_bits;
     L.pt_scale = c->pt_scale;
     L.pt_root_ref = c->pt_root_ref;
     return RT_OK;

@@ -69,7 +69,6 @@ struct rt_ctx {
     rt::CFNode* d_pt_nodes = nullptr;  // the tree's nodes, then its child-pair records (cf_child_pairs)
     uint32_t pt_root_ref = 0;          // the root's child-pair reference
     int pt_pair_depth = 0;             // pair records on the longest root-to-leaf path
-    int pt_ref_bits = 32;              // its traversal stack entries' reference bits (RenderLaunch::ref_bits)
     int32_t* d_pt_list = nullptr;
     double pt_build_ms = 0.0;
     int pt_gpu_builds = 0;

@@ -337,29 +337,6 @@ __device__ __forceinline__ const RenderLaunch& launch_args() {
     return *reinterpret_cast<const RenderLaunch*>((const char*)p);
 }
 
-// Traversal stack entries of the rayColor BVHs (mesh child pairs, sphere groups): [entry distance,
-// truncated: 32 - rb bits | compact reference: rb bits] with rb = L.ref_bits (32 = no distance). A
-// popped entry whose child box starts beyond the ray's best hit is dropped without loading its
-// pair record. The distance is the positive float's bit pattern cut to its top bits, never above the
-// true entry distance, so only subtrees node_hit would reject at the pair load are dropped.
-__device__ __forceinline__ uint32_t stack_pack(uint32_t ref, float tn) {
-    const uint32_t rb = (uint32_t)launch_args().ref_bits;
-    if (rb >= 32u) return ref;
-    const uint32_t r = (ref & kLeafRef) ? (1u << (rb - 1u)) | (((ref >> 27) & 15u) << (rb - 5u)) | (ref & 0x07FFFFFFu)
-                                        : ref;
-    return r | ((__float_as_uint(tn) >> (rb - 1u)) << rb);  // tn >= 0 (node_hit clamps it)
-}
-__device__ __forceinline__ uint32_t stack_unpack(uint32_t e, float& tq) {
-    const uint32_t rb = (uint32_t)launch_args().ref_bits;
-    if (rb >= 32u) {
-        tq = 0.0f;
-        return e;
-    }
-    tq = __uint_as_float((e >> rb) << (rb - 1u));
-    const uint32_t r = e & ((1u << rb) - 1u);
-    return (r >> (rb - 1u)) ? kLeafRef | (((r >> (rb - 5u)) & 15u) << 27) | (r & ((1u << (rb - 5u)) - 1u)) : r;
-}
-
 // The batched mesh traversal over child-pair records (rt_scene.cpp build_mesh_pairs). A lane
 // holds one reference word instead of a node: a pair index, whose 64 B record carries both
 // children's boxes and references, or a leaf reference (first triangle, count). An inner
@@ -389,9 +366,27 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
     uint32_t cur = root;  // pair index or leaf reference
     bool has = want;
     int sp = 0, bot = 0;            // pending entries: wstack[k * 64 + lane], bot <= k < sp
-    // stack entries carry the pushed child's truncated entry distance (stack_pack, stack_unpack)
-    auto pack = [&](uint32_t ref, float tn) { return stack_pack(ref, tn); };
-    auto unpack = [&](uint32_t e, float& tq) { return stack_unpack(e, tq); };
+    // A stack entry is [entry distance, truncated: 32 - rb bits | compact reference: rb bits]
+    // (L.ref_bits; 32 = no distance): a popped entry whose child box starts beyond the ray's best
+    // hit is dropped without loading its pair record. The truncated distance is never above the
+    // true one, so only subtrees node_hit would reject at the pair load are dropped.
+    auto pack = [&](uint32_t ref, float tn) -> uint32_t {
+        const uint32_t rb = (uint32_t)launch_args().ref_bits;
+        if (rb >= 32u) return ref;
+        const uint32_t r = (ref & kLeafRef) ? (1u << (rb - 1u)) | (((ref >> 27) & 15u) << (rb - 5u)) | (ref & 0x07FFFFFFu)
+                                            : ref;
+        return r | ((__float_as_uint(tn) >> (rb - 1u)) << rb);  // tn >= 0 (node_hit clamps it)
+    };
+    auto unpack = [&](uint32_t e, float& tq) -> uint32_t {
+        const uint32_t rb = (uint32_t)launch_args().ref_bits;
+        if (rb >= 32u) {
+            tq = 0.0f;
+            return e;
+        }
+        tq = __uint_as_float((e >> rb) << (rb - 1u));
+        const uint32_t r = e & ((1u << rb) - 1u);
+        return (r >> (rb - 1u)) ? kLeafRef | (((r >> (rb - 5u)) & 15u) << 27) | (r & ((1u << (rb - 5u)) - 1u)) : r;
+    };
     uint32_t qtail = 0, qdone = 0;  // wave-uniform positions in the pair queue W.slot (256 entries)
     constexpr uint32_t kQ = (uint32_t)kMaxRun * 64u;
     static_assert(kQ >= 256, "the pair queue holds 63 + 3 x 64 pairs");
@@ -687,10 +682,9 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
     };
     for (;;) {
         if (__ballot(has || sp > 0) == 0) break;
-        while (!has && sp > 0) {  // pop until an entry that can still hold a hit (stack_unpack)
-            float tq;
-            cur = stack_unpack(wstack[(--sp) * 64 + lane], tq);
-            has = !(tq > best * 1.00001f + 1e-30f);
+        if (!has && sp > 0) {
+            cur = wstack[(--sp) * 64 + lane];
+            has = true;
         }
         if (has && !(cur & kLeafRef)) {
             const BvhNode nl = nodes[2 * (size_t)cur], nr = nodes[2 * (size_t)cur + 1];
@@ -705,7 +699,7 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
                     sp = 0;
                 } else {
                     const bool left_first = tl <= tr;
-                    wstack[(sp++) * 64 + lane] = left_first ? stack_pack(nr.a, tr) : stack_pack(nl.a, tl);
+                    wstack[(sp++) * 64 + lane] = left_first ? nr.a : nl.a;
                     cur = left_first ? nl.a : nr.a;
                 }
             } else if (hl) {
@@ -1921,21 +1915,19 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
             take(r.inv.x); take(r.inv.y); take(r.inv.z);
             take(len_d); take(r.eps); take(bhz); take(bdist);
             if (thief) {
-                float tq;
-                const uint32_t entry = stack_unpack(wstack[vb * 64 + vic], tq);
+                const uint32_t entry = wstack[vb * 64 + vic];
                 refresh();
                 sp = bot = 0;
                 cur = entry;
-                has = !pruned(tq);
+                has = true;
             }
             if (spare && lane_rank(vm) < ni) ++bot;  // robbed
             __builtin_amdgcn_wave_barrier();
         }
-        if (!has && sp > bot) {  // an entry whose widened box lies beyond the best hit is dropped unloaded
-            float tq;
-            cur = stack_unpack(wstack[(--sp) * 64 + lane], tq);
+        if (!has && sp > bot) {
+            cur = wstack[(--sp) * 64 + lane];
             refresh();
-            has = !pruned(tq);  // tq <= the pushed child's tn_prune: pruned(tq) implies pruned(tn_prune)
+            has = true;
         }
         if (!has && sp == bot) sp = bot = 0;
         if (has && !(cur & kLeafRef)) {
@@ -1964,8 +1956,7 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
                     sp = bot = 0;
                 } else {
                     const bool first0 = o0 <= o1;
-                    wstack[(sp++) * 64 + lane] =
-                        first0 ? stack_pack(c1.u0, fmaxf(w1, 0.0f)) : stack_pack(c0.u0, fmaxf(w0, 0.0f));
+                    wstack[(sp++) * 64 + lane] = first0 ? c1.u0 : c0.u0;
                     cur = first0 ? c0.u0 : c1.u0;
                 }
             } else if (h0) {

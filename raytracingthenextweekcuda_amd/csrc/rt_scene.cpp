@@ -501,7 +501,10 @@ std::string HostScene::build_mesh_pairs() {
     // count - 1 and first triangle) in the low bits and the pushed child's entry distance, truncated,
     // in the rest, which lets a pop skip a subtree beyond the ray's best hit without loading it.
     auto bits = [](size_t n) { int b = 0; while (((size_t)1 << b) < n) ++b; return b; };
-    const int rb = 1 + std::max(bits(nodes.size() / 2 + 1), 4 + bits(std::max(tris.size(), objs.size()) + 1));
+    const int rb = 1 + std::max(bits(nodes.size() / 2 + 1), 4 + bits(tris.size() + 1));
+#ifndef RT_POP_PRUNE
+#define RT_POP_PRUNE 1  // 0 (A/B only): stack entries without the distance, every pop loads its pair
+#endif
     stack_ref_bits = RT_POP_PRUNE && 32 - rb >= 6 ? rb : 32;  // fewer than 6 distance bits would prune too little
     return "";
 }

@@ -56,9 +56,6 @@ constexpr uint32_t kSphereBvhMin = 16;
 // Per-lane LDS traversal stack depth; the builder rejects deeper trees, like
 // the reference's BVH_STACK_SIZE check (BVH.cpp:490-496, CUDAPathTracer.h:43).
 constexpr int kBvhStackDepth = 32;
-#ifndef RT_POP_PRUNE
-#define RT_POP_PRUNE 1  // 0 (A/B only): stack entries without the distance, every pop loads its pair
-#endif
 static_assert(sizeof(ObjRec) == 64, "ObjRec must be 64 B");
 
 // Triangle as prepared by prepareTriangleData (main.cu:334-349): v0, E1, E2.
