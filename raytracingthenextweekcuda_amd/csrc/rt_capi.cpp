@@ -723,7 +723,6 @@ rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& 
     const int depth = p->integrator == RT_INTEGRATOR_PATHTRACE ? std::max(c->pt_bvh.max_depth, c->pt_pair_depth)
                                                                 : c->scene.bvh_max_depth;
     L.stack_depth = depth > 0 ? depth : 1;
-    L.ref_bits = p->integrator == RT_INTEGRATOR_PATHTRACE ? 32 : c->scene.stack_ref_bits;
     L.pt_scale = c->pt_scale;
     L.pt_root_ref = c->pt_root_ref;
     return RT_OK;

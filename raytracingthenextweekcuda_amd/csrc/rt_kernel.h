@@ -50,8 +50,6 @@ struct RenderLaunch {
     int32_t stack_depth;      // BVH traversal stack entries per lane = the scene's BVH depth (>= 1): an
                               // ordered traversal holds at most one pending subtree per level below the
                               // root, so the LDS stacks are sized per scene (dynamic LDS)
-    int32_t ref_bits;         // mesh traversal stack entries: reference in the low ref_bits bits, the
-                              // entry distance truncated to the high 32 - ref_bits (32: none stored)
     float pt_scale;           // pathTrace: max |coordinate| of the triangles
     uint32_t pt_root_ref;     // pathTrace: the root's child-pair reference (rt_bvh.h cf_child_pairs)
     // Pixel output (Canvas.h:58-98): accumulate = 0 writes the mean color/spp to

@@ -365,28 +365,7 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
     float best = h.t;  // pruning bound for the current ray (its closestSoFar until a hit lands)
     uint32_t cur = root;  // pair index or leaf reference
     bool has = want;
-    int sp = 0, bot = 0;            // pending entries: wstack[k * 64 + lane], bot <= k < sp
-    // A stack entry is [entry distance, truncated: 32 - rb bits | compact reference: rb bits]
-    // (L.ref_bits; 32 = no distance): a popped entry whose child box starts beyond the ray's best
-    // hit is dropped without loading its pair record. The truncated distance is never above the
-    // true one, so only subtrees node_hit would reject at the pair load are dropped.
-    auto pack = [&](uint32_t ref, float tn) -> uint32_t {
-        const uint32_t rb = (uint32_t)launch_args().ref_bits;
-        if (rb >= 32u) return ref;
-        const uint32_t r = (ref & kLeafRef) ? (1u << (rb - 1u)) | (((ref >> 27) & 15u) << (rb - 5u)) | (ref & 0x07FFFFFFu)
-                                            : ref;
-        return r | ((__float_as_uint(tn) >> (rb - 1u)) << rb);  // tn >= 0 (node_hit clamps it)
-    };
-    auto unpack = [&](uint32_t e, float& tq) -> uint32_t {
-        const uint32_t rb = (uint32_t)launch_args().ref_bits;
-        if (rb >= 32u) {
-            tq = 0.0f;
-            return e;
-        }
-        tq = __uint_as_float((e >> rb) << (rb - 1u));
-        const uint32_t r = e & ((1u << rb) - 1u);
-        return (r >> (rb - 1u)) ? kLeafRef | (((r >> (rb - 5u)) & 15u) << 27) | (r & ((1u << (rb - 5u)) - 1u)) : r;
-    };
+    int sp = 0, bot = 0;            // pending references: wstack[k * 64 + lane], bot <= k < sp
     uint32_t qtail = 0, qdone = 0;  // wave-uniform positions in the pair queue W.slot (256 entries)
     constexpr uint32_t kQ = (uint32_t)kMaxRun * 64u;
     static_assert(kQ >= 256, "the pair queue holds 63 + 3 x 64 pairs");
@@ -434,21 +413,19 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             take(ri.x); take(ri.y); take(ri.z);
             take(best);
             if (thief) {
-                float tq;
-                cur = unpack(wstack[vt * 64 + vic], tq);
+                cur = wstack[vt * 64 + vic];
                 best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
                 sp = bot = 0;
-                has = !(tq > best * 1.00001f + 1e-30f);
+                has = true;
             }
             if (spare && lane_rank(vm) < ni) ++bot;  // robbed
             __builtin_amdgcn_wave_barrier();
         }
-        if (!has && sp > bot)  // the ray's best so far over all lanes (NaN while none: fminf keeps ours)
+        if (!has && sp > bot) {
+            cur = wstack[(--sp) * 64 + lane];
+            has = true;
+            // the ray's best so far over all lanes (NaN while none: fminf keeps ours)
             best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
-        while (!has && sp > bot) {  // pop until an entry that can still hold a hit (LDS reads only)
-            float tq;
-            cur = unpack(wstack[(--sp) * 64 + lane], tq);
-            has = !(tq > best * 1.00001f + 1e-30f);  // the child box starts beyond the best hit: dropped
         }
         if (!has && sp == bot) sp = bot = 0;
         if (has && !(cur & kLeafRef)) {
@@ -464,7 +441,7 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
                     sp = bot = 0;
                 } else {
                     const bool left_first = tl <= tr;
-                    wstack[(sp++) * 64 + lane] = left_first ? pack(nr.a, tr) : pack(nl.a, tl);
+                    wstack[(sp++) * 64 + lane] = left_first ? nr.a : nl.a;
                     cur = left_first ? nl.a : nr.a;
                 }
             } else if (hl) {
@@ -2409,8 +2386,7 @@ uint32_t kernel_build_flags() {
     RT_QUEUE_BLOCK_WAVES != 4
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
-#if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1) || \
-    (defined(RT_POP_PRUNE) && RT_POP_PRUNE != 1)
+#if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)
     f |= 4u;  // (host-side layout switches of rt_capi.cpp, passed to every TU through EXTRA)
 #endif
     return f;

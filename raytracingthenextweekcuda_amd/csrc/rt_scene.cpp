@@ -484,7 +484,6 @@ std::string HostScene::build_mesh_pairs() {
     if (nodes.size() & 1u) nodes.push_back(BvhNode{});
     // the LDS stacks are sized by what the traversals below may push (not the binary depth)
     bvh_max_depth = 0;
-    stack_ref_bits = 32;
     for (int k = 0; k < n_scan; ++k) {
         ObjRec& r = objs[k];
         if (!tree(r)) continue;
@@ -497,15 +496,6 @@ std::string HostScene::build_mesh_pairs() {
         bvh_max_depth = std::max(bvh_max_depth, pb.max_pairs);
         memcpy(&r.f[8], &root, 4);
     }
-    // The mesh traversal's stack entries hold a compact reference (a pair index, or a leaf's flag,
-    // count - 1 and first triangle) in the low bits and the pushed child's entry distance, truncated,
-    // in the rest, which lets a pop skip a subtree beyond the ray's best hit without loading it.
-    auto bits = [](size_t n) { int b = 0; while (((size_t)1 << b) < n) ++b; return b; };
-    const int rb = 1 + std::max(bits(nodes.size() / 2 + 1), 4 + bits(tris.size() + 1));
-#ifndef RT_POP_PRUNE
-#define RT_POP_PRUNE 1  // 0 (A/B only): stack entries without the distance, every pop loads its pair
-#endif
-    stack_ref_bits = RT_POP_PRUNE && 32 - rb >= 6 ? rb : 32;  // fewer than 6 distance bits would prune too little
     return "";
 }
 

@@ -145,7 +145,6 @@ struct HostScene {
     std::vector<BvhNode> nodes;
     std::vector<uint32_t> tri_orig;  // 2 per triangle: (mesh-local index, inverse map), see flatten()
     int bvh_max_depth = 0;
-    int stack_ref_bits = 32;  // bits a mesh traversal stack entry needs for its reference (RenderLaunch::ref_bits)
 
     // BVH builder (rt_set_bvh_builder): host Recurse, or its GPU restatement on
     // `bvh_device` (byte-identical; falls back to the host when it declines).
