@@ -629,7 +629,7 @@ rt_status rt_scene_info(const rt_ctx* c, int32_t out[8]) {
     if (!c->committed) return RT_ERR_STATE;
     for (int i = 0; i < 8; ++i) out[i] = 0;
     for (const rt::ObjRec& o : c->scene.objs) {
-        if (o.type == rt::kObjPlane) ++out[0];
+        if (rt::is_plane(o.type)) ++out[0];
         else if (o.type == rt::kObjSphere) ++out[1];
         else if (o.type == rt::kObjMovingSphere) ++out[2];
         else if (o.type == rt::kObjMesh) ++out[3];

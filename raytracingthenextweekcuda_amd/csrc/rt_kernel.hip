@@ -57,6 +57,16 @@ constexpr int kQueueBlockWaves = RT_QUEUE_BLOCK_WAVES;
 static_assert(kQueueBlockWaves == 1 || kQueueBlockWaves == 2 || kQueueBlockWaves == 4, "queue block waves");
 constexpr int block_waves(bool queue) { return queue ? kQueueBlockWaves : kWavesPerBlock; }
 
+#ifndef RT_TRIP_FLAT
+#define RT_TRIP_FLAT 0  // 1: the mesh traversal's pop, push and leaf steps as lane selects (A/B)
+#endif
+#ifndef RT_BOX_FLAT
+#define RT_BOX_FLAT 0  // 1: box_hit without early returns (A/B)
+#endif
+#ifndef RT_MERGE_SEL
+#define RT_MERGE_SEL 1  // 0: the ordered merge as a divergent branch (A/B)
+#endif
+
 struct Ray {
     v3 o, d;
     float time;
@@ -66,6 +76,24 @@ struct Ray {
 // and signs (Ray.h:10-16); tMin/tMax are ignored like the reference.
 __device__ __forceinline__ bool box_hit(const float* f, v3 o, v3 inv) {
     const bool sx = inv.x < 0.0f, sy = inv.y < 0.0f, sz = inv.z < 0.0f;
+#if RT_BOX_FLAT
+    // the same tests without early returns: a lane that fails an earlier test fails the result
+    // whatever the later ones give, so all are evaluated and or-ed (no divergent exits)
+    float tminx = ((sx ? f[3] : f[0]) - o.x) * inv.x;
+    float tmaxx = ((sx ? f[0] : f[3]) - o.x) * inv.x;
+    const float tminy = ((sy ? f[4] : f[1]) - o.y) * inv.y;
+    const float tmaxy = ((sy ? f[1] : f[4]) - o.y) * inv.y;
+    const float tminz = ((sz ? f[5] : f[2]) - o.z) * inv.z;
+    const float tmaxz = ((sz ? f[2] : f[5]) - o.z) * inv.z;
+    const bool f1 = (tminx > tmaxy) || (tminy > tmaxx);
+    tminx = tminy > tminx ? tminy : tminx;
+    tmaxx = tmaxy < tmaxx ? tmaxy : tmaxx;
+    const bool f2 = (tminx > tmaxz) || (tminz > tmaxx);
+    tminx = tminz > tminx ? tminz : tminx;
+    tmaxx = tmaxz < tmaxx ? tmaxz : tmaxx;
+    const bool f3 = (tminx < 0.0f) && (tmaxx < 0.0f);
+    return !(f1 || f2 || f3);
+#else
     float tminx = ((sx ? f[3] : f[0]) - o.x) * inv.x;
     float tmaxx = ((sx ? f[0] : f[3]) - o.x) * inv.x;
     float tminy = ((sy ? f[4] : f[1]) - o.y) * inv.y;
@@ -84,6 +112,7 @@ __device__ __forceinline__ bool box_hit(const float* f, v3 o, v3 inv) {
         if (t < 0.0f) return false;
     }
     return true;
+#endif
 }
 
 // Conservative BVH node test (boxes are inflated at build time; NaN slabs from
@@ -106,6 +135,15 @@ __device__ __forceinline__ bool sphere_root(v3 o, v3 d, v3 c, float r, float tmi
     float hb = dot(oc, d);
     float cc = dot(oc, oc) - r * r;
     float disc = hb * hb - a * cc;
+#if RT_TRIP_FLAT
+    // both roots evaluated, the choice made with lane selects (no divergent exits)
+    const float inva = fdiv(1.0f, a);
+    const float sq = fsqrt(disc);  // (NaN where disc < 0: not used then)
+    const float t1 = (-hb - sq) * inva, t2 = (-hb + sq) * inva;
+    const bool bad1 = t1 < tmin || tmax < t1, bad2 = t2 < tmin || tmax < t2;
+    root = bad1 ? t2 : t1;
+    return (disc > kFltEpsilon) && !(bad1 && bad2);
+#else
     if (!(disc > kFltEpsilon)) return false;
     float inva = fdiv(1.0f, a);
     float sq = fsqrt(disc);
@@ -116,6 +154,7 @@ __device__ __forceinline__ bool sphere_root(v3 o, v3 d, v3 c, float r, float tmi
     }
     root = t;
     return true;
+#endif
 }
 
 // MovingSphere::center (Sphere.cu:75-78).
@@ -139,10 +178,10 @@ __device__ __forceinline__ float tri_t(const TriRec& tr, v3 o, v3 d) {
     float t = coef * dot(s2, e2);
     float b1 = coef * dot(s1, s);
     float b2 = coef * dot(s2, d);
-    if (((t >= kFltEpsilon) && (t >= kTMin)) && (b1 >= kFltEpsilon) && (b2 >= kFltEpsilon) &&
-        ((1.0f - b1 - b2) >= kFltEpsilon))
-        return t;
-    return kNo;
+    // every test evaluated and the lane masks and-ed (no short-circuit branches: the same result)
+    const bool ok = (t >= kFltEpsilon) & (t >= kTMin) & (b1 >= kFltEpsilon) & (b2 >= kFltEpsilon) &
+                    ((1.0f - b1 - b2) >= kFltEpsilon);
+    return ok ? t : kNo;
 }
 
 // tri_t for a pair already known to pass the backface cull.
@@ -156,10 +195,10 @@ __device__ __forceinline__ float tri_t_culled(const TriRec& tr, v3 o, v3 d) {
     float t = coef * dot(s2, e2);
     float b1 = coef * dot(s1, s);
     float b2 = coef * dot(s2, d);
-    if (((t >= kFltEpsilon) && (t >= kTMin)) && (b1 >= kFltEpsilon) && (b2 >= kFltEpsilon) &&
-        ((1.0f - b1 - b2) >= kFltEpsilon))
-        return t;
-    return kNo;
+    // every test evaluated and the lane masks and-ed (no short-circuit branches: the same result)
+    const bool ok = (t >= kFltEpsilon) & (t >= kTMin) & (b1 >= kFltEpsilon) & (b2 >= kFltEpsilon) &
+                    ((1.0f - b1 - b2) >= kFltEpsilon);
+    return ok ? t : kNo;
 }
 
 // Closest-hit state with the reference's sequential tie rule (hit(),
@@ -205,6 +244,16 @@ struct Hit {
     __device__ __forceinline__ void merge_seq(float tc, uint32_t order, bool sphere, int32_t o, int32_t tr) {
         if constexpr (!kOrdered) {
             merge(tc, order, sphere, o, tr);
+        } else if (RT_MERGE_SEL) {
+            // the same updates as selects on the compare's lane mask (VALU), without the divergent
+            // branch's exec-mask saves and restores (scalar instructions)
+            const bool lt = tc < t, eq = sphere && tc == t;
+            ms_obj = lt ? (sphere ? o : -1) : eq ? o : ms_obj;
+            ms = (lt || eq) ? order : ms;
+            t = lt ? tc : t;
+            mi = lt ? order : mi;
+            obj = lt ? o : obj;
+            tri = lt ? tr : tri;
         } else if (tc < t) {
             t = tc;
             mi = order;
@@ -421,6 +470,20 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             if (spare && lane_rank(vm) < ni) ++bot;  // robbed
             __builtin_amdgcn_wave_barrier();
         }
+#if RT_TRIP_FLAT
+        {  // pop as lane selects (the read of slot 0 by lanes that do not pop is discarded)
+            const bool pop = !has && sp > bot;
+            const uint32_t v = wstack[(pop ? sp - 1 : 0) * 64 + lane];
+            const float kb = __uint_as_float((uint32_t)(W.key[owner] >> 32));
+            cur = pop ? v : cur;
+            best = pop ? fminf(best, kb) : best;
+            sp -= pop ? 1 : 0;
+            has = has || pop;
+            const bool empty = !has && sp == bot;
+            sp = empty ? 0 : sp;
+            bot = empty ? 0 : bot;
+        }
+#else
         if (!has && sp > bot) {
             cur = wstack[(--sp) * 64 + lane];
             has = true;
@@ -428,12 +491,26 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
         }
         if (!has && sp == bot) sp = bot = 0;
+#endif
         if (has && !(cur & kLeafRef)) {
             const BvhNode nl = nodes[2 * (size_t)cur], nr = nodes[2 * (size_t)cur + 1];
             cnt.node_visits += 2;
             float tl, tr;
             const bool hl = node_hit(nl, ro, ri, best, tl);
             const bool hr = node_hit(nr, ro, ri, best, tr);
+#if RT_TRIP_FLAT
+            // as lane selects; a lane that does not push writes the spare slot `cap` (never read)
+            const bool both = hl && hr, lf = tl <= tr;
+            const bool ovf = both && sp + 1 > cap;
+            if (__builtin_expect(__ballot(ovf) != 0, 0))
+                if (ovf) cnt.overflow();
+            const bool push = both && !ovf;
+            wstack[(push ? sp : cap) * 64 + lane] = lf ? nr.a : nl.a;
+            sp = ovf ? 0 : sp + (push ? 1 : 0);
+            bot = ovf ? 0 : bot;
+            cur = both ? (lf ? nl.a : nr.a) : (hl ? nl.a : nr.a);
+            has = (hl || hr) && !ovf;
+#else
             if (hl && hr) {
                 if (sp + 1 > cap) {
                     cnt.overflow();
@@ -451,8 +528,21 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             } else {
                 has = false;
             }
+#endif
         }
         uint32_t lk = 0, ln = 0;  // this trip's leaf pairs: triangles lk .. lk + ln - 1
+#if RT_TRIP_FLAT
+        {
+            const bool leaf = has && (cur & kLeafRef);
+            const uint32_t nt = ((cur >> 27) & 15u) + 1u;
+            lk = cur & 0x07FFFFFFu;
+            ln = leaf ? (nt < 3u ? nt : 3u) : 0u;
+            // a larger leaf keeps this lane for more trips
+            cur = leaf && nt > 3u ? (kLeafRef | ((nt - 4u) << 27) | (lk + 3u)) : cur;
+            has = has && !(leaf && nt <= 3u);
+            cnt.tri_tests += ln;
+        }
+#else
         if (has && (cur & kLeafRef)) {
             const uint32_t nt = ((cur >> 27) & 15u) + 1u;
             lk = cur & 0x07FFFFFFu;
@@ -463,6 +553,7 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
                 has = false;
             cnt.tri_tests += ln;
         }
+#endif
         // enqueue the leaf pairs (converged): a lane's slots follow those of the lanes below it
         const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
         if (b1) {
@@ -559,24 +650,22 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
         const v3 ro{__shfl(o.x, src, 64), __shfl(o.y, src, 64), __shfl(o.z, src, 64)};
         const v3 rd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
         const float rt0 = __shfl(t0, src, 64);
-        if (act) {
-            const float t = tri_t_culled(tris[tri], ro, rd);
-            if (t <= rt0) atomicMin(&W.key[src], ((unsigned long long)__float_as_uint(t) << 32) | tri);
-        }
+        // inactive lanes test the pair of slot 0 (a valid triangle) and drop the result: no divergent
+        // branch around the loads
+        const float t = tri_t_culled(tris[tri], ro, rd);
+        if (act && t <= rt0) atomicMin(&W.key[src], ((unsigned long long)__float_as_uint(t) << 32) | tri);
         tested += count;
     };
     for (uint32_t p0 = 0; p0 < total; p0 += 64) {
         const uint32_t p = p0 + (uint32_t)lane;
         const bool act = p < total;
-        const uint32_t r = act ? (m > 1u ? __umulhi(p, magic) : p) : 0u;
+        const uint32_t pc = act ? p : 0u;  // inactive lanes read pair 0 (valid) and keep nothing
+        const uint32_t r = m > 1u ? __umulhi(pc, magic) : pc;
         const uint32_t e = W.slot[r];
         const int src = (int)(e & 63u);
         const v3 rd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
-        bool keep = false;
-        if (act) {
-            const TriRec& tr = tris[(e >> 6) + (p - r * m)];
-            keep = !(dot(rd, v3{tr.nx, tr.ny, tr.nz}) > kFltEpsilon);  // TriangleMesh.cu:72
-        }
+        const TriRec& tr = tris[(e >> 6) + (pc - r * m)];
+        const bool keep = act && !(dot(rd, v3{tr.nx, tr.ny, tr.nz}) > kFltEpsilon);  // TriangleMesh.cu:72
         const uint64_t km = __ballot(keep);
         if (keep) W.ring[(queued + (uint32_t)lane_rank(km)) & 127u] = (uint16_t)p;
         queued += (uint32_t)__popcll(km);
@@ -659,16 +748,47 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
     };
     for (;;) {
         if (__ballot(has || sp > 0) == 0) break;
+#if RT_TRIP_FLAT
+        {  // (as mesh_bvh_pairs)
+            const bool pop = !has && sp > 0;
+            const uint32_t v = wstack[(pop ? sp - 1 : 0) * 64 + lane];
+            cur = pop ? v : cur;
+            sp -= pop ? 1 : 0;
+            has = has || pop;
+        }
+#else
         if (!has && sp > 0) {
             cur = wstack[(--sp) * 64 + lane];
             has = true;
         }
+#endif
         if (has && !(cur & kLeafRef)) {
             const BvhNode nl = nodes[2 * (size_t)cur], nr = nodes[2 * (size_t)cur + 1];
             cnt.node_visits += 2;
             float tl, tr;
             const bool hl = node_hit(nl, o, inv, best, tl);
             const bool hr = node_hit(nr, o, inv, best, tr);
+#if RT_TRIP_FLAT
+            const bool both = hl && hr, lf = tl <= tr;
+            const bool ovf = both && sp + 1 > cap;
+            if (__builtin_expect(__ballot(ovf) != 0, 0))
+                if (ovf) cnt.overflow();
+            const bool push = both && !ovf;
+            wstack[(push ? sp : cap) * 64 + lane] = lf ? nr.a : nl.a;
+            sp = ovf ? 0 : sp + (push ? 1 : 0);
+            cur = both ? (lf ? nl.a : nr.a) : (hl ? nl.a : nr.a);
+            has = (hl || hr) && !ovf;
+        }
+        uint32_t lk = 0, ln = 0;
+        {
+            const bool leaf = has && (cur & kLeafRef);
+            const uint32_t nt = ((cur >> 27) & 15u) + 1u;
+            lk = cur & 0x07FFFFFFu;
+            ln = leaf ? (nt < 3u ? nt : 3u) : 0u;
+            cur = leaf && nt > 3u ? (kLeafRef | ((nt - 4u) << 27) | (lk + 3u)) : cur;
+            has = has && !(leaf && nt <= 3u);
+        }
+#else
             if (hl && hr) {
                 if (sp + 1 > cap) {
                     cnt.overflow();
@@ -697,6 +817,7 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
             else
                 has = false;
         }
+#endif
         const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
         if (b1) {
             const uint32_t at = qtail + (uint32_t)(lane_rank(b1) + lane_rank(b2) + lane_rank(b3));
@@ -804,6 +925,44 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
 // each updating the Hit state). Both were measured slower on the other scenes.
 // kParts (BVH kernels): 1 = the scene has BVH meshes, 2 = sphere groups; the other traversal is
 // not compiled in (rt_capi.cpp picks the variant from the committed scene).
+#ifndef RT_SCAN_PAIRS
+#define RT_SCAN_PAIRS 1  // 0: one prefetched record, copied per object (A/B)
+#endif
+#ifndef RT_PLANE_AXIAL
+#define RT_PLANE_AXIAL 1  // 0: every plane through the general dot products (A/B)
+#endif
+template <int K>
+__device__ __forceinline__ float axis(v3 v) {
+    return K == 0 ? v.x : K == 1 ? v.y : v.z;
+}
+
+// Plane::hit (Plane.cu:4-52) for a kObjPlaneAxial record: normal n = +-1 on the orientation's normal
+// axis K and +-0 on the in-plane axes A, B. Plane.cu's den = dot(n, d) and num = dot(p - o, n) are
+// (0 * d_A + 0 * d_B) + n_K * d_K and the like: exactly n_K * d_K and (p_K - o_K) * n_K whenever those are
+// non-zero, so t is the same float. A zero den or num (of either sign) fails |den| > tMin (or
+// den > tMin) or t >= tMin in both forms. Where the full dot products are NaN (a NaN or inf d_A, d_B,
+// o_A or o_B) these are not, but then the hit point's coordinate on that axis, o_A + d_A * t, is NaN or
+// infinite and fails the open bounds test: the candidate is NaN (none) in both forms.
+template <int K, int A, int B>
+__device__ __forceinline__ float plane_axial(const ObjRec& ob, v3 o, v3 d) {
+    const float* f = ob.f;
+    const float nk = f[3 + K];
+    const float den = nk * axis<K>(d);
+    const bool proceed = ob.u1 ? (fabsf(den) > kTMin) : (den > kTMin);
+    const float num = (f[K] - axis<K>(o)) * nk;
+#if RT_DIV_NR
+    float t = div_y(num, den, rcp_nr(den));  // domain and fallback: closest_hit's general plane
+    if (__builtin_expect(__ballot(proceed && !(fmaxf(fabsf(num), fabsf(den)) < 0x1p100f)) != 0, 0))
+        t = fdiv(num, den);
+#else
+    const float t = fdiv(num, den);
+#endif
+    const float pa = axis<A>(o) + axis<A>(d) * t;
+    const float pb = axis<B>(o) + axis<B>(d) * t;
+    const bool in = (pa > f[6]) & (pa < f[7]) & (pb > f[8]) & (pb < f[9]);
+    return (proceed & (t >= kTMin) & in) ? t : __builtin_nanf("");
+}
+
 template <bool kBvh, bool kMed = false, bool kSph = true, int kParts = 3>
 __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v3 inv, bool live,
                                            Rng& rng, WaveLds& W, uint32_t* stack, int lane,
@@ -818,10 +977,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
     constexpr bool kPf = !kMed;
     // no sphere groups: merges come in scan order (the media variant measured slower with it)
     constexpr bool kOrd = !kBvh && !kMed;
-    ObjRec cur = load_obj(S.objs, 0);
-    for (int i = 0; i < n; ++i) {
-        const ObjRec ob = kPf ? cur : load_obj(S.objs, i);
-        if (kPf && i + 1 < n) cur = load_obj(S.objs, i + 1);
+    auto visit = [&](const ObjRec& ob, const int i) {
         const float* f = ob.f;
         float tc = __builtin_nanf("");  // kMed: this object's candidate, merged once below
         bool tsph = false;
@@ -833,7 +989,14 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 h.merge_seq<kOrd>(t, ob.order, sphere, i, -1);
             }
         };
-        if (ob.type == kObjPlane) {
+        // wave-uniform dispatch on the record type; the reference's scenes are mostly axial planes
+        if (RT_PLANE_AXIAL && ob.type == kObjPlaneAxial) {
+            cand(plane_axial<2, 0, 1>(ob, o, d), false);  // XY
+        } else if (RT_PLANE_AXIAL && ob.type == kObjPlaneAxial + 1) {
+            cand(plane_axial<0, 1, 2>(ob, o, d), false);  // YZ
+        } else if (RT_PLANE_AXIAL && ob.type == kObjPlaneAxial + 2) {
+            cand(plane_axial<1, 0, 2>(ob, o, d), false);  // XZ
+        } else if (is_plane(ob.type)) {
             // Plane::hit (Plane.cu:4-52); t is only used when `proceed` holds.
             const v3 nrm{f[3], f[4], f[5]};
             const float den = dot(nrm, d);
@@ -896,6 +1059,28 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                                  cnt, S.stack_cap);
         }
         if constexpr (kMed) h.merge_seq<kOrd>(tc, ob.order, tsph, i, -1);  // NaN: no candidate
+    };
+    if constexpr (kPf && RT_SCAN_PAIRS) {
+        // Records prefetched one object ahead, in two alternating register sets (the scan unrolled by
+        // two): each load lands in the registers of a record already visited, so no record is copied
+        // between scalar registers per object (a single prefetched record costs 14 s_mov per object,
+        // and the scalar unit, shared by the CU's four SIMDs, is as loaded as the VALU in this kernel).
+        // The clamped index keeps every load in bounds; the loaded copy past the end is not visited.
+        ObjRec ra = load_obj(S.objs, 0);
+        for (int i = 0; i < n; i += 2) {
+            const ObjRec rb = load_obj(S.objs, i + 1 < n ? i + 1 : i);
+            visit(ra, i);
+            if (i + 1 >= n) break;
+            ra = load_obj(S.objs, i + 2 < n ? i + 2 : i + 1);
+            visit(rb, i + 1);
+        }
+    } else {
+        ObjRec cur = load_obj(S.objs, 0);
+        for (int i = 0; i < n; ++i) {
+            const ObjRec ob = kPf ? cur : load_obj(S.objs, i);
+            if (kPf && i + 1 < n) cur = load_obj(S.objs, i + 1);
+            visit(ob, i);
+        }
     }
     h.finish();
     return h;
@@ -1319,7 +1504,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         W.grp_s[lane] = 0;
         W.grp_m[lane] = 0;
     }
-    uint32_t* stack = kBvh ? dyn_stacks + (size_t)wave * L.stack_depth * 64 + lane : nullptr;
+    uint32_t* stack = kBvh ? dyn_stacks + (size_t)wave * (L.stack_depth + RT_TRIP_FLAT) * 64 + lane : nullptr;
 
     // Lane layout: SP = lanes_per_pixel adjacent lanes share one pixel and split
     // its samples (sub-lane c takes samples c, c+SP, c+2SP, ...). A wave covers
@@ -1494,7 +1679,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             constexpr bool kAnySph = kSph || kMed;
             if ((kMed || (kBvh && kSph)) && ob.type == kObjMedium) {
                 outward = v3{1.0f, 0.0f, 0.0f};  // arbitrary; isotropic scatter ignores it
-            } else if (ob.type == kObjPlane) {
+            } else if (is_plane(ob.type)) {
                 outward = v3{f[3], f[4], f[5]};
             } else if (kAnySph && ob.type == kObjSphere) {
                 outward = divs(sub(p, v3{f[0], f[1], f[2]}), f[3]);
@@ -2263,8 +2448,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
 }
 
 // Dynamic LDS of a traversal kernel: the per-lane stacks of the block's `bw` waves.
-static size_t stack_bytes(const RenderLaunch& L, int bw) {
-    return (size_t)bw * (size_t)(L.stack_depth > 0 ? L.stack_depth : 1) * 64 * sizeof(uint32_t);
+// `spare`: one more slot per lane past the stack (RT_TRIP_FLAT: the render kernels' unconditional push target)
+static size_t stack_bytes(const RenderLaunch& L, int bw, int spare = 0) {
+    return (size_t)bw * (size_t)((L.stack_depth > 0 ? L.stack_depth : 1) + spare) * 64 * sizeof(uint32_t);
 }
 
 hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const RenderLaunch& L,
@@ -2307,7 +2493,7 @@ int queue_blocks(int n_cu, uint32_t variant, const RenderLaunch& L) {
             lds = (size_t)bw * (sizeof(WaveLds) + sizeof(CamSlots));
             break;
         default:
-            lds = (size_t)bw * sizeof(WaveLds) + stack_bytes(L, bw);
+            lds = (size_t)bw * sizeof(WaveLds) + stack_bytes(L, bw, RT_TRIP_FLAT);
     }
     const int fit = (int)((size_t)160 * 1024 / (lds ? lds : 1));
     return n_cu * std::max(1, std::min(4 * waves / bw, fit));
@@ -2383,7 +2569,7 @@ uint32_t kernel_build_flags() {
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
-    RT_QUEUE_BLOCK_WAVES != 4
+    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_SCAN_PAIRS != 1 || RT_MERGE_SEL != 1 || RT_BOX_FLAT != 0 || RT_TRIP_FLAT != 0
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)
@@ -2405,7 +2591,7 @@ hipError_t launch_render(uint32_t variant, const SceneArgs& sc, const CamRec* ca
                          unsigned long long* counters, hipStream_t stream, hipEvent_t main_done) {
     const int bw = block_waves(L.queue != 0);
     const dim3 block(64 * bw);
-    const size_t lds = stack_bytes(L, bw);
+    const size_t lds = stack_bytes(L, bw, RT_TRIP_FLAT);
     dim3 grid;
     if (L.queue) {
         if (L.n_items == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;

@@ -411,6 +411,11 @@ std::string HostScene::flatten() {
         r.f[7] = pa + ea;
         r.f[8] = pb - eb;
         r.f[9] = pb + eb;
+        const int k = r.u0 == 0u ? 2 : r.u0 == 1u ? 0 : 1;  // the orientation's normal axis
+        const float nk = r.f[3 + k];
+        if ((nk == 1.0f || nk == -1.0f) && r.f[3 + (k + 1) % 3] == 0.0f && r.f[3 + (k + 2) % 3] == 0.0f &&
+            r.u0 < 3u)
+            r.type = kObjPlaneAxial + r.u0;
     }
     n_scan = (int)objs.size();
     const std::string err = group_spheres();

@@ -25,8 +25,14 @@ enum ObjType : uint32_t {
     kObjPlane = 2,
     kObjMesh = 3,
     kObjSphereGroup = 4,  // BVH over (moving) spheres: u0 = first member, u1 = count, u2 = root, f[8] = root pair ref
-    kObjMedium = 5        // constant medium in a cube: f = (center - extend) xyz, (center + extend) xyz, -1/density; u0 = slot
+    kObjMedium = 5,       // constant medium in a cube: f = (center - extend) xyz, (center + extend) xyz, -1/density; u0 = slot
+    // A plane whose normal is (0, 0, +-1) for XY, (+-1, 0, 0) for YZ, (0, +-1, 0) for XZ (every plane of the
+    // reference's scenes): kObjPlaneAxial + orientation, the record otherwise a kObjPlane one. The kernel's
+    // Plane::hit then forms the two dot products from their one non-zero term (rt_kernel.hip plane_axial),
+    // and the scan dispatches on the type alone.
+    kObjPlaneAxial = 6    // 6: XY, 7: YZ, 8: XZ
 };
+RT_HD bool is_plane(uint32_t type) { return type == kObjPlane || (type - kObjPlaneAxial) < 3u; }
 
 // One hitable (Sphere.h, Plane.h, TriangleMesh.h). Cube is flattened into its
 // six planes at build time: Cube::hit (Cube.cu:10-23) is a closest scan over its
