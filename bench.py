@@ -490,6 +490,10 @@ def build_line(args, agg: dict, world: int, cpu=None) -> dict:
     achieved = valu_launch / (t_iso * 1e-3) / 1e9 if vp and not vp_bad else None
     achieved_ovl = valu_launch / (ms_frame * 1e-3) / 1e9 if vp and not vp_bad else None
     lane_u = vp.get("valu_lane_util") if vp and not vp_bad else None
+    # the scalar unit (one per CU, shared by its four SIMDs): SALU instructions of the same
+    # kernel per launch / (CUs x 2.4 GHz x the isolated kernel time)
+    salu_seg = vp.get("salu_insts_per_segment") if vp and not vp_bad else None
+    salu_frac = salu_seg * seg_launch / (agg["n_cu"] * 2.4e9 * t_iso * 1e-3) if salu_seg else None
     tp = load_pmc_traffic(workload)
     tp_bad = profile_check(tp, agg["variant"], sha)
     traffic = float(tp["hbm_bytes_per_launch"]) if tp and not tp_bad else None
@@ -542,6 +546,9 @@ def build_line(args, agg: dict, world: int, cpu=None) -> dict:
             # frac into the fraction of the chip's lane-operations that did useful work
             "valu_lane_util": round(lane_u, 4) if lane_u else None,
             "useful_frac": round(achieved / valu_peak * lane_u, 4) if achieved and lane_u else None,
+            # the co-bound: scalar instructions against one per CU per cycle
+            "salu_insts_per_segment": round(salu_seg, 3) if salu_seg else None,
+            "salu_frac": round(salu_frac, 4) if salu_frac else None,
             "traffic": traffic,
             # the isolated launch's megakernel time (library event pair, combine pass excluded)
             "kernel_ms": round(t_iso, 4),
@@ -562,7 +569,9 @@ def build_line(args, agg: dict, world: int, cpu=None) -> dict:
                      "excluded - what rocprofv3's kernel trace measures); frac_overlapped divides by the timed "
                      "frame time instead (two launches in flight); peak = CUs x 4 SIMDs x 2.4 GHz / 2 cycles per "
                      "wave64 VALU op; useful_frac = frac x valu_lane_util (the same pass's SQ_THREAD_CYCLES_VALU "
-                     "/ 64 / SQ_ACTIVE_INST_VALU: active lanes per issued instruction). traffic = HBM-side bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, "
+                     "/ 64 / SQ_ACTIVE_INST_VALU: active lanes per issued instruction); salu_frac = SQ_INSTS_SALU of "
+                     "the same kernel per launch / (CUs x 2.4 GHz x kernel_ms): the CU's one scalar ALU, which "
+                     "the scan kernels load as much as their VALU (DESIGN 5). traffic = HBM-side bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, "
                      "profiles/pmc_traffic.json), hbm_frac its share of 8 TB/s; a profile of another kernel "
                      "symbol or other kernel sources is not used (profile_mismatch); record_* = SURVEY 8(d)'s "
                      "cache-served record-byte model"),

@@ -591,15 +591,18 @@ static rt_status rt_commit_impl(rt_ctx* c) {
     RT_HIP(c, hipSetDevice(c->device));
     free_device(c);
     const auto& S = c->scene;
-    auto up = [&](auto** dst, const auto& vec) -> hipError_t {
-        size_t bytes = vec.size() * sizeof(vec[0]);
+    // `pad` zeroed bytes after the table: the scan kernels prefetch the record after the last one
+    auto up = [&](auto** dst, const auto& vec, size_t pad = 0) -> hipError_t {
+        size_t bytes = vec.size() * sizeof(vec[0]) + pad;
         if (bytes == 0) bytes = 64;  // keep a valid pointer for empty tables
         hipError_t err = hipMalloc((void**)dst, bytes);
         if (err != hipSuccess) return err;
-        if (!vec.empty()) err = hipMemcpy(*dst, vec.data(), vec.size() * sizeof(vec[0]), hipMemcpyHostToDevice);
+        if (pad) err = hipMemset((char*)*dst + vec.size() * sizeof(vec[0]), 0, pad);
+        if (err == hipSuccess && !vec.empty())
+            err = hipMemcpy(*dst, vec.data(), vec.size() * sizeof(vec[0]), hipMemcpyHostToDevice);
         return err;
     };
-    RT_HIP(c, up(&c->d_objs, S.objs));
+    RT_HIP(c, up(&c->d_objs, S.objs, sizeof(rt::ObjRec)));
     RT_HIP(c, up(&c->d_tris, S.tris));
     RT_HIP(c, up(&c->d_mats, S.mats));
     RT_HIP(c, up(&c->d_nodes, S.nodes));

@@ -58,7 +58,13 @@ static_assert(kQueueBlockWaves == 1 || kQueueBlockWaves == 2 || kQueueBlockWaves
 constexpr int block_waves(bool queue) { return queue ? kQueueBlockWaves : kWavesPerBlock; }
 
 #ifndef RT_TRIP_FLAT
-#define RT_TRIP_FLAT 0  // 1: the mesh traversal's pop, push and leaf steps as lane selects (A/B)
+#define RT_TRIP_FLAT 1  // 0: the mesh traversal's pop, push and leaf steps as divergent branches (A/B)
+#endif
+#ifndef RT_SPH_TRIP_FLAT
+#define RT_SPH_TRIP_FLAT 0  // 1: the same for the sphere-group traversal (A/B; measured slower)
+#endif
+#ifndef RT_SPH_ROOT_FLAT
+#define RT_SPH_ROOT_FLAT 0  // 1: sphere_root without early exits (A/B)
 #endif
 #ifndef RT_BOX_FLAT
 #define RT_BOX_FLAT 0  // 1: box_hit without early returns (A/B)
@@ -135,7 +141,7 @@ __device__ __forceinline__ bool sphere_root(v3 o, v3 d, v3 c, float r, float tmi
     float hb = dot(oc, d);
     float cc = dot(oc, oc) - r * r;
     float disc = hb * hb - a * cc;
-#if RT_TRIP_FLAT
+#if RT_SPH_ROOT_FLAT
     // both roots evaluated, the choice made with lane selects (no divergent exits)
     const float inva = fdiv(1.0f, a);
     const float sq = fsqrt(disc);  // (NaN where disc < 0: not used then)
@@ -748,7 +754,7 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
     };
     for (;;) {
         if (__ballot(has || sp > 0) == 0) break;
-#if RT_TRIP_FLAT
+#if RT_SPH_TRIP_FLAT
         {  // (as mesh_bvh_pairs)
             const bool pop = !has && sp > 0;
             const uint32_t v = wstack[(pop ? sp - 1 : 0) * 64 + lane];
@@ -768,7 +774,7 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
             float tl, tr;
             const bool hl = node_hit(nl, o, inv, best, tl);
             const bool hr = node_hit(nr, o, inv, best, tr);
-#if RT_TRIP_FLAT
+#if RT_SPH_TRIP_FLAT
             const bool both = hl && hr, lf = tl <= tr;
             const bool ovf = both && sp + 1 > cap;
             if (__builtin_expect(__ballot(ovf) != 0, 0))
@@ -948,7 +954,10 @@ __device__ __forceinline__ float plane_axial(const ObjRec& ob, v3 o, v3 d) {
     const float* f = ob.f;
     const float nk = f[3 + K];
     const float den = nk * axis<K>(d);
-    const bool proceed = ob.u1 ? (fabsf(den) > kTMin) : (den > kTMin);
+    // twoSide ? |den| > tMin : den > tMin, with u1 = the bits of 1.0f (two-sided) or 0 (rt_scene.cpp):
+    // max(|den| * 1, den) = |den|; max(|den| * 0, den) > tMin iff den > tMin (+0 or NaN against den,
+    // and fmaxf returns den for a NaN first operand); a NaN den fails both. No scalar select.
+    const bool proceed = fmaxf(fabsf(den) * __uint_as_float(ob.u1), den) > kTMin;
     const float num = (f[K] - axis<K>(o)) * nk;
 #if RT_DIV_NR
     float t = div_y(num, den, rcp_nr(den));  // domain and fallback: closest_hit's general plane
@@ -1065,13 +1074,14 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
         // two): each load lands in the registers of a record already visited, so no record is copied
         // between scalar registers per object (a single prefetched record costs 14 s_mov per object,
         // and the scalar unit, shared by the CU's four SIMDs, is as loaded as the VALU in this kernel).
-        // The clamped index keeps every load in bounds; the loaded copy past the end is not visited.
+        // The record after the last one is read but not visited (rt_capi.cpp allocates the table with one
+        // record of padding).
         ObjRec ra = load_obj(S.objs, 0);
         for (int i = 0; i < n; i += 2) {
-            const ObjRec rb = load_obj(S.objs, i + 1 < n ? i + 1 : i);
+            const ObjRec rb = load_obj(S.objs, i + 1);
             visit(ra, i);
             if (i + 1 >= n) break;
-            ra = load_obj(S.objs, i + 2 < n ? i + 2 : i + 1);
+            ra = load_obj(S.objs, i + 2);
             visit(rb, i + 1);
         }
     } else {
@@ -2569,7 +2579,7 @@ uint32_t kernel_build_flags() {
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
-    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_SCAN_PAIRS != 1 || RT_MERGE_SEL != 1 || RT_BOX_FLAT != 0 || RT_TRIP_FLAT != 0
+    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_SCAN_PAIRS != 1 || RT_MERGE_SEL != 1 || RT_BOX_FLAT != 0 || RT_TRIP_FLAT != 1 || RT_SPH_TRIP_FLAT != 0 || RT_SPH_ROOT_FLAT != 0
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)

@@ -414,8 +414,10 @@ std::string HostScene::flatten() {
         const int k = r.u0 == 0u ? 2 : r.u0 == 1u ? 0 : 1;  // the orientation's normal axis
         const float nk = r.f[3 + k];
         if ((nk == 1.0f || nk == -1.0f) && r.f[3 + (k + 1) % 3] == 0.0f && r.f[3 + (k + 2) % 3] == 0.0f &&
-            r.u0 < 3u)
+            r.u0 < 3u) {
             r.type = kObjPlaneAxial + r.u0;
+            r.u1 = r.u1 ? 0x3F800000u : 0u;  // twoSide as the float 1 or 0 (still non-zero iff two-sided)
+        }
     }
     n_scan = (int)objs.size();
     const std::string err = group_spheres();

@@ -41,7 +41,7 @@ struct alignas(16) ObjRec {
     uint32_t type;
     uint32_t material;
     uint32_t u0;  // plane: orientation | mesh: first triangle
-    uint32_t u1;  // plane: twoSide     | mesh: triangle count
+    uint32_t u1;  // plane: twoSide (axial kinds: the bits of 1.0f or 0) | mesh: triangle count
     uint32_t u2;     // mesh / sphere group: BVH root node index, or kNoBvh (brute-force scan)
     uint32_t order;  // position in the reference's sequential hit() scan (tie rule)
     // sphere: center xyz, radius

@@ -3,9 +3,10 @@
 #   TESTS=1   pytest -m gpu + smoke()
 #   BENCH=1   the default bench line (config 2, frame overlap, CPU baseline)
 #   SCENES    bench lines of these workloads (no CPU baseline); ALT = A/B libraries run after each
-#   VALU      SQ_INSTS_VALU (+ lane utilisation, wait shares) passes of these workloads (--no-overlap,
+#   VALU      SQ_INSTS_VALU (+ lane utilisation, wait shares) and SQ_INSTS_SALU passes of these workloads (--no-overlap,
 #             BENCH_ARGS appended: --in-flight-layout for the timed layout), for profiles/valu_issue.json
 #   PROBE=1   tools/valu_probe under SQ counters with 64 and 16 active lanes (lane-utilisation calibration)
+#   SPROBE=1  tools/valu_probe's issue rates: VALU, SALU and both, at 4 and 8 waves/SIMD
 #   TRAFFIC   FETCH_SIZE and WRITE_SIZE passes (separate runs), for profiles/pmc_traffic.json
 #   PROF      rocprofv3 --kernel-trace --stats of these workloads (--no-overlap)
 #   MULTI=1   examples/multigpu (RCCL through the C ABI, N = 1 on this box)
@@ -46,9 +47,18 @@ if [ "${PROBE:-0}" = "1" ] && [ -x ./tools/valu_probe ]; then  # lane-utilisatio
     stop_if_fatal $? probe_lanes_$a
   done
 fi
+if [ "${SPROBE:-0}" = "1" ] && [ -x ./tools/valu_probe ]; then  # issue-rate probes: VALU, SALU, both (4 and 8 waves/SIMD)
+  for w in 4 8; do for m in 0 1 2 3; do
+    timeout -k 10 60 ./tools/valu_probe 20000 $w $m > "$O/issue_probe_w${w}_m$m.json" 2>&1
+    stop_if_fatal $? issue_probe_w${w}_m$m
+  done; done
+fi
 for sc in ${VALU:-}; do
   timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_ANY --output-format csv -d "$O/pmc_valu_$sc" -o pmc -- python3 bench.py --scene $sc --steps 2 --warmup 1 --no-cpu-baseline --no-overlap $(lay $sc) > "$O/pmc_valu_$sc.log" 2>&1
   stop_if_fatal $? pmc_valu_$sc
+  # the scalar side (one scalar ALU per CU, shared by its four SIMDs): a pass of its own (8 SQ counters per pass)
+  timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d "$O/pmc_salu_$sc" -o pmc -- python3 bench.py --scene $sc --steps 2 --warmup 1 --no-cpu-baseline --no-overlap $(lay $sc) > "$O/pmc_salu_$sc.log" 2>&1
+  stop_if_fatal $? pmc_salu_$sc
 done
 for sc in ${TRAFFIC:-}; do
   for c in FETCH_SIZE WRITE_SIZE; do

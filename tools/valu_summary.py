@@ -100,6 +100,20 @@ def workload(pmc_dir, bench_log, out_json):
            "wait_any_share": (tot["SQ_WAIT_ANY"] / tot["SQ_WAVE_CYCLES"]) if tot.get("SQ_WAVE_CYCLES") else None,
            # what bench.py checks before using the entry: the launched symbol and the kernel sources
            "variant": variant, "kernel_source_sha": line["config"].get("kernel_source_sha")}
+    # the scalar side, from the sibling pmc_salu_<scene> pass (gpu_session.sh VALU=...) when present:
+    # SALU instructions per segment (the CU's one scalar ALU issues at most one per cycle)
+    sdir = pmc_dir.replace("pmc_valu_", "pmc_salu_")
+    sds = dispatches(sdir, [variant] if variant else ["render_kernel", "pathtrace_kernel"]) if sdir != pmc_dir else {}
+    if sds:
+        salu = [v["counters"]["SQ_INSTS_SALU"] for v in sds.values()]
+        stot = collections.Counter()
+        for v in sds.values():
+            stot.update(v["counters"])
+        n = len(salu)
+        ent.update({"salu_insts_per_segment": sum(salu) / n / segs,
+                    "smem_insts_per_segment": stot["SQ_INSTS_SMEM"] / n / segs,
+                    "branch_insts_per_segment": stot["SQ_INSTS_BRANCH"] / n / segs,
+                    "salu_source": os.path.relpath(sdir, REPO)})
     d = json.load(open(out_json)) if os.path.exists(out_json) else {}
     d.setdefault("note", "SQ_INSTS_VALU (whole chip, wave64 instructions; calibrated in profiles/r02/valu_probe.json) "
                          "of the bench workload's render kernel per traced segment; bench.py multiplies it by the "
