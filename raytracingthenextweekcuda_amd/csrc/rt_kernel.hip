@@ -66,9 +66,6 @@ constexpr int block_waves(bool queue) { return queue ? kQueueBlockWaves : kWaves
 #ifndef RT_SPH_ROOT_FLAT
 #define RT_SPH_ROOT_FLAT 0  // 1: sphere_root without early exits (A/B)
 #endif
-#ifndef RT_BOX_FLAT
-#define RT_BOX_FLAT 0  // 1: box_hit without early returns (A/B)
-#endif
 #ifndef RT_MERGE_SEL
 #define RT_MERGE_SEL 1  // 0: the ordered merge as a divergent branch (A/B)
 #endif
@@ -82,24 +79,6 @@ struct Ray {
 // and signs (Ray.h:10-16); tMin/tMax are ignored like the reference.
 __device__ __forceinline__ bool box_hit(const float* f, v3 o, v3 inv) {
     const bool sx = inv.x < 0.0f, sy = inv.y < 0.0f, sz = inv.z < 0.0f;
-#if RT_BOX_FLAT
-    // the same tests without early returns: a lane that fails an earlier test fails the result
-    // whatever the later ones give, so all are evaluated and or-ed (no divergent exits)
-    float tminx = ((sx ? f[3] : f[0]) - o.x) * inv.x;
-    float tmaxx = ((sx ? f[0] : f[3]) - o.x) * inv.x;
-    const float tminy = ((sy ? f[4] : f[1]) - o.y) * inv.y;
-    const float tmaxy = ((sy ? f[1] : f[4]) - o.y) * inv.y;
-    const float tminz = ((sz ? f[5] : f[2]) - o.z) * inv.z;
-    const float tmaxz = ((sz ? f[2] : f[5]) - o.z) * inv.z;
-    const bool f1 = (tminx > tmaxy) || (tminy > tmaxx);
-    tminx = tminy > tminx ? tminy : tminx;
-    tmaxx = tmaxy < tmaxx ? tmaxy : tmaxx;
-    const bool f2 = (tminx > tmaxz) || (tminz > tmaxx);
-    tminx = tminz > tminx ? tminz : tminx;
-    tmaxx = tmaxz < tmaxx ? tmaxz : tmaxx;
-    const bool f3 = (tminx < 0.0f) && (tmaxx < 0.0f);
-    return !(f1 || f2 || f3);
-#else
     float tminx = ((sx ? f[3] : f[0]) - o.x) * inv.x;
     float tmaxx = ((sx ? f[0] : f[3]) - o.x) * inv.x;
     float tminy = ((sy ? f[4] : f[1]) - o.y) * inv.y;
@@ -118,7 +97,6 @@ __device__ __forceinline__ bool box_hit(const float* f, v3 o, v3 inv) {
         if (t < 0.0f) return false;
     }
     return true;
-#endif
 }
 
 // Conservative BVH node test (boxes are inflated at build time; NaN slabs from
@@ -434,11 +412,18 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
         const v3 po{__shfl(o.x, own, 64), __shfl(o.y, own, 64), __shfl(o.z, own, 64)};
         const v3 pd{__shfl(d.x, own, 64), __shfl(d.y, own, 64), __shfl(d.z, own, 64)};
         const float pt0 = __shfl(h.t, own, 64);
+#if RT_TRIP_FLAT
+        // lanes past `count` test triangle 0 (valid) and drop the result: no branch around the loads
+        const float t = tri_t(tris[k], po, pd);
+        if (act && t <= pt0)
+            atomicMin(&W.key[own], ((unsigned long long)__float_as_uint(t) << 32) | tri_orig[2 * k]);
+#else
         if (act) {
             const float t = tri_t(tris[k], po, pd);
             if (t <= pt0)
                 atomicMin(&W.key[own], ((unsigned long long)__float_as_uint(t) << 32) | tri_orig[2 * k]);
         }
+#endif
         qdone += count;
         __builtin_amdgcn_wave_barrier();
     };
@@ -452,9 +437,14 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             const int nv = __popcll(vm), ni = __popcll(im);
             if (spare) W.src[lane_rank(vm)] = lane;
             __builtin_amdgcn_wave_barrier();
-            int vic = lane;
             const bool thief = idle && lane_rank(im) < nv;
+#if RT_TRIP_FLAT
+            const int vr = W.src[lane_rank(im)];  // (read by every lane: the rank is below 64)
+            const int vic = thief ? vr : lane;
+#else
+            int vic = lane;
             if (thief) vic = W.src[lane_rank(im)];
+#endif
             const int vt = __shfl(bot, vic, 64);  // the victim's oldest pending reference
             auto take = [&](float& x) {
                 const float v = __shfl(x, vic, 64);
@@ -467,6 +457,17 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             take(ro.x); take(ro.y); take(ro.z);
             take(ri.x); take(ri.y); take(ri.z);
             take(best);
+#if RT_TRIP_FLAT
+            {
+                const uint32_t vref = wstack[vt * 64 + vic];  // (a valid slot for every lane)
+                const float kb = __uint_as_float((uint32_t)(W.key[owner] >> 32));
+                cur = thief ? vref : cur;
+                best = thief ? fminf(best, kb) : best;
+                sp = thief ? 0 : sp;
+                bot = thief ? 0 : bot + (spare && lane_rank(vm) < ni ? 1 : 0);  // robbed
+                has = has || thief;
+            }
+#else
             if (thief) {
                 cur = wstack[vt * 64 + vic];
                 best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
@@ -474,6 +475,7 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
                 has = true;
             }
             if (spare && lane_rank(vm) < ni) ++bot;  // robbed
+#endif
             __builtin_amdgcn_wave_barrier();
         }
 #if RT_TRIP_FLAT
@@ -2066,8 +2068,8 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
             const int nv = __popcll(vm), ni = __popcll(im);
             if (spare) vlist[lane_rank(vm)] = lane;
             __builtin_amdgcn_wave_barrier();
-            int vic = lane;
             const bool thief = idle && lane_rank(im) < nv;
+            int vic = lane;
             if (thief) vic = vlist[lane_rank(im)];
             const int vb = __shfl(bot, vic, 64);
             auto take = [&](float& x) {
@@ -2579,7 +2581,7 @@ uint32_t kernel_build_flags() {
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
-    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_SCAN_PAIRS != 1 || RT_MERGE_SEL != 1 || RT_BOX_FLAT != 0 || RT_TRIP_FLAT != 1 || RT_SPH_TRIP_FLAT != 0 || RT_SPH_ROOT_FLAT != 0
+    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_SCAN_PAIRS != 1 || RT_MERGE_SEL != 1 || RT_TRIP_FLAT != 1 || RT_SPH_TRIP_FLAT != 0 || RT_SPH_ROOT_FLAT != 0
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)
