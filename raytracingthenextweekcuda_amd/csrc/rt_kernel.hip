@@ -60,12 +60,6 @@ constexpr int block_waves(bool queue) { return queue ? kQueueBlockWaves : kWaves
 #ifndef RT_TRIP_FLAT
 #define RT_TRIP_FLAT 1  // 0: the mesh traversal's pop, push and leaf steps as divergent branches (A/B)
 #endif
-#ifndef RT_SPH_TRIP_FLAT
-#define RT_SPH_TRIP_FLAT 0  // 1: the same for the sphere-group traversal (A/B; measured slower)
-#endif
-#ifndef RT_SPH_ROOT_FLAT
-#define RT_SPH_ROOT_FLAT 0  // 1: sphere_root without early exits (A/B)
-#endif
 #ifndef RT_MERGE_SEL
 #define RT_MERGE_SEL 1  // 0: the ordered merge as a divergent branch (A/B)
 #endif
@@ -119,15 +113,6 @@ __device__ __forceinline__ bool sphere_root(v3 o, v3 d, v3 c, float r, float tmi
     float hb = dot(oc, d);
     float cc = dot(oc, oc) - r * r;
     float disc = hb * hb - a * cc;
-#if RT_SPH_ROOT_FLAT
-    // both roots evaluated, the choice made with lane selects (no divergent exits)
-    const float inva = fdiv(1.0f, a);
-    const float sq = fsqrt(disc);  // (NaN where disc < 0: not used then)
-    const float t1 = (-hb - sq) * inva, t2 = (-hb + sq) * inva;
-    const bool bad1 = t1 < tmin || tmax < t1, bad2 = t2 < tmin || tmax < t2;
-    root = bad1 ? t2 : t1;
-    return (disc > kFltEpsilon) && !(bad1 && bad2);
-#else
     if (!(disc > kFltEpsilon)) return false;
     float inva = fdiv(1.0f, a);
     float sq = fsqrt(disc);
@@ -138,7 +123,6 @@ __device__ __forceinline__ bool sphere_root(v3 o, v3 d, v3 c, float r, float tmi
     }
     root = t;
     return true;
-#endif
 }
 
 // MovingSphere::center (Sphere.cu:75-78).
@@ -756,47 +740,16 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
     };
     for (;;) {
         if (__ballot(has || sp > 0) == 0) break;
-#if RT_SPH_TRIP_FLAT
-        {  // (as mesh_bvh_pairs)
-            const bool pop = !has && sp > 0;
-            const uint32_t v = wstack[(pop ? sp - 1 : 0) * 64 + lane];
-            cur = pop ? v : cur;
-            sp -= pop ? 1 : 0;
-            has = has || pop;
-        }
-#else
         if (!has && sp > 0) {
             cur = wstack[(--sp) * 64 + lane];
             has = true;
         }
-#endif
         if (has && !(cur & kLeafRef)) {
             const BvhNode nl = nodes[2 * (size_t)cur], nr = nodes[2 * (size_t)cur + 1];
             cnt.node_visits += 2;
             float tl, tr;
             const bool hl = node_hit(nl, o, inv, best, tl);
             const bool hr = node_hit(nr, o, inv, best, tr);
-#if RT_SPH_TRIP_FLAT
-            const bool both = hl && hr, lf = tl <= tr;
-            const bool ovf = both && sp + 1 > cap;
-            if (__builtin_expect(__ballot(ovf) != 0, 0))
-                if (ovf) cnt.overflow();
-            const bool push = both && !ovf;
-            wstack[(push ? sp : cap) * 64 + lane] = lf ? nr.a : nl.a;
-            sp = ovf ? 0 : sp + (push ? 1 : 0);
-            cur = both ? (lf ? nl.a : nr.a) : (hl ? nl.a : nr.a);
-            has = (hl || hr) && !ovf;
-        }
-        uint32_t lk = 0, ln = 0;
-        {
-            const bool leaf = has && (cur & kLeafRef);
-            const uint32_t nt = ((cur >> 27) & 15u) + 1u;
-            lk = cur & 0x07FFFFFFu;
-            ln = leaf ? (nt < 3u ? nt : 3u) : 0u;
-            cur = leaf && nt > 3u ? (kLeafRef | ((nt - 4u) << 27) | (lk + 3u)) : cur;
-            has = has && !(leaf && nt <= 3u);
-        }
-#else
             if (hl && hr) {
                 if (sp + 1 > cap) {
                     cnt.overflow();
@@ -825,7 +778,6 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
             else
                 has = false;
         }
-#endif
         const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
         if (b1) {
             const uint32_t at = qtail + (uint32_t)(lane_rank(b1) + lane_rank(b2) + lane_rank(b3));
@@ -2581,7 +2533,7 @@ uint32_t kernel_build_flags() {
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
-    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_SCAN_PAIRS != 1 || RT_MERGE_SEL != 1 || RT_TRIP_FLAT != 1 || RT_SPH_TRIP_FLAT != 0 || RT_SPH_ROOT_FLAT != 0
+    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_SCAN_PAIRS != 1 || RT_MERGE_SEL != 1 || RT_TRIP_FLAT != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)

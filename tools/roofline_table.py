@@ -17,7 +17,8 @@ def main(src):
     valu = json.load(open(os.path.join(REPO, "profiles", "valu_issue.json")))["workloads"]
     traffic = json.load(open(os.path.join(REPO, "profiles", "pmc_traffic.json")))
     print("| workload | kernel variant | ms/frame | kernel ms (isolated) | G segments/s | VALU inst / segment | "
-          "VALU issue (frac) | VALU lane util | useful frac | HBM bytes / launch (frac) |")
+          "VALU issue (frac) | VALU lane util | useful frac | SALU inst / segment (frac of 1 per CU-cycle) | "
+          "HBM bytes / launch (frac) |")
     for sc in SCENES:
         f = os.path.join(src, f"bench_{sc}.log")
         if not os.path.exists(f) and sc == "cornellbox1":  # the default line (gpu_session.sh BENCH=1)
@@ -31,11 +32,14 @@ def main(src):
         v = valu.get(wl, {}).get("valu_insts_per_segment")
         lu = valu.get(wl, {}).get("valu_lane_util")
         t = traffic.get(wl, {}).get("hbm_bytes_per_launch")
+        sv = valu.get(wl, {}).get("salu_insts_per_segment")
+        sf = sv * segs / (256 * 2.4e9 * kms * 1e-3) if sv else None
         ach = v * segs / (kms * 1e-3) / 1e9 if v else None
         hbm = t / (kms * 1e-3) / 1e9 if t else None
         print(f"| {wl} | `{line['config'].get('variant')}` | {line['ms_per_step']:.3f} | {kms:.3f} | {segs / (line['ms_per_step'] * 1e-3) / 1e9:.2f} | "
               f"{v:.2f} | {ach:.0f} G/s ({ach / PEAK_VALU:.3f}) | "
               + (f"{lu:.3f} | {ach / PEAK_VALU * lu:.3f} | " if lu else "— | — | ")
+              + (f"{sv:.2f} ({sf:.3f}) | " if sv else "— | ")
               + (f"{t / 1e9:.2f} GB ({hbm / PEAK_HBM:.4f}) |" if t else "— |"))
 
 
