@@ -953,12 +953,14 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             }
         };
         // wave-uniform dispatch on the record type; the reference's scenes are mostly axial planes
-        if (RT_PLANE_AXIAL && ob.type == kObjPlaneAxial) {
-            cand(plane_axial<2, 0, 1>(ob, o, d), false);  // XY
-        } else if (RT_PLANE_AXIAL && ob.type == kObjPlaneAxial + 1) {
-            cand(plane_axial<0, 1, 2>(ob, o, d), false);  // YZ
-        } else if (RT_PLANE_AXIAL && ob.type == kObjPlaneAxial + 2) {
+        const uint32_t ty = ob.type;
+        auto is = [&](uint32_t k) { return ty == k; };
+        if (RT_PLANE_AXIAL && is(kObjPlaneAxial + 2)) {
             cand(plane_axial<1, 0, 2>(ob, o, d), false);  // XZ
+        } else if (RT_PLANE_AXIAL && is(kObjPlaneAxial + 1)) {
+            cand(plane_axial<0, 1, 2>(ob, o, d), false);  // YZ
+        } else if (RT_PLANE_AXIAL && is(kObjPlaneAxial)) {
+            cand(plane_axial<2, 0, 1>(ob, o, d), false);  // XY
         } else if (is_plane(ob.type)) {
             // Plane::hit (Plane.cu:4-52); t is only used when `proceed` holds.
             const v3 nrm{f[3], f[4], f[5]};
@@ -1898,26 +1900,42 @@ __device__ __forceinline__ bool pt_box_decide(const CFNode& n, const PtRay& r, f
     return pt_box(n, r.o, r.d, tx);
 }
 
-// Entry-parameter bounds of a leaf box (leaves are never box-tested by the
-// reference: these only order and prune).
-__device__ __forceinline__ void pt_box_bounds(const CFNode& n, const PtRay& r, float& tn_prune,
-                                              float& order) {
-    float tn = -3.40282347e+38f, tw = -3.40282347e+38f;
+// A child of a pair record: pt_box_decide for an inner child; for a leaf's box (n.u1), which the
+// reference never box-tests, only the entry bounds that order and prune (none in exact mode). One pass
+// without divergent branches (round 4: the traversal's exec-mask bookkeeping loaded the CU's scalar
+// unit): the slab values are shared, and the exact fallback (pt_box's divisions) runs behind a
+// wave-uniform test for the rare inner-box lanes inside the rounding band. Same decisions and bounds.
+__device__ __forceinline__ bool pt_child(const CFNode& n, const PtRay& r, float& tn_prune, float& order) {
+    float tn = -3.40282347e+38f, tf = 3.40282347e+38f, tw = -3.40282347e+38f;
+    bool miss = false;
     const float oo[3] = {r.o.x, r.o.y, r.o.z}, dd[3] = {r.d.x, r.d.y, r.d.z};
     const float iv[3] = {r.inv.x, r.inv.y, r.inv.z};
-    const float pt[3] = {r.eps * fabsf(r.inv.x), r.eps * fabsf(r.inv.y), r.eps * fabsf(r.inv.z)};
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        if (dd[c] != 0.0f && !r.exact) {
-            const float t1 = (n.bottom[c] - oo[c]) * iv[c];
-            const float t2 = (n.top[c] - oo[c]) * iv[c];
-            const float tnear_c = fminf(t1, t2);
-            tn = fmaxf(tn, tnear_c);
-            tw = fmaxf(tw, tnear_c - pt[c]);
-        }
+        const float lo = n.bottom[c], hi = n.top[c];
+        const bool z = dd[c] == 0.0f;
+        miss |= z & ((oo[c] < lo) | (oo[c] > hi));
+        const float t1 = (lo - oo[c]) * iv[c];
+        const float t2 = (hi - oo[c]) * iv[c];
+        const float tnear_c = fminf(t1, t2);
+        tn = z ? tn : fmaxf(tn, tnear_c);
+        tf = z ? tf : fminf(tf, fmaxf(t1, t2));
+        tw = z ? tw : fmaxf(tw, tnear_c - r.eps * fabsf(iv[c]));
     }
-    tn_prune = tw;
-    order = tn;
+    const bool leaf = n.u1 != 0u;
+    // a leaf's bounds: none in exact mode
+    tn_prune = leaf && r.exact ? -3.40282347e+38f : tw;
+    order = leaf && r.exact ? -3.40282347e+38f : tn;
+    const float m = fmaxf(fabsf(tn), fabsf(tf));
+    const bool fast = !r.exact && m < 1e30f && fabsf(tn - tf) > 4e-6f * m;
+    bool res = !miss && tn <= tf && !(tf < 0.0f);
+    const bool need = !leaf && !miss && !fast;
+    if (__builtin_expect(__ballot(need) != 0, 0))
+        if (need) {
+            float tx;
+            res = pt_box(n, r.o, r.d, tx);
+        }
+    return leaf || res;
 }
 
 struct PtBest {
@@ -2061,18 +2079,8 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
             cnt.node_visits += 2;
             float w0, o0, w1, o1;
             bool h0, h1;
-            if (c0.u1) {  // a leaf's box: distance pruning only
-                pt_box_bounds(c0, r, w0, o0);
-                h0 = true;
-            } else {
-                h0 = pt_box_decide(c0, r, w0, o0);
-            }
-            if (c1.u1) {
-                pt_box_bounds(c1, r, w1, o1);
-                h1 = true;
-            } else {
-                h1 = pt_box_decide(c1, r, w1, o1);
-            }
+            h0 = pt_child(c0, r, w0, o0);
+            h1 = pt_child(c1, r, w1, o1);
             h0 = h0 && !pruned(w0);
             h1 = h1 && !pruned(w1);
             if (h0 && h1) {
