@@ -57,12 +57,6 @@ constexpr int kQueueBlockWaves = RT_QUEUE_BLOCK_WAVES;
 static_assert(kQueueBlockWaves == 1 || kQueueBlockWaves == 2 || kQueueBlockWaves == 4, "queue block waves");
 constexpr int block_waves(bool queue) { return queue ? kQueueBlockWaves : kWavesPerBlock; }
 
-#ifndef RT_TRIP_FLAT
-#define RT_TRIP_FLAT 1  // 0: the mesh traversal's pop, push and leaf steps as divergent branches (A/B)
-#endif
-#ifndef RT_MERGE_SEL
-#define RT_MERGE_SEL 1  // 0: the ordered merge as a divergent branch (A/B)
-#endif
 
 struct Ray {
     v3 o, d;
@@ -105,16 +99,17 @@ __device__ __forceinline__ bool node_hit(const BvhNode& n, v3 o, v3 inv, float t
     return tn <= fminf(tf, tmax * 1.00001f + 1e-30f);
 }
 
-// Sphere::hit / MovingSphere::hit root selection (Sphere.cu:3-37, 39-73).
+// Sphere::hit / MovingSphere::hit root selection (Sphere.cu:3-37, 39-73). `inva` = 1.0f / dot(d, d), the
+// same IEEE quotient for every sphere a ray tests: the caller forms it once per ray (sphere_inva).
+__device__ __forceinline__ float sphere_inva(v3 d) { return fdiv(1.0f, dot(d, d)); }
 __device__ __forceinline__ bool sphere_root(v3 o, v3 d, v3 c, float r, float tmin, float tmax,
-                                            float& root) {
+                                            float& root, float inva) {
     v3 oc = sub(o, c);
     float a = dot(d, d);
     float hb = dot(oc, d);
     float cc = dot(oc, oc) - r * r;
     float disc = hb * hb - a * cc;
     if (!(disc > kFltEpsilon)) return false;
-    float inva = fdiv(1.0f, a);
     float sq = fsqrt(disc);
     float t = (-hb - sq) * inva;
     if (t < tmin || tmax < t) {
@@ -212,9 +207,9 @@ struct Hit {
     __device__ __forceinline__ void merge_seq(float tc, uint32_t order, bool sphere, int32_t o, int32_t tr) {
         if constexpr (!kOrdered) {
             merge(tc, order, sphere, o, tr);
-        } else if (RT_MERGE_SEL) {
-            // the same updates as selects on the compare's lane mask (VALU), without the divergent
-            // branch's exec-mask saves and restores (scalar instructions)
+        } else {
+            // as selects on the compare's lane mask (VALU), without a divergent branch's exec-mask
+            // saves and restores (scalar instructions: DESIGN §4)
             const bool lt = tc < t, eq = sphere && tc == t;
             ms_obj = lt ? (sphere ? o : -1) : eq ? o : ms_obj;
             ms = (lt || eq) ? order : ms;
@@ -222,16 +217,6 @@ struct Hit {
             mi = lt ? order : mi;
             obj = lt ? o : obj;
             tri = lt ? tr : tri;
-        } else if (tc < t) {
-            t = tc;
-            mi = order;
-            obj = o;
-            tri = tr;
-            ms_obj = sphere ? o : -1;
-            ms = order;
-        } else if (sphere && tc == t) {
-            ms_obj = o;
-            ms = order;
         }
     }
     __device__ __forceinline__ void finish() {
@@ -396,18 +381,10 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
         const v3 po{__shfl(o.x, own, 64), __shfl(o.y, own, 64), __shfl(o.z, own, 64)};
         const v3 pd{__shfl(d.x, own, 64), __shfl(d.y, own, 64), __shfl(d.z, own, 64)};
         const float pt0 = __shfl(h.t, own, 64);
-#if RT_TRIP_FLAT
         // lanes past `count` test triangle 0 (valid) and drop the result: no branch around the loads
         const float t = tri_t(tris[k], po, pd);
         if (act && t <= pt0)
             atomicMin(&W.key[own], ((unsigned long long)__float_as_uint(t) << 32) | tri_orig[2 * k]);
-#else
-        if (act) {
-            const float t = tri_t(tris[k], po, pd);
-            if (t <= pt0)
-                atomicMin(&W.key[own], ((unsigned long long)__float_as_uint(t) << 32) | tri_orig[2 * k]);
-        }
-#endif
         qdone += count;
         __builtin_amdgcn_wave_barrier();
     };
@@ -422,13 +399,8 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             if (spare) W.src[lane_rank(vm)] = lane;
             __builtin_amdgcn_wave_barrier();
             const bool thief = idle && lane_rank(im) < nv;
-#if RT_TRIP_FLAT
             const int vr = W.src[lane_rank(im)];  // (read by every lane: the rank is below 64)
             const int vic = thief ? vr : lane;
-#else
-            int vic = lane;
-            if (thief) vic = W.src[lane_rank(im)];
-#endif
             const int vt = __shfl(bot, vic, 64);  // the victim's oldest pending reference
             auto take = [&](float& x) {
                 const float v = __shfl(x, vic, 64);
@@ -441,7 +413,6 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             take(ro.x); take(ro.y); take(ro.z);
             take(ri.x); take(ri.y); take(ri.z);
             take(best);
-#if RT_TRIP_FLAT
             {
                 const uint32_t vref = wstack[vt * 64 + vic];  // (a valid slot for every lane)
                 const float kb = __uint_as_float((uint32_t)(W.key[owner] >> 32));
@@ -451,18 +422,8 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
                 bot = thief ? 0 : bot + (spare && lane_rank(vm) < ni ? 1 : 0);  // robbed
                 has = has || thief;
             }
-#else
-            if (thief) {
-                cur = wstack[vt * 64 + vic];
-                best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
-                sp = bot = 0;
-                has = true;
-            }
-            if (spare && lane_rank(vm) < ni) ++bot;  // robbed
-#endif
             __builtin_amdgcn_wave_barrier();
         }
-#if RT_TRIP_FLAT
         {  // pop as lane selects (the read of slot 0 by lanes that do not pop is discarded)
             const bool pop = !has && sp > bot;
             const uint32_t v = wstack[(pop ? sp - 1 : 0) * 64 + lane];
@@ -475,22 +436,12 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             sp = empty ? 0 : sp;
             bot = empty ? 0 : bot;
         }
-#else
-        if (!has && sp > bot) {
-            cur = wstack[(--sp) * 64 + lane];
-            has = true;
-            // the ray's best so far over all lanes (NaN while none: fminf keeps ours)
-            best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
-        }
-        if (!has && sp == bot) sp = bot = 0;
-#endif
         if (has && !(cur & kLeafRef)) {
             const BvhNode nl = nodes[2 * (size_t)cur], nr = nodes[2 * (size_t)cur + 1];
             cnt.node_visits += 2;
             float tl, tr;
             const bool hl = node_hit(nl, ro, ri, best, tl);
             const bool hr = node_hit(nr, ro, ri, best, tr);
-#if RT_TRIP_FLAT
             // as lane selects; a lane that does not push writes the spare slot `cap` (never read)
             const bool both = hl && hr, lf = tl <= tr;
             const bool ovf = both && sp + 1 > cap;
@@ -502,28 +453,8 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             bot = ovf ? 0 : bot;
             cur = both ? (lf ? nl.a : nr.a) : (hl ? nl.a : nr.a);
             has = (hl || hr) && !ovf;
-#else
-            if (hl && hr) {
-                if (sp + 1 > cap) {
-                    cnt.overflow();
-                    has = false;
-                    sp = bot = 0;
-                } else {
-                    const bool left_first = tl <= tr;
-                    wstack[(sp++) * 64 + lane] = left_first ? nr.a : nl.a;
-                    cur = left_first ? nl.a : nr.a;
-                }
-            } else if (hl) {
-                cur = nl.a;
-            } else if (hr) {
-                cur = nr.a;
-            } else {
-                has = false;
-            }
-#endif
         }
         uint32_t lk = 0, ln = 0;  // this trip's leaf pairs: triangles lk .. lk + ln - 1
-#if RT_TRIP_FLAT
         {
             const bool leaf = has && (cur & kLeafRef);
             const uint32_t nt = ((cur >> 27) & 15u) + 1u;
@@ -534,18 +465,6 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             has = has && !(leaf && nt <= 3u);
             cnt.tri_tests += ln;
         }
-#else
-        if (has && (cur & kLeafRef)) {
-            const uint32_t nt = ((cur >> 27) & 15u) + 1u;
-            lk = cur & 0x07FFFFFFu;
-            ln = nt < 3u ? nt : 3u;
-            if (nt > 3u)  // a larger leaf keeps this lane for more trips
-                cur = kLeafRef | ((nt - 4u) << 27) | (lk + 3u);
-            else
-                has = false;
-            cnt.tri_tests += ln;
-        }
-#endif
         // enqueue the leaf pairs (converged): a lane's slots follow those of the lanes below it
         const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
         if (b1) {
@@ -682,13 +601,13 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
 // Candidate root of a (moving) sphere independent of closestSoFar: the near
 // root if >= tMin, else the far root (Sphere.cu:20-31 with tMax = +inf; the
 // sequential tMax test is applied by Hit::merge). NaN = no candidate.
-__device__ __forceinline__ float sphere_candidate(const ObjRec& ob, v3 o, v3 d, float time) {
+__device__ __forceinline__ float sphere_candidate(const ObjRec& ob, v3 o, v3 d, float time, float inva) {
     const float* f = ob.f;
     const bool moving = ob.type == kObjMovingSphere;
     const v3 c = moving ? moving_center(f, time) : v3{f[0], f[1], f[2]};
     const float r = moving ? f[8] : f[3];
     float t = 0.0f;
-    return sphere_root(o, d, c, r, kTMin, kInf, t) ? t : __builtin_nanf("");
+    return sphere_root(o, d, c, r, kTMin, kInf, t, inva) ? t : __builtin_nanf("");
 }
 
 // Sphere group: the object BVH over the scene's spheres (members are ObjRecs stored after the
@@ -703,8 +622,9 @@ __device__ __forceinline__ float sphere_candidate(const ObjRec& ob, v3 o, v3 d, 
 // lane whose pair set the final minimum records the member (orders are unique) in W.src.
 __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ objs,
                                                      const BvhNode* __restrict__ nodes, uint32_t root,
-                                                     bool live, const Ray& ray, v3 inv, Hit& h, uint32_t* wstack,
-                                                     WaveLds& W, int lane, Counters& cnt, int cap) {
+                                                     bool live, const Ray& ray, v3 inv, float inva, Hit& h,
+                                                     uint32_t* wstack, WaveLds& W, int lane, Counters& cnt,
+                                                     int cap) {
     if (__ballot(live) == 0) return;
     key_reset(W.key[lane]);
     const v3 o = ray.o;
@@ -723,11 +643,12 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
         const v3 po{__shfl(ray.o.x, own, 64), __shfl(ray.o.y, own, 64), __shfl(ray.o.z, own, 64)};
         const v3 pd{__shfl(ray.d.x, own, 64), __shfl(ray.d.y, own, 64), __shfl(ray.d.z, own, 64)};
         const float ptime = __shfl(ray.time, own, 64), pt0 = __shfl(h.t, own, 64);
+        const float pinva = __shfl(inva, own, 64);  // the owner's 1 / dot(d, d)
         unsigned long long mine = ~0ull;
         if (act) {
             const ObjRec ob = load_obj(objs, (int)k);
             cnt.grp += ob.type == kObjMovingSphere ? 0x10000u : 1u;
-            const float t = sphere_candidate(ob, po, pd, ptime);
+            const float t = sphere_candidate(ob, po, pd, ptime, pinva);
             if (t <= pt0) {
                 mine = ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)(~ob.order);
                 atomicMin(&W.key[own], mine);
@@ -885,9 +806,6 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
 // each updating the Hit state). Both were measured slower on the other scenes.
 // kParts (BVH kernels): 1 = the scene has BVH meshes, 2 = sphere groups; the other traversal is
 // not compiled in (rt_capi.cpp picks the variant from the committed scene).
-#ifndef RT_SCAN_PAIRS
-#define RT_SCAN_PAIRS 1  // 0: one prefetched record, copied per object (A/B)
-#endif
 #ifndef RT_PLANE_AXIAL
 #define RT_PLANE_AXIAL 1  // 0: every plane through the general dot products (A/B)
 #endif
@@ -936,6 +854,8 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                                            ) {
     Hit h{kInf, -1, -1, 0xFFFFFFFFu, -1, 0u};
     const v3 o = ray.o, d = ray.d;
+    // the spheres' 1 / dot(d, d), once per ray (only the variants that test spheres)
+    const float inva = (kSph || kMed) ? sphere_inva(d) : 0.0f;
     const int n = S.n_objs;
     constexpr bool kPf = !kMed;
     // no sphere groups: merges come in scan order (the media variant measured slower with it)
@@ -996,7 +916,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             const bool ok = proceed & (t >= kTMin) & in;
             cand(ok ? t : __builtin_nanf(""), false);
         } else if ((kSph || kMed) && (ob.type == kObjSphere || ob.type == kObjMovingSphere)) {
-            cand(sphere_candidate(ob, o, d, ray.time), true);
+            cand(sphere_candidate(ob, o, d, ray.time, inva), true);
         } else if (ob.type == kObjMesh) {
             // TriangleMesh::hit (TriangleMesh.cu:34-117): the AABB early-out
             // gates the triangle scan exactly as in the reference.
@@ -1020,12 +940,12 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             // media to the kMed variant, so its register allocation need not cover this test)
             cand(live ? medium_candidate(ob, o, d, rng) : __builtin_nanf(""), false);
         } else if (kBvh && (kParts & 2) != 0) {  // kObjSphereGroup
-            sphere_group_batched(S.objs, S.nodes, __float_as_uint(ob.f[8]), live, ray, inv, h, stack - lane, W, lane,
+            sphere_group_batched(S.objs, S.nodes, __float_as_uint(ob.f[8]), live, ray, inv, inva, h, stack - lane, W, lane,
                                  cnt, S.stack_cap);
         }
         if constexpr (kMed) h.merge_seq<kOrd>(tc, ob.order, tsph, i, -1);  // NaN: no candidate
     };
-    if constexpr (kPf && RT_SCAN_PAIRS) {
+    if constexpr (kPf) {
         // Records prefetched one object ahead, in two alternating register sets (the scan unrolled by
         // two): each load lands in the registers of a record already visited, so no record is copied
         // between scalar registers per object (a single prefetched record costs 14 s_mov per object,
@@ -1041,12 +961,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             visit(rb, i + 1);
         }
     } else {
-        ObjRec cur = load_obj(S.objs, 0);
-        for (int i = 0; i < n; ++i) {
-            const ObjRec ob = kPf ? cur : load_obj(S.objs, i);
-            if (kPf && i + 1 < n) cur = load_obj(S.objs, i + 1);
-            visit(ob, i);
-        }
+        for (int i = 0; i < n; ++i) visit(load_obj(S.objs, i), i);
     }
     h.finish();
     return h;
@@ -1470,7 +1385,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         W.grp_s[lane] = 0;
         W.grp_m[lane] = 0;
     }
-    uint32_t* stack = kBvh ? dyn_stacks + (size_t)wave * (L.stack_depth + RT_TRIP_FLAT) * 64 + lane : nullptr;
+    uint32_t* stack = kBvh ? dyn_stacks + (size_t)wave * (L.stack_depth + 1) * 64 + lane : nullptr;
 
     // Lane layout: SP = lanes_per_pixel adjacent lanes share one pixel and split
     // its samples (sub-lane c takes samples c, c+SP, c+2SP, ...). A wave covers
@@ -2420,7 +2335,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
 }
 
 // Dynamic LDS of a traversal kernel: the per-lane stacks of the block's `bw` waves.
-// `spare`: one more slot per lane past the stack (RT_TRIP_FLAT: the render kernels' unconditional push target)
+// `spare`: one more slot per lane past the stack (the render kernels' traversals push there unconditionally)
 static size_t stack_bytes(const RenderLaunch& L, int bw, int spare = 0) {
     return (size_t)bw * (size_t)((L.stack_depth > 0 ? L.stack_depth : 1) + spare) * 64 * sizeof(uint32_t);
 }
@@ -2465,7 +2380,7 @@ int queue_blocks(int n_cu, uint32_t variant, const RenderLaunch& L) {
             lds = (size_t)bw * (sizeof(WaveLds) + sizeof(CamSlots));
             break;
         default:
-            lds = (size_t)bw * sizeof(WaveLds) + stack_bytes(L, bw, RT_TRIP_FLAT);
+            lds = (size_t)bw * sizeof(WaveLds) + stack_bytes(L, bw, 1);
     }
     const int fit = (int)((size_t)160 * 1024 / (lds ? lds : 1));
     return n_cu * std::max(1, std::min(4 * waves / bw, fit));
@@ -2541,7 +2456,7 @@ uint32_t kernel_build_flags() {
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
-    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_SCAN_PAIRS != 1 || RT_MERGE_SEL != 1 || RT_TRIP_FLAT != 1
+    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)
@@ -2563,7 +2478,7 @@ hipError_t launch_render(uint32_t variant, const SceneArgs& sc, const CamRec* ca
                          unsigned long long* counters, hipStream_t stream, hipEvent_t main_done) {
     const int bw = block_waves(L.queue != 0);
     const dim3 block(64 * bw);
-    const size_t lds = stack_bytes(L, bw, RT_TRIP_FLAT);
+    const size_t lds = stack_bytes(L, bw, 1);
     dim3 grid;
     if (L.queue) {
         if (L.n_items == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
