@@ -84,6 +84,13 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true",
                     help="one context and stream: consecutive frames do not overlap (per-launch roofline)")
     ap.add_argument("--cpu-spp", type=int, default=None)
+    ap.add_argument("--exchange", choices=("abi", "torch"), default="abi",
+                    help="N > 1 row-tile exchange: abi = the library's rt_gather_rows (one ncclGather + the root's "
+                         "de-interleave) on each frame's render stream, gloo for the control plane; torch = "
+                         "torch.distributed.gather over ProcessGroupNCCL (its own stream: at most 2 contexts)")
+    ap.add_argument("--rehearse-shard", type=int, default=0, metavar="N",
+                    help="one GPU, one process: render rank 0's rows of an N-rank frame with the N > 1 stream layout "
+                         "and exchange (a one-rank RCCL communicator gathers the tile on the render stream)")
     ap.add_argument("--line-selftest", action="store_true",
                     help="CPU only: synthetic per-rank numbers through the N > 1 collectives and the JSON line")
     a = ap.parse_args()
@@ -225,20 +232,14 @@ def load_pmc_traffic(workload: str):
     return d.get(workload)
 
 
-KERNEL_SOURCES = ("rt_kernel.hip", "rt_kernel.h", "rt_math.h", "rt_scene.h", "rt_bvh.h", "Makefile")  # + flags
-
-
 def kernel_source_sha() -> str:
-    """sha256 of the megakernel's sources and build flags (csrc/: the kernel TU, its headers, the
-    Makefile): a VALU or traffic profile recorded with the same digest (tools/valu_summary.py,
-    tools/pmc_summary.py) was taken of this code, compiled this way."""
-    import hashlib
+    """The loaded librtmi.so's source digest (rt_kernel_source_sha: every native source, the
+    Makefile, include/rtmi.h and the EXTRA flags, baked in at build time; source_digest.py). The
+    binding refuses an in-tree library whose digest is not the tree's, so a profile stamped with
+    this digest (tools/valu_summary.py, tools/pmc_summary.py) was taken of the library timed here."""
+    from raytracingthenextweekcuda_amd import _lib
 
-    h = hashlib.sha256()
-    for f in KERNEL_SOURCES:
-        with open(os.path.join(REPO, "raytracingthenextweekcuda_amd", "csrc", f), "rb") as fh:
-            h.update(f.encode() + b"\0" + fh.read())
-    return h.hexdigest()[:16]
+    return _lib.source_sha()
 
 
 def profile_check(ent, variant_name: str, sha: str):
@@ -274,10 +275,15 @@ def measure(args, world, rank, local, rehearsal):
     # last work items drain (tools/overlap_probe.py: CB1 N = 8 shard 1.17 -> 1.00 ms/frame,
     # N = 1 7.57 -> 7.42). Every frame is still rendered completely.
     contexts = args.contexts
+    shard_world = args.rehearse_shard or world  # row tiling of the frame (the rehearsal: rank 0 of N)
+    abi_exchange = (world > 1 or args.rehearse_shard) and not rehearsal and args.exchange == "abi"
     if contexts == 0:  # auto: a third context pays off where the launch's tail is a visible share of it
-        samples = rtmi.owned_rows(H, args.row_block, rank, world) * W * args.spp
+        samples = rtmi.owned_rows(H, args.row_block, rank, shard_world) * W * args.spp
         small = samples <= (1 << 25) and INTEGRATOR.get(args.scene, "rayColor") != "pathTrace"
         contexts = 3 if small else 2
+        if world > 1 and not abi_exchange:
+            # ProcessGroupNCCL's own stream is a fourth busy stream besides the default one
+            contexts = 2
     if contexts < 2 and not args.no_overlap:
         raise SystemExit("--contexts must be >= 2 (or 0 = auto, or --no-overlap)")
     # every context takes at least one timed frame (its first timed launch resets its counters)
@@ -287,25 +293,31 @@ def measure(args, world, rank, local, rehearsal):
     for rr in rs:
         getattr(rtmi, SCENES[args.scene][0])(rr, W, H)
     r = rs[0]
-    from raytracingthenextweekcuda_amd.distributed import RowShardedFrame
+    from raytracingthenextweekcuda_amd.distributed import RcclRowFrames, RowShardedFrame
 
     block = args.row_block
-    rows = rtmi.owned_rows(H, block, rank, world)
+    rows = rtmi.owned_rows(H, block, rank, shard_world)
     streams = [torch.cuda.Stream(device=local) for _ in rs] if overlap else None
-    # N > 1: frames are pipelined - frame k's RCCL gather runs on the NCCL stream under
-    # frame k+1's render (double-buffered tiles); every frame is complete by the end
-    frame = RowShardedFrame(W, H, block,
-                            device=torch.device("cpu") if rehearsal else torch.device("cuda", local),
-                            pipeline=world > 1, streams=streams)
+    if abi_exchange:
+        # N > 1 (and the one-GPU shard rehearsal): the C ABI's rt_gather_rows (one ncclGather + the
+        # root's de-interleave) on each frame's own render stream; gloo carries the control plane
+        frame = RcclRowFrames(rs, W, H, block, rank, shard_world, streams or [torch.cuda.current_stream()],
+                              torch.device("cuda", local), comm_world=world)
+    else:
+        # N > 1 over ProcessGroupNCCL (--exchange torch): frame k's gather runs on the NCCL stream under
+        # frame k+1's render (double-buffered tiles); every frame is complete by the end
+        frame = RowShardedFrame(W, H, block,
+                                device=torch.device("cpu") if rehearsal else torch.device("cuda", local),
+                                pipeline=world > 1, streams=streams)
     integrator = INTEGRATOR.get(args.scene, "rayColor")
     # three or more frames in flight: the library may pick a layout for throughput
     # (RT_RENDER_FRAMES_IN_FLIGHT; the isolated frames below use the same layout)
     in_flight = (overlap and n_ctx >= 3) or args.in_flight_layout
-    params = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, world, args.lanes, integrator,
+    params = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, shard_world, args.lanes, integrator,
                       frames_in_flight=in_flight)
     # timed launches add to the device counters (one read after the loop, no
     # per-frame host sync); each context's first timed launch resets them
-    params_keep = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, world, args.lanes, integrator,
+    params_keep = r.params(W, H, args.spp, args.depth, 1984, 0, block, rank, shard_world, args.lanes, integrator,
                            keep_counters=True, frames_in_flight=in_flight)
     stream = torch.cuda.current_stream()
     scratch = torch.empty(frame.tile.shape, dtype=torch.float32, device="cuda") if rehearsal else None
@@ -323,7 +335,7 @@ def measure(args, world, rank, local, rehearsal):
     # every context renders at least one untimed frame (its first launch allocates its work queue
     # and partial sums), however small --warmup is
     for _ in range(max(args.warmup, len(rs))):
-        if overlap:
+        if overlap or abi_exchange:
             frame.submit(lambda tile, b: render_into(tile, params, b))
         else:
             frame.submit(lambda tile: render_into(tile, params))
@@ -376,7 +388,7 @@ def measure(args, world, rank, local, rehearsal):
             r.render_device(params, frame.tile.data_ptr(), cur.cuda_stream)
         torch.cuda.synchronize()
         iso_kernel.append(r.stats()["kernel_ms"])
-        if world > 1:
+        if world > 1 or abi_exchange:
             if rehearsal:  # gloo on host tensors: no device events
                 g0 = time.perf_counter()
                 frame.gather()
@@ -386,7 +398,8 @@ def measure(args, world, rank, local, rehearsal):
                 frame.gather(events=(e0, e1))
                 torch.cuda.synchronize()
                 iso_gather.append(e0.elapsed_time(e1))
-            dist.barrier()
+            if world > 1:
+                dist.barrier()
         torch.cuda.synchronize()
         iso_frame.append((time.perf_counter() - t1) * 1e3)
     n_cu = torch.cuda.get_device_properties(local).multi_processor_count
@@ -406,7 +419,12 @@ def measure(args, world, rank, local, rehearsal):
         "queue_blocks": int(st["queue_blocks"]), "variant": st["variant_name"],
         "object_bytes_per_segment": object_bytes_per_segment(r) if integrator != "pathTrace" else 0,
         "n_cu": n_cu, "overlap": overlap, "contexts": len(rs), "frames_in_flight": in_flight,
+        "exchange": ("abi" if abi_exchange else "torch-gloo" if rehearsal else "torch") if world > 1 or abi_exchange
+        else None,
+        "shard_world": shard_world,
     }
+    if abi_exchange:
+        frame.close()
     for rr in rs:
         rr.close()
     return out
@@ -422,7 +440,8 @@ def selftest_measure(args, world, rank):
         "kernel_ms": 5.0 + rank, "kernel_ms_isolated": 4.0 + rank, "gather_ms": 0.05 * (rank + 1),
         "frame_ms_isolated": 6.0 + 0.5 * rank, "launch_ms": 5.5 + rank, "lanes_per_pixel": 32, "refill": 8,
         "queue_blocks": 1536, "variant": "render_kernel<selftest>",  # matches no profile: refused
-        "object_bytes_per_segment": 240, "n_cu": 256, "overlap": False,
+        "object_bytes_per_segment": 240, "n_cu": 256, "overlap": True, "contexts": 3,
+        "exchange": "abi" if world > 1 else None,
     }
 
 
@@ -479,6 +498,8 @@ def build_line(args, agg: dict, world: int, cpu=None) -> dict:
                  + agg["rows"] / world * W * BYTES["pixel"])
     t_iso = agg["kernel_ms_isolated"]
     workload = f"{args.scene}_{W}x{H}_spp{args.spp}_d{args.depth}_n{world}"
+    if args.rehearse_shard:  # one GPU rendering rank 0's shard of an N-rank frame
+        workload += f"_shard{args.rehearse_shard}"
     sha = kernel_source_sha()
     # Roofline: the megakernel is bound by VALU issue. achieved = VALU
     # wave-instructions per launch (SQ_INSTS_VALU per traced segment, profiled of this very
@@ -519,6 +540,12 @@ def build_line(args, agg: dict, world: int, cpu=None) -> dict:
             "variant": agg["variant"], "queue": agg["queue_blocks"] > 0,
             "refill": agg["refill"], "queue_blocks": agg["queue_blocks"], "contexts": agg.get("contexts", 1),
             "frames_in_flight": bool(agg.get("frames_in_flight", False)),
+            # N > 1: the row-tile exchange, and the HIP streams a rank keeps busy or holds: its render
+            # streams + the default stream (+ ProcessGroupNCCL's with --exchange torch); the process
+            # has GPU_MAX_HW_QUEUES = 4 hardware queues
+            "exchange": agg.get("exchange"),
+            "streams_per_rank": (agg.get("contexts", 1) + 1 + (1 if agg.get("exchange") == "torch" else 0)),
+            "rehearse_shard": args.rehearse_shard or None,
             "kernel_source_sha": sha,
             "parallelism": f"row-tiles x{world} + RCCL gather" if world > 1 else "single GPU",
             "segments_per_frame": int(segs / K),
@@ -593,8 +620,25 @@ def build_line(args, agg: dict, world: int, cpu=None) -> dict:
     return line
 
 
+def spawn_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) without an outer launcher: start torch.distributed.run with N
+    ranks on this node as a CHILD process (never exec: nothing here has touched the GPU yet, and the
+    parent stays out of it), let rank 0's JSON line through, and return the child's exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     import torch
     import torch.distributed as dist
 
@@ -602,7 +646,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.rehearse_shard and world > 1:
+        raise SystemExit("--rehearse-shard runs one process on one GPU")
     if args.line_selftest:  # CPU: the N > 1 collectives and line building, without a GPU
         if world > 1:
             dist.init_process_group("gloo")
@@ -619,14 +665,18 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        if rehearsal:
+        if rehearsal or args.exchange == "abi":
+            # the ABI exchange's control plane (unique id, barriers, stats); the frames move over
+            # the library's own RCCL communicator
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     m = measure(args, world, rank, local, rehearsal)
-    agg = aggregate(m, world, "cpu" if rehearsal else torch.device("cuda", local))
+    on_host = rehearsal or (world > 1 and args.exchange == "abi")
+    agg = aggregate(m, world, "cpu" if on_host else torch.device("cuda", local))
     if rank == 0:
-        cpu = cpu_baseline(args, host_threads()) if not args.no_cpu_baseline and world == 1 else None
+        cpu = (cpu_baseline(args, host_threads())
+               if not args.no_cpu_baseline and world == 1 and not args.rehearse_shard else None)
         print(json.dumps(build_line(args, agg, world, cpu)), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RTMI_ABI_VERSION 9
+#define RTMI_ABI_VERSION 10
 
 typedef int32_t rt_status;
 enum {
@@ -168,6 +168,11 @@ uint32_t rt_build_flags(void);
 /* The symbol of RT_VARIANT_* `variant` as rocprofv3 prints it, e.g.
  * "render_kernel<false, true, false, false, 3>"; NULL for an unknown id. */
 const char* rt_kernel_variant_name(uint32_t variant);
+/* 16 hex digits: sha256 of the library's native sources (the .hip, .cpp and .h files of csrc, its Makefile,
+ * this header) and EXTRA build flags, computed at build time by source_digest.py. The Python
+ * binding refuses an in-tree library whose digest differs from its source tree's (a stale
+ * binary), and bench.py stamps it on every line and profile. */
+const char* rt_kernel_source_sha(void);
 /* device >= 0: HIP ordinal. device = -1: scene-building only (no GPU calls). */
 rt_status rt_create(int32_t device, rt_ctx** out);
 void rt_destroy(rt_ctx* ctx);

@@ -27,7 +27,7 @@ BVH_CACHE_OFF, BVH_CACHE_READ, BVH_CACHE_WRITE = 0, 1, 2
 GATHER_RCCL, GATHER_COPY = 1, 2
 
 # Every symbol include/rtmi.h declares (checked by tests/test_abi.py).
-ABI_VERSION = 9  # include/rtmi.h RTMI_ABI_VERSION
+ABI_VERSION = 10  # include/rtmi.h RTMI_ABI_VERSION
 
 EXPORTS = [
     "rt_abi_version", "rt_create", "rt_destroy", "rt_last_error", "rt_clear_scene",
@@ -42,7 +42,7 @@ EXPORTS = [
     "rt_render_u8", "rt_accumulate", "rt_render_multi", "rt_gamma_u8",
     "rt_build_flags", "rt_set_bvh_cache", "rt_bvh_cache_stats",
     "rt_owned_rows", "rt_max_tile_rows", "rt_render_multi_device", "rt_comm_unique_id", "rt_comm_init",
-    "rt_comm_destroy", "rt_gather_rows", "rt_assemble_rows", "rt_kernel_variant_name",
+    "rt_comm_destroy", "rt_gather_rows", "rt_assemble_rows", "rt_kernel_variant_name", "rt_kernel_source_sha",
     "rt_camera_initialize", "rt_camera_update_view_matrix", "rt_camera_walk", "rt_camera_strafe", "rt_camera_raise",
     "rt_camera_yaw", "rt_camera_pitch", "rt_camera_orbit", "rt_camera_set_aperture", "rt_camera_apply",
     "rt_get_camera", "rt_canvas_create", "rt_canvas_destroy", "rt_canvas_clear_accumulation",
@@ -120,6 +120,7 @@ def lib():
             f"librtmi.so not found at {LIB_PATH}: build it with __graft_entry__.build() "
             "(the renderer has no fallback path)")
     L = C.CDLL(LIB_PATH)
+    check_source_digest(L)
     vp, fp, i32 = C.c_void_p, C.POINTER(C.c_float), C.c_int32
     L.rt_abi_version.restype = i32
     L.rt_create.argtypes = [i32, C.POINTER(vp)]
@@ -185,6 +186,8 @@ def lib():
     L.rt_canvas_write_accumulation.argtypes = [vp, fp]
     L.rt_kernel_variant_name.argtypes = [C.c_uint32]
     L.rt_kernel_variant_name.restype = C.c_char_p
+    L.rt_kernel_source_sha.argtypes = []
+    L.rt_kernel_source_sha.restype = C.c_char_p
     L.rt_set_bvh_cache.argtypes = [vp, i32]
     L.rt_bvh_cache_stats.argtypes = [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]
     L.rt_owned_rows.argtypes = [i32, i32, i32, i32]
@@ -199,6 +202,51 @@ def lib():
     L.rt_assemble_rows.argtypes = [vp, C.POINTER(RenderParams), i32, vp, vp, vp]
     _lib = L
     return L
+
+
+class StaleLibraryError(ImportError):
+    pass
+
+
+def library_digest(L) -> str:
+    """rt_kernel_source_sha() of a loaded library ('' for a library that predates it)."""
+    f = getattr(L, "rt_kernel_source_sha", None)
+    if f is None:
+        return ""
+    f.argtypes = []
+    f.restype = C.c_char_p
+    return (f() or b"").decode()
+
+
+def tree_digest(csrc: str = CSRC) -> str | None:
+    """The digest of the library's sources in this tree (None if they are not here)."""
+    from .source_digest import source_digest
+
+    if not os.path.exists(os.path.join(csrc, "Makefile")):
+        return None
+    return source_digest(csrc)
+
+
+def check_source_digest(L, csrc: str = CSRC, lib_path: str | None = None) -> str:
+    """Refuses a library that was not built from the sources next to it: its embedded digest
+    (rt_kernel_source_sha, baked in by the Makefile) must equal the tree's. A library named by
+    RTMI_LIB (an A/B build of other sources or flags, tools/) is exempt, and bench.py then reports
+    the library's own digest. Returns the library's digest."""
+    lib_path = lib_path or LIB_PATH
+    have = library_digest(L)
+    if os.environ.get("RTMI_LIB"):
+        return have
+    want = tree_digest(csrc)
+    if want is not None and have != want:
+        raise StaleLibraryError(
+            f"stale {lib_path}: built from sources with digest {have or '(none)'}, but the tree's sources "
+            f"hash to {want}; rebuild it (__graft_entry__.build() or make -C {csrc})")
+    return have
+
+
+def source_sha() -> str:
+    """The loaded library's source digest (what bench.py stamps on its line)."""
+    return library_digest(lib())
 
 
 def build_flags() -> int:

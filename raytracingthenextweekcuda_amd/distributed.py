@@ -178,6 +178,115 @@ class RowShardedFrame:
         return self.frame if self.rank == 0 else None
 
 
+class RcclRowFrames:
+    """N > 1 frames through the C ABI, the exchange bench.py times.
+
+    Every rank renders its row tiles with rt_render_device on context b's own stream, and the
+    SAME stream then carries that frame's rt_gather_rows: one ncclGather of the tiles to rank 0
+    plus the root's de-interleave kernel (include/rtmi.h). No collective stream
+    exists besides the render streams, so a rank's streams are its render streams and the
+    default stream (which the timed loop leaves idle): three contexts fit the process's four
+    hardware queues (GPU_MAX_HW_QUEUES). torch.distributed (gloo) carries only the control plane:
+    the RCCL unique id, barriers and the per-rank stats.
+
+    Frame b of a rotation lands in context b's staging buffer and in frames[b] on rank 0; the
+    tile and frame of context b are reused by frame b + n, which its stream orders after this
+    frame's gather. `comm_world` 1 with `world` > 1 is the one-GPU rehearsal of a shard
+    (bench.py --rehearse-shard): rank 0's rows of a `world`-rank frame, gathered by a one-rank
+    communicator (the same kernels and streams; only the landing is this rank's tile).
+    """
+
+    def __init__(self, renderers, width, height, row_block, rank, world, streams, device,
+                 comm_world=None, group=None):
+        import ctypes as C
+
+        import torch
+        import torch.distributed as dist
+
+        from . import _lib
+
+        self.C, self.torch, self.L = C, torch, _lib.lib()
+        self.renderers, self.streams = renderers, streams
+        self.width, self.height, self.row_block = width, height, row_block
+        self.rank, self.world = rank, world
+        self.comm_world = world if comm_world is None else comm_world
+        self.max_rows = max_tile_rows(height, row_block, world)
+        idb = (C.c_uint8 * 128)()
+        if self.comm_world > 1:
+            ids = torch.zeros(128, dtype=torch.uint8)
+            if dist.get_rank(group) == 0:
+                r0 = self.L.rt_comm_unique_id(idb)
+                if r0 != 0:
+                    raise RuntimeError(f"rt_comm_unique_id failed ({r0})")
+                ids.copy_(torch.frombuffer(bytearray(bytes(idb)), dtype=torch.uint8))
+            dist.broadcast(ids, src=0, group=group)
+            C.memmove(idb, bytes(ids.numpy().tobytes()), 128)
+        elif self.L.rt_comm_unique_id(idb) != 0:
+            raise RuntimeError("rt_comm_unique_id failed")
+        self.comm = C.c_void_p()
+        renderers[0]._check(self.L.rt_comm_init(renderers[0].ctx, idb, self.comm_world,
+                                                 rank if self.comm_world > 1 else 0, C.byref(self.comm)))
+        n = len(renderers)
+        self.tiles = [torch.zeros((self.max_rows, width, 3), dtype=torch.float32, device=device) for _ in range(n)]
+        self.tile = self.tiles[0]
+        # the root's frames (the rehearsal lands its one tile: a frame of max_rows rows)
+        fh = height if self.comm_world > 1 else self.max_rows
+        self.frames = ([torch.zeros((fh, width, 3), dtype=torch.float32, device=device) for _ in range(n)]
+                       if rank == 0 else None)
+        self.frame = self.frames[0] if self.frames else None
+        # the gather's frame geometry: the real frame, or in the rehearsal the tile itself as a
+        # one-rank frame (identity de-interleave)
+        from .renderer import Renderer
+
+        if self.comm_world > 1:
+            self.gparams = Renderer.params(width, height, 1, 1, row_block=row_block, row_rank=rank, row_world=world)
+        else:
+            self.gparams = Renderer.params(width, self.max_rows, 1, 1, row_block=self.max_rows)
+        self.n_submitted = 0
+
+    def _gather(self, b, stream_ptr):
+        C = self.C
+        fr = self.frames[b].data_ptr() if self.frames else None
+        r = self.renderers[b]
+        g_rank = self.rank if self.comm_world > 1 else 0
+        r._check(self.L.rt_gather_rows(r.ctx, self.comm, C.byref(self.gparams), g_rank, self.comm_world,
+                                       C.c_void_p(self.tiles[b].data_ptr()), C.c_void_p(fr), C.c_void_p(stream_ptr)))
+
+    def submit(self, render_into: Callable[..., None]):
+        """render_into(tile, b) enqueues this rank's rows on streams[b]; the frame's gather follows
+        on the same stream."""
+        b = self.n_submitted % len(self.renderers)
+        self.n_submitted += 1
+        render_into(self.tiles[b], b)
+        self._gather(b, self.streams[b].cuda_stream)
+        if self.frames:
+            self.frame = self.frames[b]
+
+    def drain(self):
+        """The caller's current stream waits for the last submitted frame (gather included)."""
+        if self.n_submitted:
+            self.torch.cuda.current_stream().wait_stream(self.streams[(self.n_submitted - 1) % len(self.renderers)])
+        return self.frame if self.rank == 0 else None
+
+    def gather(self, events=None):
+        """Gathers context 0's tile on the current stream (the isolated frames after the timed
+        region); `events` (start, end) are recorded around the collective alone."""
+        s = self.torch.cuda.current_stream()
+        if events:
+            events[0].record(s)
+        self._gather(0, s.cuda_stream)
+        if events:
+            events[1].record(s)
+        if self.frames:
+            self.frame = self.frames[0]
+        return self.frame if self.rank == 0 else None
+
+    def close(self):
+        if self.comm:
+            self.L.rt_comm_destroy(self.comm)
+            self.comm = None
+
+
 def render_params_for_rank(renderer, width, height, spp, depth, row_block, rank, world, seed=1984,
                            sample_offset=0, lanes_per_pixel=0):
     """rt_render_params for this rank's share of the frame."""

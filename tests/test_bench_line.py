@@ -57,3 +57,28 @@ def test_one_rank_line_has_no_scale_block():
     d = _run(1)
     assert d["n_gpus"] == 1 and "scale" not in d
     assert d["frame_latency"]["gather_ms"] == 0.05 and d["frame_latency"]["kernel_ms_isolated"] == 4.0
+
+
+def test_bench_spawns_its_own_ranks_without_an_outer_launcher():
+    """`python3 bench.py --gpus 2` (the driver's form for every N) starts torch.distributed.run as a
+    child process and forwards rank 0's line."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
+           "--line-selftest", "--no-cpu-baseline"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    out = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [line for line in out.stdout.splitlines() if line.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scale"]["world_size_comm"] == 2
+    assert d["value"] == pytest.approx(3.0e6 / 0.011 / 1e6, abs=1e-3)
+    # three render streams + the default stream: within the process's 4 hardware queues
+    assert d["config"]["exchange"] == "abi" and d["config"]["streams_per_rank"] == 4
+
+
+def test_bench_refuses_a_world_size_that_is_not_gpus():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", OMP_NUM_THREADS="1")
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--line-selftest"],
+                         cwd=REPO, capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr

@@ -10,6 +10,9 @@
 #   TRAFFIC   FETCH_SIZE and WRITE_SIZE passes (separate runs), for profiles/pmc_traffic.json
 #   PROF      rocprofv3 --kernel-trace --stats of these workloads (--no-overlap)
 #   MULTI=1   examples/multigpu (RCCL through the C ABI, N = 1 on this box)
+#   STREAMS=1 tools/queue_probe.py (how many streams run concurrently: 4 and 8 hardware queues), then
+#             bench.py --rehearse-shard N (rank 0's rows of an N-rank CB1 frame, the N > 1 stream layout and
+#             ABI exchange on a one-rank communicator) for N in SHARDS (default "8") and CTXS contexts
 # Every GPU step has its own time limit; a fault, abort or time-out ends the session there.
 #   TAG=r03c TESTS=1 BENCH=1 VALU="cornellbox1 bunny" bash tools/gpu_session.sh
 set -u
@@ -70,6 +73,24 @@ for sc in ${PROF:-}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$sc" -o run --output-format csv -- python3 bench.py --scene $sc --steps ${PROF_STEPS:-10} --warmup ${PROF_WARMUP:-2} --no-cpu-baseline --no-overlap $(lay $sc) > "$O/prof_$sc.log" 2>&1
   stop_if_fatal $? prof_$sc
 done
+if [ "${STREAMS:-0}" = "1" ]; then
+  timeout -k 10 120 python tools/queue_probe.py > "$O/queue_probe.json" 2> "$O/queue_probe.err"
+  stop_if_fatal $? queue_probe
+  timeout -k 10 120 python tools/queue_probe.py --rccl-first > "$O/queue_probe_rccl_first.json" 2> "$O/queue_probe_rccl_first.err"
+  stop_if_fatal $? queue_probe_rccl_first
+  GPU_MAX_HW_QUEUES=8 timeout -k 10 120 python tools/queue_probe.py > "$O/queue_probe_q8.json" 2> "$O/queue_probe_q8.err"
+  stop_if_fatal $? queue_probe_q8
+  for rep in $(seq 1 ${REPS:-1}); do
+    for n in ${SHARDS:-8}; do for c in ${CTXS:-2 3}; do
+      timeout -k 10 180 python bench.py --rehearse-shard $n --contexts $c --steps ${SSTEPS:-60} --warmup 6 --no-cpu-baseline > "$O/shard${n}_c${c}_r$rep.log" 2>&1
+      stop_if_fatal $? shard${n}_c${c}_r$rep
+    done; done
+    for q in ${QUEUES:-}; do  # more hardware queues for the process: one more context than the default
+      GPU_MAX_HW_QUEUES=$q timeout -k 10 180 python bench.py --rehearse-shard 8 --contexts 4 --steps ${SSTEPS:-60} --warmup 6 --no-cpu-baseline > "$O/shard8_c4_q${q}_r$rep.log" 2>&1
+      stop_if_fatal $? shard8_c4_q${q}_r$rep
+    done
+  done
+fi
 if [ "${MULTI:-0}" = "1" ] && [ -x ./examples/multigpu ]; then
   timeout -k 10 120 ./examples/multigpu 128 96 8 1 > "$O/multigpu.log" 2>&1
   stop_if_fatal $? multigpu
