@@ -546,6 +546,7 @@ def build_line(args, agg: dict, world: int, cpu=None) -> dict:
             "exchange": agg.get("exchange"),
             "streams_per_rank": (agg.get("contexts", 1) + 1 + (1 if agg.get("exchange") == "torch" else 0)),
             "rehearse_shard": args.rehearse_shard or None,
+            "n_cu": agg["n_cu"],
             "kernel_source_sha": sha,
             "parallelism": f"row-tiles x{world} + RCCL gather" if world > 1 else "single GPU",
             "segments_per_frame": int(segs / K),

@@ -148,6 +148,8 @@ typedef struct rt_render_stats {
     uint32_t variant;       /* RT_VARIANT_* of the last launch */
     uint32_t substreams_per_item; /* sub-streams a work item runs in sequence (work queue; 1 on the static
                                      grid): the schedule's item length, which does not change the image */
+    uint32_t stack_depth;         /* BVH traversal stack entries per lane of the launch (the scene's deepest
+                                     path; 0 for a launch without BVH traversal) */
 } rt_render_stats;
 
 #define RT_GATHER_RCCL 1 /* one ncclGather over the contexts' devices */
@@ -376,6 +378,10 @@ rt_status rt_commit(rt_ctx* ctx);
  * [6] BVH nodes, [7] spheres placed behind the object BVH (the counts
  * [1]/[2] include them). */
 rt_status rt_scene_info(const rt_ctx* ctx, int32_t out[8]);
+/* The rayColor BVHs' deepest root-to-leaf path in child-pair records (meshes of more than 64
+ * triangles, sphere groups): the traversal stack entries per lane a render needs (rt_render_stats.
+ * stack_depth; at most 32, the builder's limit like BVH_STACK_SIZE, CUDAPathTracer.h:43); 0 without BVHs. */
+rt_status rt_scene_bvh_depth(const rt_ctx* ctx, int32_t* out);
 /* FNV-1a 64 digest of the committed host tables (objects, triangles, materials,
  * BVH nodes, triangle maps, camera): two scene builds that agree on it upload
  * identical device data. Works on device -1 contexts. */

@@ -37,7 +37,7 @@ EXPORTS = [
     "rt_cube", "rt_mesh", "rt_mesh_obj", "rt_mesh_triangle_count", "rt_mesh_vertices",
     "rt_mesh_ply", "rt_ply_bvh_image", "rt_load_object", "rt_process_triangle_data",
     "rt_pathtrace_bvh_image", "rt_set_bvh_builder", "rt_bvh_build_stats", "rt_ply_bvh_image_gpu",
-    "rt_camera", "rt_commit", "rt_scene_info", "rt_scene_digest", "rt_load_yaml_scene",
+    "rt_camera", "rt_commit", "rt_scene_info", "rt_scene_bvh_depth", "rt_scene_digest", "rt_load_yaml_scene",
     "rt_render", "rt_render_device", "rt_sync_stats",
     "rt_render_u8", "rt_accumulate", "rt_render_multi", "rt_gamma_u8",
     "rt_build_flags", "rt_set_bvh_cache", "rt_bvh_cache_stats",
@@ -92,6 +92,7 @@ class RenderStats(C.Structure):
         ("debug", C.c_uint64 * 8),
         ("refill", C.c_uint32), ("queue_blocks", C.c_uint32), ("gather", C.c_uint32), ("launches", C.c_uint32),
         ("kernel_ms_sum", C.c_double), ("variant", C.c_uint32), ("substreams_per_item", C.c_uint32),
+        ("stack_depth", C.c_uint32),
     ]
 
 
@@ -157,6 +158,7 @@ def lib():
     L.rt_camera.argtypes = [vp, fp, fp, fp] + [C.c_float] * 6
     L.rt_commit.argtypes = [vp]
     L.rt_scene_info.argtypes = [vp, C.POINTER(C.c_int32)]
+    L.rt_scene_bvh_depth.argtypes = [vp, C.POINTER(C.c_int32)]
     L.rt_scene_digest.argtypes = [vp, C.POINTER(C.c_uint64)]
     L.rt_load_yaml_scene.argtypes = [vp, C.c_char_p, C.c_char_p, i32, i32]
     L.rt_render.argtypes = [vp, C.POINTER(RenderParams), fp]

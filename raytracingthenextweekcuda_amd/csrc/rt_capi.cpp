@@ -644,6 +644,13 @@ rt_status rt_scene_info(const rt_ctx* c, int32_t out[8]) {
     return RT_OK;
 }
 
+rt_status rt_scene_bvh_depth(const rt_ctx* c, int32_t* out) {
+    if (!c || !out) return RT_ERR_INVALID;
+    if (!c->committed) return RT_ERR_STATE;
+    *out = c->scene.nodes.empty() ? 0 : (int32_t)c->scene.bvh_max_depth;
+    return RT_OK;
+}
+
 }  // extern "C"
 
 rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& L) {
@@ -782,7 +789,10 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
         }
     }
     const uint32_t variant = rt::select_variant(pathtrace, L.queue != 0, bvh, c->has_media, c->full_scan, c->bvh_parts);
-    if (L.queue == 0 || pathtrace) L.grp_log2 = 0;  // the static grid and pathTrace: one sub-stream per item
+    if (L.queue == 0 || pathtrace) {  // the static grid and pathTrace: one sub-stream per item
+        L.grp_log2 = 0;
+        L.n_qitems = L.n_items;
+    }
     if (L.queue == 0 && L.lanes_per_pixel > 64)  // the static grid keeps a pixel's sub-streams in one wave
         return fail(c, RT_ERR_INVALID, "lanes_per_pixel > 64 needs the work queue, which this frame does not fit");
     const bool keep = (p->flags & RT_RENDER_KEEP_COUNTERS) != 0;
@@ -839,6 +849,7 @@ rt_status rtc::launch(rt_ctx* c, const rt_render_params* p, const rt::RenderLaun
     c->last.queue_blocks = (uint32_t)L.queue;
     c->last.variant = variant;
     c->last.substreams_per_item = L.queue ? 1u << L.grp_log2 : 1u;
+    c->last.stack_depth = (pathtrace ? c->pt_tris > 0 : bvh) ? (uint32_t)L.stack_depth : 0u;
     c->stats_pending = true;
     return RT_OK;
 }

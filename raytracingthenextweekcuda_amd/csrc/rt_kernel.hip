@@ -228,6 +228,13 @@ struct Hit {
 };
 
 constexpr int kMaxRun = (int)kMeshRunMax;  // meshes per run (rt_scene.cpp marks the runs)
+// The render kernels' traversal stacks hold L.stack_depth entries per lane (the scene's deepest path in
+// pair records, rt_scene.cpp PairBuilder::max_pairs) PLUS this spare slot: a lane that does not push
+// writes its would-be entry to slot stack_cap = L.stack_depth unconditionally (mesh_bvh_pairs' lane
+// selects), so that slot must exist in every lane's column. The kernel's stack base and the launch's
+// dynamic LDS size (stack_bytes) both count it; tests/test_fuzz_parity.py renders a chain BVH whose
+// deepest pair is reached with both children hit.
+constexpr int kStackSpare = 1;
 
 struct WaveLds {
     unsigned long long key[64];  // per-ray (t bits << 32 | triangle) minima
@@ -314,6 +321,22 @@ __device__ __forceinline__ float div_y(float a, float b, float y) {
     return __builtin_fmaf(__builtin_fmaf(-b, q0, a), y, q0);
 }
 
+// __shfl(v, src, 64) without HIP's lane-id arithmetic: ds_bpermute reads lane (address / 4) mod 64,
+// the same lane __shfl picks. HIP's version derives its own lane id (mbcnt) for the width mask,
+// a value the register allocator kept live across the persistent loop - and spilled to scratch.
+#ifndef RT_LANE_READ
+#define RT_LANE_READ 1  // 0: HIP's __shfl (A/B)
+#endif
+#if RT_LANE_READ
+__device__ __forceinline__ int lane_read(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
+__device__ __forceinline__ float lane_read(float v, int src) {
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
+}
+#else
+__device__ __forceinline__ int lane_read(int v, int src) { return __shfl(v, src, 64); }
+__device__ __forceinline__ float lane_read(float v, int src) { return __shfl(v, src, 64); }
+#endif
+
 // Sets an LDS 64-bit minimum slot to +inf (all ones).
 __device__ __forceinline__ void key_reset(unsigned long long& k) {
     const uint32_t ones = fresh_u32(~0u);
@@ -378,9 +401,9 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
         const uint32_t e = act ? W.slot[(qdone + (uint32_t)lane) & (kQ - 1)] : 0u;
         const uint32_t k = e >> 6;
         const int own = (int)(e & 63u);
-        const v3 po{__shfl(o.x, own, 64), __shfl(o.y, own, 64), __shfl(o.z, own, 64)};
-        const v3 pd{__shfl(d.x, own, 64), __shfl(d.y, own, 64), __shfl(d.z, own, 64)};
-        const float pt0 = __shfl(h.t, own, 64);
+        const v3 po{lane_read(o.x, own), lane_read(o.y, own), lane_read(o.z, own)};
+        const v3 pd{lane_read(d.x, own), lane_read(d.y, own), lane_read(d.z, own)};
+        const float pt0 = lane_read(h.t, own);
         // lanes past `count` test triangle 0 (valid) and drop the result: no branch around the loads
         const float t = tri_t(tris[k], po, pd);
         if (act && t <= pt0)
@@ -401,13 +424,13 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             const bool thief = idle && lane_rank(im) < nv;
             const int vr = W.src[lane_rank(im)];  // (read by every lane: the rank is below 64)
             const int vic = thief ? vr : lane;
-            const int vt = __shfl(bot, vic, 64);  // the victim's oldest pending reference
+            const int vt = lane_read(bot, vic);  // the victim's oldest pending reference
             auto take = [&](float& x) {
-                const float v = __shfl(x, vic, 64);
+                const float v = lane_read(x, vic);
                 if (thief) x = v;
             };
             {
-                const int v_owner = __shfl(owner, vic, 64);
+                const int v_owner = lane_read(owner, vic);
                 if (thief) owner = v_owner;
             }
             take(ro.x); take(ro.y); take(ro.z);
@@ -558,9 +581,9 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
         const uint32_t e = W.slot[r];
         const int src = (int)(e & 63u);
         const uint32_t tri = (e >> 6) + (p - r * m);
-        const v3 ro{__shfl(o.x, src, 64), __shfl(o.y, src, 64), __shfl(o.z, src, 64)};
-        const v3 rd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
-        const float rt0 = __shfl(t0, src, 64);
+        const v3 ro{lane_read(o.x, src), lane_read(o.y, src), lane_read(o.z, src)};
+        const v3 rd{lane_read(d.x, src), lane_read(d.y, src), lane_read(d.z, src)};
+        const float rt0 = lane_read(t0, src);
         // inactive lanes test the pair of slot 0 (a valid triangle) and drop the result: no divergent
         // branch around the loads
         const float t = tri_t_culled(tris[tri], ro, rd);
@@ -574,7 +597,7 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
         const uint32_t r = m > 1u ? __umulhi(pc, magic) : pc;
         const uint32_t e = W.slot[r];
         const int src = (int)(e & 63u);
-        const v3 rd{__shfl(d.x, src, 64), __shfl(d.y, src, 64), __shfl(d.z, src, 64)};
+        const v3 rd{lane_read(d.x, src), lane_read(d.y, src), lane_read(d.z, src)};
         const TriRec& tr = tris[(e >> 6) + (pc - r * m)];
         const bool keep = act && !(dot(rd, v3{tr.nx, tr.ny, tr.nz}) > kFltEpsilon);  // TriangleMesh.cu:72
         const uint64_t km = __ballot(keep);
@@ -640,10 +663,10 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
         const uint32_t e = act ? W.slot[(qdone + (uint32_t)lane) & (kQ - 1)] : 0u;
         const uint32_t k = e >> 6;
         const int own = (int)(e & 63u);
-        const v3 po{__shfl(ray.o.x, own, 64), __shfl(ray.o.y, own, 64), __shfl(ray.o.z, own, 64)};
-        const v3 pd{__shfl(ray.d.x, own, 64), __shfl(ray.d.y, own, 64), __shfl(ray.d.z, own, 64)};
-        const float ptime = __shfl(ray.time, own, 64), pt0 = __shfl(h.t, own, 64);
-        const float pinva = __shfl(inva, own, 64);  // the owner's 1 / dot(d, d)
+        const v3 po{lane_read(ray.o.x, own), lane_read(ray.o.y, own), lane_read(ray.o.z, own)};
+        const v3 pd{lane_read(ray.d.x, own), lane_read(ray.d.y, own), lane_read(ray.d.z, own)};
+        const float ptime = lane_read(ray.time, own), pt0 = lane_read(h.t, own);
+        const float pinva = lane_read(inva, own);  // the owner's 1 / dot(d, d)
         unsigned long long mine = ~0ull;
         if (act) {
             const ObjRec ob = load_obj(objs, (int)k);
@@ -1170,7 +1193,7 @@ __device__ __forceinline__ uint32_t queue_take(const RenderLaunch& L, int sh, ui
     const int first = __builtin_ctzll(need);
     uint32_t base = 0;
     if (lane == first) base = atomicAdd(L.q_counter + sh * kQueueStride, (unsigned)__popcll(need));
-    base = (uint32_t)__shfl((int)base, first, 64);
+    base = (uint32_t)lane_read((int)base, first);
     const uint32_t it = lo + base + (uint32_t)lane_rank(need);
     if (it >= hi) return ~0u;
     // group it -> (pixel, first sub-stream c < S'): item = pixel << sp_log2 | c
@@ -1230,6 +1253,9 @@ __global__ __launch_bounds__(256) void combine_kernel(RenderLaunch L, float* __r
     write_pixel(L, out, ((size_t)lrow * (size_t)L.cols + (size_t)(px - L.col0)) * 3, acc, (float)L.spp);
 }
 
+#ifndef RT_DEPTH_LDS
+#define RT_DEPTH_LDS 1  // linear-scan kernels: the path depth in the camera slot (0: a VGPR; A/B)
+#endif
 #ifndef RT_CAM_BATCH
 #define RT_CAM_BATCH 32  // lanes lacking a prepared next sample that start a camera pass on their own
 #endif
@@ -1303,8 +1329,8 @@ __device__ __forceinline__ void tail_steal(const RenderLaunch& L, WaveLds& W, in
         for (int k = 0; k < 4; ++k) {
             const int src = (int)((tl_pack >> (8 * k)) & 0xFFu) - 1;
             const int sl = waiting && src >= 0 ? src : lane;
-            vals[k] = v3{__shfl(thr.x, sl, 64), __shfl(thr.y, sl, 64), __shfl(thr.z, sl, 64)};
-            const bool hd = __shfl((int)held, sl, 64) != 0;
+            vals[k] = v3{lane_read(thr.x, sl), lane_read(thr.y, sl), lane_read(thr.z, sl)};
+            const bool hd = lane_read((int)held, sl) != 0;
             if (waiting && src >= 0) ready = ready && hd;
         }
         if (waiting && ready) {
@@ -1316,7 +1342,7 @@ __device__ __forceinline__ void tail_steal(const RenderLaunch& L, WaveLds& W, in
             tl_pack = 0;
         }
         // thieves whose owner has folded their value are free again
-        const uint32_t otp = (uint32_t)__shfl((int)tl_pack, towner >= 0 ? towner : lane, 64);
+        const uint32_t otp = (uint32_t)lane_read((int)tl_pack, towner >= 0 ? towner : lane);
         if (held && otp == 0u) {
             held = false;
             towner = -1;
@@ -1336,8 +1362,8 @@ __device__ __forceinline__ void tail_steal(const RenderLaunch& L, WaveLds& W, in
     __builtin_amdgcn_wave_barrier();
     const bool thief = idle && ri < nv;
     const int vic = thief ? W.src[ri] : lane;
-    const int v_end = __shfl(own_end, vic, 64);
-    const uint32_t v_item = (uint32_t)__shfl((int)item, vic, 64) & ~kPrepared;
+    const int v_end = lane_read(own_end, vic);
+    const uint32_t v_item = (uint32_t)lane_read((int)item, vic) & ~kPrepared;
     if (spare && rv < ni) {  // robbed: its last unstarted sample goes to the thief of the same rank
         own_end -= SP;
         const int pos = (own_end - c) >> L.sp_log2;
@@ -1385,7 +1411,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         W.grp_s[lane] = 0;
         W.grp_m[lane] = 0;
     }
-    uint32_t* stack = kBvh ? dyn_stacks + (size_t)wave * (L.stack_depth + 1) * 64 + lane : nullptr;
+    uint32_t* stack = kBvh ? dyn_stacks + (size_t)wave * (L.stack_depth + kStackSpare) * 64 + lane : nullptr;
 
     // Lane layout: SP = lanes_per_pixel adjacent lanes share one pixel and split
     // its samples (sub-lane c takes samples c, c+SP, c+2SP, ...). A wave covers
@@ -1492,7 +1518,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                                                  (float)(L.height - 1));
                     C.a[lane] = float4{cr.o.x, cr.o.y, cr.o.z, cr.d.x};
                     C.b[lane] = float4{cr.d.y, cr.d.z, cr.time, __uint_as_float(r2.s0)};
+#if RT_DEPTH_LDS
+                    // (.w holds the lane's path depth, which a tracing lane still needs)
+                    uint32_t* cw = reinterpret_cast<uint32_t*>(&C.c[lane]);
+                    cw[0] = r2.s1;
+                    cw[1] = r2.s2;
+                    cw[2] = r2.s3;
+#else
                     C.c[lane] = uint4{r2.s1, r2.s2, r2.s3, 0u};
+#endif
                     item |= kPrepared;
                 }
             }
@@ -1506,6 +1540,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                 need_cam = false;
                 thr = v3{1.0f, 1.0f, 1.0f};
                 depth = 0;
+#if RT_DEPTH_LDS
+                reinterpret_cast<uint32_t*>(&C.c[lane])[3] = fresh_u32(0u);
+#endif
                 if (L.max_depth <= 0)  // rayColor with BOUNCES = 0 returns black
                     sample_done(L, v3{0.0f, 0.0f, 0.0f}, SP, item, own_end, s, sum, thr, alive, need_cam,
                                 towner, held, waiting, tl_pack);
@@ -1641,8 +1678,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             if (scattered) {
                 thr = mul(thr, att);
                 ray = Ray{p, nd, ray.time};
-                ++depth;
-                done = depth >= L.max_depth;
+#if RT_DEPTH_LDS
+                if constexpr (kCamPf) {
+                    // the linear-scan kernels keep the path depth in the camera slot's spare word (LDS)
+                    // instead of a VGPR of the persistent loop (at 7 waves/SIMD the CB1 kernel spilled it)
+                    uint32_t* dw = reinterpret_cast<uint32_t*>(&cslots[wave].c[lane]) + 3;
+                    const uint32_t dn = *dw + 1u;
+                    *dw = dn;
+                    done = (int)dn >= L.max_depth;
+                } else
+#endif
+                {
+                    ++depth;
+                    done = depth >= L.max_depth;
+                }
                 contrib = v3{0.0f, 0.0f, 0.0f};  // exceeded recursion (main.cu:93)
             } else {
                 done = true;
@@ -1673,7 +1722,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         const int base = lane - c;
         v3 acc = sum;
         for (int j = 1; j < SP; ++j) {
-            v3 pj{__shfl(sum.x, base + j, 64), __shfl(sum.y, base + j, 64), __shfl(sum.z, base + j, 64)};
+            v3 pj{lane_read(sum.x, base + j), lane_read(sum.y, base + j), lane_read(sum.z, base + j)};
             acc = add(acc, pj);
         }
         sum = acc;
@@ -1915,9 +1964,9 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
         const uint32_t e = act ? queue[(qdone + (uint32_t)lane) & 255u] : 0u;
         const uint32_t i = e >> 6;
         const int own = (int)(e & 63u);
-        const v3 po{__shfl(ray.o.x, own, 64), __shfl(ray.o.y, own, 64), __shfl(ray.o.z, own, 64)};
-        const v3 pd{__shfl(ray.d.x, own, 64), __shfl(ray.d.y, own, 64), __shfl(ray.d.z, own, 64)};
-        const int pav = __shfl(avoid_in, own, 64);
+        const v3 po{lane_read(ray.o.x, own), lane_read(ray.o.y, own), lane_read(ray.o.z, own)};
+        const v3 pd{lane_read(ray.d.x, own), lane_read(ray.d.y, own), lane_read(ray.d.z, own)};
+        const int pav = lane_read(avoid_in, own);
         if (act) {
             // the Kuchkuda test for list position i (CUDAPathTracer.cu:258-345)
             const int idx = tri_list[i];
@@ -1956,14 +2005,14 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
             const bool thief = idle && lane_rank(im) < nv;
             int vic = lane;
             if (thief) vic = vlist[lane_rank(im)];
-            const int vb = __shfl(bot, vic, 64);
+            const int vb = lane_read(bot, vic);
             auto take = [&](float& x) {
-                const float v = __shfl(x, vic, 64);
+                const float v = lane_read(x, vic);
                 if (thief) x = v;
             };
             {
-                const int v_owner = __shfl(owner, vic, 64);
-                const int v_exact = __shfl((int)r.exact, vic, 64);
+                const int v_owner = lane_read(owner, vic);
+                const int v_exact = lane_read((int)r.exact, vic);
                 if (thief) {
                     owner = v_owner;
                     r.exact = v_exact != 0;
@@ -2315,7 +2364,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
         const int base = lane - c;
         v3 acc = sum;
         for (int j = 1; j < SP; ++j) {
-            v3 pj{__shfl(sum.x, base + j, 64), __shfl(sum.y, base + j, 64), __shfl(sum.z, base + j, 64)};
+            v3 pj{lane_read(sum.x, base + j), lane_read(sum.y, base + j), lane_read(sum.z, base + j)};
             acc = add(acc, pj);
         }
         sum = acc;
@@ -2344,7 +2393,7 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
                             float* out, unsigned long long* counters, hipStream_t stream, hipEvent_t main_done) {
     if (L.queue) {
         if (L.n_items == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
-        const uint32_t waves = (L.n_items + 63u) / 64u;
+        const uint32_t waves = (L.n_qitems + 63u) / 64u;  // the queue's items (grp_log2 = 0 here)
         const uint32_t blocks = std::min<uint32_t>((waves + kQueueBlockWaves - 1) / kQueueBlockWaves,
                                                    (uint32_t)L.queue);
         hipLaunchKernelGGL(pathtrace_kernel<true>, dim3(blocks), dim3(64 * kQueueBlockWaves),
@@ -2380,7 +2429,7 @@ int queue_blocks(int n_cu, uint32_t variant, const RenderLaunch& L) {
             lds = (size_t)bw * (sizeof(WaveLds) + sizeof(CamSlots));
             break;
         default:
-            lds = (size_t)bw * sizeof(WaveLds) + stack_bytes(L, bw, 1);
+            lds = (size_t)bw * sizeof(WaveLds) + stack_bytes(L, bw, kStackSpare);
     }
     const int fit = (int)((size_t)160 * 1024 / (lds ? lds : 1));
     return n_cu * std::max(1, std::min(4 * waves / bw, fit));
@@ -2456,7 +2505,7 @@ uint32_t kernel_build_flags() {
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
-    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1
+    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)
@@ -2478,11 +2527,12 @@ hipError_t launch_render(uint32_t variant, const SceneArgs& sc, const CamRec* ca
                          unsigned long long* counters, hipStream_t stream, hipEvent_t main_done) {
     const int bw = block_waves(L.queue != 0);
     const dim3 block(64 * bw);
-    const size_t lds = stack_bytes(L, bw, 1);
+    const size_t lds = stack_bytes(L, bw, kStackSpare);
     dim3 grid;
     if (L.queue) {
         if (L.n_items == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
-        const uint32_t waves_needed = (L.n_items + 63u) / 64u;
+        // what the queue hands out: groups of 2^grp_log2 sub-streams
+        const uint32_t waves_needed = (L.n_qitems + 63u) / 64u;
         grid = dim3(std::min<uint32_t>((waves_needed + bw - 1) / bw, (uint32_t)L.queue), 1);
     } else {
         grid = dim3((L.cols + 2 * L.tile_w - 1) / (2 * L.tile_w), (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));

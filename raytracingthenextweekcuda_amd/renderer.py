@@ -302,6 +302,12 @@ class Renderer:
                 "grouped_spheres"]
         return {k: int(out[i]) for i, k in enumerate(keys)}
 
+    def bvh_depth(self) -> int:
+        """rt_scene_bvh_depth: the traversal stack entries per lane the committed scene needs."""
+        out = C.c_int32()
+        self._check(self.L.rt_scene_bvh_depth(self.ctx, C.byref(out)))
+        return int(out.value)
+
     def scene_digest(self) -> int:
         """FNV-1a 64 digest of the committed host tables (rt_scene_digest)."""
         out = C.c_uint64()

@@ -250,6 +250,15 @@ def test_frames_in_flight_layout(rtmi):
         rtmi.suzanne_cornell_box(r, 64, 64)
         r.render(64, 64, 32, 3, lanes_per_pixel=0, frames_in_flight=True)
         assert r.stats()["lanes_per_pixel"] == 32 and r.stats()["substreams_per_item"] == 1
+    # pathTrace takes one sub-stream per item even when the flag asks for groups: its queue must
+    # still hand out every item (the item count is taken after the group size is reset)
+    with rtmi.Renderer(0) as r:
+        rtmi.materialball(r, 24, 16)
+        img = r.render(24, 16, 64, 5, lanes_per_pixel=0, integrator="pathTrace", frames_in_flight=True)
+        st = r.stats()
+        assert st["substreams_per_item"] == 1
+        assert np.array_equal(img, r.render(24, 16, 64, 5, lanes_per_pixel=0, integrator="pathTrace"))
+        assert st["segments"] == r.stats()["segments"]
 
 
 def test_auto_lane_layout_bvh(rtmi):

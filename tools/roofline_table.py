@@ -8,7 +8,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PEAK_VALU = 256 * 4 * 2.4 / 2  # G wave64 VALU instructions / s (bench.py VALU_GINST_PER_CU x 256 CUs)
+VALU_GINST_PER_CU = 4 * 2.4 / 2  # G wave64 VALU instructions / s per CU (bench.py)
 PEAK_HBM = 8000.0  # GB/s
 SCENES = ["cornellbox1", "spheres", "bunny", "media", "materialball", "suzanne"]
 
@@ -33,7 +33,10 @@ def main(src):
         lu = valu.get(wl, {}).get("valu_lane_util")
         t = traffic.get(wl, {}).get("hbm_bytes_per_launch")
         sv = valu.get(wl, {}).get("salu_insts_per_segment")
-        sf = sv * segs / (256 * 2.4e9 * kms * 1e-3) if sv else None
+        # the device's CUs as the line measured them (its VALU peak = CUs x 4.8 G/s), as bench.py's salu_frac
+        n_cu = line["config"].get("n_cu") or round(line["roofline"]["peak"] / VALU_GINST_PER_CU)
+        PEAK_VALU = n_cu * VALU_GINST_PER_CU
+        sf = sv * segs / (n_cu * 2.4e9 * kms * 1e-3) if sv else None
         ach = v * segs / (kms * 1e-3) / 1e9 if v else None
         hbm = t / (kms * 1e-3) / 1e9 if t else None
         print(f"| {wl} | `{line['config'].get('variant')}` | {line['ms_per_step']:.3f} | {kms:.3f} | {segs / (line['ms_per_step'] * 1e-3) / 1e9:.2f} | "
