@@ -516,6 +516,211 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
     __builtin_amdgcn_wave_barrier();
 }
 
+#if RT_MESH_WIDE
+// The batched mesh traversal over 4-wide nodes (rt_scene.cpp WideBuilder: the binary SAH tree with
+// adjacent levels collapsed). An inner step is one aligned 128 B node load and four
+// box tests; the hit children are ordered by entry distance (the key's two low bits carry the child
+// slot, so one unsigned sort network orders keys and slots together), the nearest becomes the lane's
+// reference and the others wait in ONE stack entry: the node and their slots, nearest first. A pop
+// takes the entry's next child (one 4 B load of its reference) and keeps the entry while children
+// remain, so a lane holds at most one entry per wide level: the LDS stacks are no deeper than the
+// binary tree's (round 4 pushed every other child and needed 27 entries for the bunny against 18,
+// which cost a block per CU). Thieves take the next child of a victim's oldest entry. Leaves,
+// batched triangle tests, pruning and the (t, index) minimum are those of mesh_bvh_pairs, so the
+// candidate set - and the image - is the binary tree's.
+__device__ __forceinline__ void mesh_bvh_wide(const TriRec* __restrict__ tris,
+                                              const uint32_t* __restrict__ tri_orig,
+                                              const BvhNode* __restrict__ nodes, uint32_t root, uint32_t base,
+                                              bool want, v3 o, v3 d, v3 inv, Hit& h, int32_t obj,
+                                              uint32_t order, uint32_t* wstack, WaveLds& W, int lane,
+                                              Counters& cnt, int cap) {
+    const uint64_t wm = __ballot(want);
+    if (wm == 0) return;
+    key_reset(W.key[lane]);
+    int owner = lane;
+    v3 ro = o, ri = inv;
+    float best = h.t;
+    uint32_t cur = root;  // wide node index or leaf reference
+    bool has = want;
+    int sp = 0, bot = 0;
+    uint32_t qtail = 0, qdone = 0;
+    constexpr uint32_t kQ = (uint32_t)kMaxRun * 64u;
+    constexpr uint32_t kNodeMask = (1u << kWideNodeBits) - 1u;
+    constexpr uint32_t kKeyInf = 0x7F800000u;  // +inf: a missed child
+    const uint32_t* nref = reinterpret_cast<const uint32_t*>(nodes);  // child refs: word 32 q + 24 + slot
+    // an entry whose next child exists for every lane (reads by lanes whose own entry is not used)
+    const uint32_t e_safe = (root & kNodeMask) | (1u << 29);
+    __builtin_amdgcn_wave_barrier();
+    auto batch = [&](uint32_t count) {
+        const bool act = (uint32_t)lane < count;
+        const uint32_t e = act ? W.slot[(qdone + (uint32_t)lane) & (kQ - 1)] : 0u;
+        const uint32_t k = e >> 6;
+        const int own = (int)(e & 63u);
+        const v3 po{lane_read(o.x, own), lane_read(o.y, own), lane_read(o.z, own)};
+        const v3 pd{lane_read(d.x, own), lane_read(d.y, own), lane_read(d.z, own)};
+        const float pt0 = lane_read(h.t, own);
+        const float t = tri_t(tris[k], po, pd);
+        if (act && t <= pt0)
+            atomicMin(&W.key[own], ((unsigned long long)__float_as_uint(t) << 32) | tri_orig[2 * k]);
+        qdone += count;
+        __builtin_amdgcn_wave_barrier();
+    };
+    // the entry without its next child (0: none left)
+    auto rest_of = [&](uint32_t e) -> uint32_t {
+        const uint32_t n = e >> 29;
+        return n > 1u ? ((e & kNodeMask) | (((e >> (kWideNodeBits + 2)) & 15u) << kWideNodeBits) | ((n - 1u) << 29))
+                      : 0u;
+    };
+    auto next_ref = [&](uint32_t e) -> uint32_t {
+        return nref[32u * (e & kNodeMask) + 24u + ((e >> kWideNodeBits) & 3u)];
+    };
+    for (;;) {
+        if (__ballot(has || sp > bot) == 0) break;
+        // steal: the r-th idle lane takes the next child of the oldest entry of the r-th lane with a spare one
+        const bool idle = !has && sp == bot;
+        const bool spare = sp - bot >= (has ? 1 : 2);
+        const uint64_t im = __ballot(idle), vm = __ballot(spare);
+        if (im != 0 && vm != 0) {
+            const int nv = __popcll(vm), ni = __popcll(im);
+            if (spare) W.src[lane_rank(vm)] = lane;
+            __builtin_amdgcn_wave_barrier();
+            const bool thief = idle && lane_rank(im) < nv;
+            const int vr = W.src[lane_rank(im)];
+            const int vic = thief ? vr : lane;
+            const int vt = lane_read(bot, vic);
+            auto take = [&](float& x) {
+                const float v = lane_read(x, vic);
+                if (thief) x = v;
+            };
+            {
+                const int v_owner = lane_read(owner, vic);
+                if (thief) owner = v_owner;
+            }
+            take(ro.x); take(ro.y); take(ro.z);
+            take(ri.x); take(ri.y); take(ri.z);
+            take(best);
+            const bool robbed = spare && lane_rank(vm) < ni;
+            {
+                const uint32_t ve = wstack[vt * 64 + vic];  // the victim's oldest entry (a valid slot for every lane)
+                const uint32_t vref = next_ref(thief ? ve : e_safe);
+                const float kb = __uint_as_float((uint32_t)(W.key[owner] >> 32));
+                cur = thief ? vref : cur;
+                best = thief ? fminf(best, kb) : best;
+                sp = thief ? 0 : sp;
+                has = has || thief;
+                // the victim drops the child its thief took: the entry shrinks, or is gone
+                const uint32_t mine = wstack[bot * 64 + lane];
+                const uint32_t rest = rest_of(mine);
+                wstack[(robbed && rest ? bot : cap) * 64 + lane] = rest;
+                bot = thief ? 0 : bot + (robbed && !rest ? 1 : 0);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        {  // pop the newest entry's next child (the entry stays while children remain)
+            const bool pop = !has && sp > bot;
+            if (__ballot(pop) != 0) {
+                const uint32_t e = wstack[(pop ? sp - 1 : 0) * 64 + lane];
+                const uint32_t r = next_ref(pop ? e : e_safe);
+                const uint32_t rest = rest_of(e);
+                const float kb = __uint_as_float((uint32_t)(W.key[owner] >> 32));
+                wstack[(pop && rest ? sp - 1 : cap) * 64 + lane] = rest;
+                cur = pop ? r : cur;
+                best = pop ? fminf(best, kb) : best;
+                sp -= pop && !rest ? 1 : 0;
+                has = has || pop;
+            }
+            const bool empty = !has && sp == bot;
+            sp = empty ? 0 : sp;
+            bot = empty ? 0 : bot;
+        }
+        if (has && !(cur & kLeafRef)) {
+            const float4* q = reinterpret_cast<const float4*>(nodes + 4 * (size_t)cur);
+            const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
+            const uint4 rf = reinterpret_cast<const uint4*>(q)[6];
+            cnt.node_visits += 4;
+            const float bound = best * 1.00001f + 1e-30f;
+            // entry distance of each child with its slot in the two low bits (+inf: missed; an empty
+            // slot, lo = hi = +inf, never yields a finite entry)
+            auto key = [&](float x0, float y0, float z0, float x1, float y1, float z1, uint32_t slot) {
+                const float tx0 = (x0 - ro.x) * ri.x, tx1 = (x1 - ro.x) * ri.x;
+                const float ty0 = (y0 - ro.y) * ri.y, ty1 = (y1 - ro.y) * ri.y;
+                const float tz0 = (z0 - ro.z) * ri.z, tz1 = (z1 - ro.z) * ri.z;
+                const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+                const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+                const uint32_t kb = tn <= fminf(tf, bound) ? __float_as_uint(tn) : kKeyInf;
+                return (kb & ~3u) | slot;
+            };
+            uint32_t k0 = key(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, 0u);
+            uint32_t k1 = key(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, 1u);
+            uint32_t k2 = key(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, 2u);
+            uint32_t k3 = key(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, 3u);
+            // sorting network (0,1) (2,3) (0,2) (1,3) (1,2): ascending entry distance, then slot
+            auto cx = [](uint32_t& a, uint32_t& b) {
+                const uint32_t lo = a < b ? a : b;
+                b = a < b ? b : a;
+                a = lo;
+            };
+            cx(k0, k1);
+            cx(k2, k3);
+            cx(k0, k2);
+            cx(k1, k3);
+            cx(k1, k2);
+            const uint32_t nh = (uint32_t)(k0 < kKeyInf) + (uint32_t)(k1 < kKeyInf) + (uint32_t)(k2 < kKeyInf) +
+                                (uint32_t)(k3 < kKeyInf);
+            const uint32_t s0 = k0 & 3u;
+            const uint32_t r01 = (s0 & 1u) ? rf.y : rf.x, r23 = (s0 & 1u) ? rf.w : rf.z;
+            const uint32_t near = (s0 & 2u) ? r23 : r01;
+            const uint32_t entry = cur | (((k1 & 3u) | ((k2 & 3u) << 2) | ((k3 & 3u) << 4)) << kWideNodeBits) |
+                                   ((nh - 1u) << 29);
+            const bool more = nh >= 2u;
+            const bool ovf = more && sp + 1 > cap;
+            if (__builtin_expect(__ballot(ovf) != 0, 0))
+                if (ovf) cnt.overflow();
+            const bool push = more && !ovf;
+            wstack[(push ? sp : cap) * 64 + lane] = entry;
+            sp = ovf ? 0 : sp + (push ? 1 : 0);
+            bot = ovf ? 0 : bot;
+            cur = near;
+            has = nh > 0u && !ovf;
+        }
+        uint32_t lk = 0, ln = 0;
+        {
+            const bool leaf = has && (cur & kLeafRef);
+            const uint32_t nt = ((cur >> 27) & 15u) + 1u;
+            lk = cur & 0x07FFFFFFu;
+            ln = leaf ? (nt < 3u ? nt : 3u) : 0u;
+            cur = leaf && nt > 3u ? (kLeafRef | ((nt - 4u) << 27) | (lk + 3u)) : cur;
+            has = has && !(leaf && nt <= 3u);
+            cnt.tri_tests += ln;
+        }
+        const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
+        if (b1) {
+            const uint32_t at = qtail + (uint32_t)(lane_rank(b1) + lane_rank(b2) + lane_rank(b3));
+            const uint32_t tag = (uint32_t)owner;
+            for (uint32_t j = 0; j < ln; ++j) W.slot[(at + j) & (kQ - 1)] = ((lk + j) << 6) | tag;
+            qtail += (uint32_t)(__popcll(b1) + __popcll(b2) + __popcll(b3));
+            __builtin_amdgcn_wave_barrier();
+            if (qtail - qdone >= 64u) {
+                do {
+                    batch(64u);
+                } while (qtail - qdone >= 64u);
+                if (has || sp > bot) best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
+            }
+        }
+    }
+    if (qtail > qdone) batch(qtail - qdone);
+    __builtin_amdgcn_wave_barrier();
+    if (want) {
+        const unsigned long long key = W.key[lane];
+        if (key != ~0ull) {
+            const uint32_t k = tri_orig[2 * (base + (uint32_t)(key & 0xFFFFFFFFu)) + 1];
+            h.merge(__uint_as_float((uint32_t)(key >> 32)), order, false, obj, (int32_t)k);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+#endif
+
 // One object record (64 B) as a single wave-uniform scalar load; the same
 // helper serves per-lane loads of sphere-group members.
 __device__ __forceinline__ ObjRec load_obj(const ObjRec* __restrict__ objs, int i) {
@@ -955,8 +1160,13 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             } else if constexpr ((kParts & 1) != 0) {
                 const bool want = live && box_hit(f, o, inv);
                 cnt.box_tests += (uint32_t)__popcll(__ballot(live));
+#if RT_MESH_WIDE
+                mesh_bvh_wide(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0, want, o, d, inv, h, i,
+                              ob.order, stack - lane, W, lane, cnt, S.stack_cap);
+#else
                 mesh_bvh_pairs(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0, want, o, d, inv, h, i,
                                ob.order, stack - lane, W, lane, cnt, S.stack_cap);
+#endif
             }
         } else if ((kMed || (kBvh && kSph)) && ob.type == kObjMedium) {
             // (the general linear-scan kernel never sees a medium: launch_render sends scenes with
@@ -2505,7 +2715,7 @@ uint32_t kernel_build_flags() {
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
-    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1
+    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)

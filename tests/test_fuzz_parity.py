@@ -301,9 +301,10 @@ def test_gpu_division_edge_parity(lanes):
 def deep_leaf_spec():
     """One triangle repeated 260 times: the SAH builder keeps them in one leaf, which build_mesh_pairs
     splits into halves under the same box (260 -> 130 -> 65 -> 33 -> 17 -> 9): five levels of pair
-    records, every one with both children hit by any ray that hits the box. A lane descending it pushes
-    at every level, so its stack reaches exactly the scene's bound (rt_scene_bvh_depth = 5) while its
-    non-pushing steps write the spare slot past it (rt_kernel.hip kStackSpare)."""
+    records (four levels of 4-wide nodes), every child of every node hit by any ray that hits the box.
+    A lane descending it pushes at every level, so its stack reaches exactly the scene's bound
+    (rt_scene_bvh_depth) while its non-pushing steps write the spare slot past it (rt_kernel.hip
+    kStackSpare)."""
     one = np.array([[-0.6, -0.5, -0.2, 0.7, -0.4, -0.3, -0.1, 0.6, -0.25]], np.float32)
     mats = [("lambertian", 0, (0.8, 0.3, 0.3)), ("emission", 1, (1.0, 0.9, 0.8), 4.0)]
     objs = [("mesh", 0, np.repeat(one, 260, axis=0).reshape(-1), 0),
@@ -313,12 +314,12 @@ def deep_leaf_spec():
     return {"camera": cam, "materials": mats, "objects": objs}
 
 
-def test_deep_leaf_spec_has_five_pair_levels():
+def test_deep_leaf_spec_depth():
     import raytracingthenextweekcuda_amd as rtmi
 
     r = rtmi.Renderer(-1)
     build_product(r, deep_leaf_spec())
-    assert r.bvh_depth() == 5
+    assert r.bvh_depth() in (4, 5)  # 4-wide nodes (RT_MESH_WIDE, the default) or child pairs
     r.close()
 
 
@@ -331,10 +332,11 @@ def test_gpu_stack_reaches_its_bound(lanes):
     w, h, spp, depth = 40, 30, 8, 4
     r = rtmi.Renderer(0)
     build_product(r, spec)
+    bound = r.bvh_depth()
     got = r.render(w, h, spp, depth, lanes_per_pixel=lanes)
     st = r.stats()
     r.close()
-    assert st["stack_depth"] == 5 and st["overflow"] == 0
+    assert bound in (4, 5) and st["stack_depth"] == bound and st["overflow"] == 0
     want, ost = build_oracle(spec).render(w, h, spp, depth, lanes_per_pixel=lanes)
     assert np.array_equal(got, want)
     assert st["segments"] == ost["segments"]
