@@ -1037,6 +1037,9 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
 #ifndef RT_PLANE_AXIAL
 #define RT_PLANE_AXIAL 1  // 0: every plane through the general dot products (A/B)
 #endif
+#ifndef RT_PLANE_MIN
+#define RT_PLANE_MIN 1  // axial planes: the six conditions as one float minimum (0: compares and ANDs; A/B)
+#endif
 template <int K>
 __device__ __forceinline__ float axis(v3 v) {
     return K == 0 ? v.x : K == 1 ? v.y : v.z;
@@ -1057,8 +1060,27 @@ __device__ __forceinline__ float plane_axial(const ObjRec& ob, v3 o, v3 d) {
     // twoSide ? |den| > tMin : den > tMin, with u1 = the bits of 1.0f (two-sided) or 0 (rt_scene.cpp):
     // max(|den| * 1, den) = |den|; max(|den| * 0, den) > tMin iff den > tMin (+0 or NaN against den,
     // and fmaxf returns den for a NaN first operand); a NaN den fails both. No scalar select.
-    const bool proceed = fmaxf(fabsf(den) * __uint_as_float(ob.u1), den) > kTMin;
     const float num = (f[K] - axis<K>(o)) * nk;
+#if RT_PLANE_MIN
+    // t matters only where proceed holds (then |den| > tMin): a wave with any |num| or |den| >= 2^100
+    // takes the IEEE division (closest_hit's general plane argues the domain)
+    float t = div_y(num, den, rcp_nr(den));
+    if (__builtin_expect(__ballot(!(fmaxf(fabsf(num), fabsf(den)) < 0x1p100f)) != 0, 0)) t = fdiv(num, den);
+    const float pa = axis<A>(o) + axis<A>(d) * t;
+    const float pb = axis<B>(o) + axis<B>(d) * t;
+    // The six conditions as one compare: each is a difference that is > 0 exactly when it holds
+    // (x - y > 0 iff x > y for floats with gradual underflow; t >= tMin iff t > the float below tMin),
+    // and the candidate stands iff their minimum is > 0. That needs no lane-mask ANDs (scalar
+    // instructions, the co-bound of this kernel: DESIGN §5). NaNs: den is finite (directions are), so
+    // the proceed term is a number; where it is <= 0 the minimum is too, whatever fminf drops, and
+    // where it is > 0, |den| > tMin and the quotient, pa and pb are finite: the same result as the
+    // compares for every ray.
+    const float p1 = fmaxf(fabsf(den) * __uint_as_float(ob.u1), den) - kTMin;
+    const float m = fminf(fminf(fminf(pa - f[6], f[7] - pa), fminf(pb - f[8], f[9] - pb)),
+                          fminf(p1, t - 0x1.0624dcp-10f /* the float below kTMin */));
+    return m > 0.0f ? t : __builtin_nanf("");
+#else
+    const bool proceed = fmaxf(fabsf(den) * __uint_as_float(ob.u1), den) > kTMin;
 #if RT_DIV_NR
     float t = div_y(num, den, rcp_nr(den));  // domain and fallback: closest_hit's general plane
     if (__builtin_expect(__ballot(proceed && !(fmaxf(fabsf(num), fabsf(den)) < 0x1p100f)) != 0, 0))
@@ -1070,6 +1092,7 @@ __device__ __forceinline__ float plane_axial(const ObjRec& ob, v3 o, v3 d) {
     const float pb = axis<B>(o) + axis<B>(d) * t;
     const bool in = (pa > f[6]) & (pa < f[7]) & (pb > f[8]) & (pb < f[9]);
     return (proceed & (t >= kTMin) & in) ? t : __builtin_nanf("");
+#endif
 }
 
 template <bool kBvh, bool kMed = false, bool kSph = true, int kParts = 3>
@@ -2715,7 +2738,7 @@ uint32_t kernel_build_flags() {
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
-    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 1
+    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)

@@ -102,7 +102,7 @@ struct alignas(16) WideNode {
 };
 static_assert(sizeof(WideNode) == 128, "WideNode must be 128 B");
 #ifndef RT_MESH_WIDE
-#define RT_MESH_WIDE 1  // rayColor mesh BVHs as 4-wide nodes (0: child-pair records; A/B)
+#define RT_MESH_WIDE 0  // 1: rayColor mesh BVHs as 4-wide nodes (A/B: slower than child pairs)
 #endif
 // A lane's traversal stack entry over wide nodes: the node (bits 0-22) and the children still to
 // visit, nearest first (2-bit child slots at bits 23-24, 25-26, 27-28; their count at bits 29-30).

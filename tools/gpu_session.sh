@@ -10,6 +10,7 @@
 #   TRAFFIC   FETCH_SIZE and WRITE_SIZE passes (separate runs), for profiles/pmc_traffic.json
 #   PROF      rocprofv3 --kernel-trace --stats of these workloads (--no-overlap)
 #   MULTI=1   examples/multigpu (RCCL through the C ABI, N = 1 on this box)
+#   STAMPS    tools/stamps_breakdown.py of these workloads with librtmi_stamps.so (tools/build_ab.sh stamps -DRT_STAMPS)
 #   STREAMS=1 tools/queue_probe.py (how many streams run concurrently: 4 and 8 hardware queues), then
 #             bench.py --rehearse-shard N (rank 0's rows of an N-rank CB1 frame, the N > 1 stream layout and
 #             ABI exchange on a one-rank communicator) for N in SHARDS (default "8") and CTXS contexts
@@ -73,6 +74,10 @@ for sc in ${PROF:-}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$sc" -o run --output-format csv -- python3 bench.py --scene $sc --steps ${PROF_STEPS:-10} --warmup ${PROF_WARMUP:-2} --no-cpu-baseline --no-overlap $(lay $sc) > "$O/prof_$sc.log" 2>&1
   stop_if_fatal $? prof_$sc
 done
+if [ -n "${STAMPS:-}" ] && [ -f raytracingthenextweekcuda_amd/librtmi_stamps.so ]; then  # section timers (RT_STAMPS build)
+  RTMI_LIB=raytracingthenextweekcuda_amd/librtmi_stamps.so timeout -k 10 300 python tools/stamps_breakdown.py $STAMPS > "$O/stamps.log" 2>&1
+  stop_if_fatal $? stamps
+fi
 if [ "${STREAMS:-0}" = "1" ]; then
   timeout -k 10 120 python tools/queue_probe.py > "$O/queue_probe.json" 2> "$O/queue_probe.err"
   stop_if_fatal $? queue_probe
