@@ -755,10 +755,13 @@ __device__ __forceinline__ ObjRec load_obj(const ObjRec* __restrict__ objs, int 
 // consecutive meshes are consecutive in `tris` (their bases rise with scan order), so
 // the per-lane minimum of (t, global triangle index) over the run is the candidate the
 // sequential hit() keeps: smallest t, then the earliest mesh, then its lowest triangle.
+// `skip`: the object index of a convex mesh the lane's ray starts on and leaves (render_kernel, RT_MESH_SELF;
+// -1: none): its triangles cannot accept the ray (rt_scene.cpp convex_shell), so the lane takes no ray slot
+// for it. The event counters still count the reference's AABB passes and triangle tests.
 template <bool kOrdered>
 __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
                                          int i0, uint32_t g, uint32_t m, uint32_t magic, bool live, v3 o, v3 d,
-                                         v3 inv, Hit& h, Counters& cnt, WaveLds& W, int lane) {
+                                         v3 inv, Hit& h, Counters& cnt, WaveLds& W, int lane, int skip) {
     uint32_t nslot = 0;  // wave-uniform
     bool any = false;
     const uint32_t lives = (uint32_t)__popcll(__ballot(live));
@@ -768,9 +771,11 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
         const uint64_t mask = __ballot(want);
         cnt.box_tests += lives;
         cnt.tri_wave += (uint32_t)__popcll(mask) * m;
-        if (want) W.slot[nslot + (uint32_t)lane_rank(mask)] = (uint32_t)lane | (ob.u0 << 6);
-        nslot += (uint32_t)__popcll(mask);
-        any = any || want;
+        const bool take = want && skip != i0 + (int)j;
+        const uint64_t tmask = __ballot(take);
+        if (take) W.slot[nslot + (uint32_t)lane_rank(tmask)] = (uint32_t)lane | (ob.u0 << 6);
+        nslot += (uint32_t)__popcll(tmask);
+        any = any || take;
     }
     if (nslot == 0) return;
     if (any) key_reset(W.key[lane]);
@@ -1098,7 +1103,7 @@ __device__ __forceinline__ float plane_axial(const ObjRec& ob, v3 o, v3 d) {
 template <bool kBvh, bool kMed = false, bool kSph = true, int kParts = 3>
 __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v3 inv, bool live,
                                            Rng& rng, WaveLds& W, uint32_t* stack, int lane,
-                                           Counters& cnt
+                                           Counters& cnt, int skip
 #ifdef RT_STAMPS
                                            , uint64_t* tm
 #endif
@@ -1177,7 +1182,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 RT_STAMP(t_m0);
                 if (g != 0u)
                     mesh_run<kOrd>(S.objs, S.tris, i, g, ob.u1, __float_as_uint(ob.f[6]), live, o, d, inv, h, cnt, W,
-                                   lane);
+                                   lane, skip);
                 RT_STAMP(t_m1);
                 RT_ACC(3, t_m0, t_m1);
             } else if constexpr ((kParts & 1) != 0) {
@@ -1317,6 +1322,9 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #endif
 #ifndef RT_PT_WAVES
 #define RT_PT_WAVES 6
+#endif
+#ifndef RT_PT_BATCH_SEL
+#define RT_PT_BATCH_SEL 1  // pathTrace's batched Kuchkuda test as lane selects (0: nested branches; A/B)
 #endif
 #ifdef RT_WAVES_PER_EU
 #undef RT_BVH_WAVES
@@ -1805,7 +1813,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
 #endif
 
         const v3 inv = rcp_exact(ray.d);
-        const Hit h = closest_hit<kBvh, kMed, kSph, kParts>(S, ray, inv, live, rng, W, stack, lane, cnt
+        // RT_MESH_SELF: the convex mesh this segment starts on and leaves (shading below), kept beside the
+        // path depth in the camera slot's spare word: bits 20-31 = its object index + 1
+        int skip = -1;
+        if constexpr (kCamPf && RT_MESH_SELF && RT_DEPTH_LDS)
+            skip = (int)(reinterpret_cast<const uint32_t*>(&cslots[wave].c[lane])[3] >> 20) - 1;
+        const Hit h = closest_hit<kBvh, kMed, kSph, kParts>(S, ray, inv, live, rng, W, stack, lane, cnt, skip
 #ifdef RT_STAMPS
                                         , tm
 #endif
@@ -1908,6 +1921,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                 scattered = false;
                 nd = ray.d;
             }
+            // RT_MESH_SELF: a ray that leaves a convex brute-force mesh (rt_scene.cpp convex_shell) outward from a
+            // point well inside a face cannot be accepted by any of its triangles: the next segment
+            // skips that mesh. Margins: the hit at least 1e-3 (barycentric) inside its triangle's three edges,
+            // the new direction at least 1e-3 (cosine) off the face's plane. Only a skip is decided here; the
+            // triangles of every other object are tested as before.
+            uint32_t self_bits = 0u;
+#if RT_MESH_SELF && RT_DEPTH_LDS
+            if constexpr (kCamPf) {
+                const bool cand = scattered && h.tri >= 0 && h.obj < 4094 && ob.type == kObjMesh &&
+                                  __float_as_uint(f[9]) != 0u;
+                if (__ballot(cand) != 0) {
+                    const TriRec& tr = S.tris[cand ? h.tri : 0];
+                    const v3 e1{tr.e1x, tr.e1y, tr.e1z}, e2{tr.e2x, tr.e2y, tr.e2z};
+                    const v3 sv = sub(ray.o, v3{tr.v0x, tr.v0y, tr.v0z});
+                    const v3 s1 = cross(ray.d, e2), s2 = cross(sv, e1);
+                    const float ic = __builtin_amdgcn_rcpf(dot(s1, e1));  // (a margin test: 1 ulp is plenty)
+                    const float b1 = ic * dot(s1, sv), b2 = ic * dot(s2, ray.d);
+                    const bool ok = cand & (b1 >= 1e-3f) & (b2 >= 1e-3f) & (1.0f - b1 - b2 >= 1e-3f) &
+                                    (dot(nd, outward) > 1e-3f);
+                    self_bits = ok ? (uint32_t)h.obj + 1u : 0u;
+                }
+            }
+#endif
             if (scattered) {
                 thr = mul(thr, att);
                 ray = Ray{p, nd, ray.time};
@@ -1916,8 +1952,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                     // the linear-scan kernels keep the path depth in the camera slot's spare word (LDS)
                     // instead of a VGPR of the persistent loop (at 7 waves/SIMD the CB1 kernel spilled it)
                     uint32_t* dw = reinterpret_cast<uint32_t*>(&cslots[wave].c[lane]) + 3;
-                    const uint32_t dn = *dw + 1u;
-                    *dw = dn;
+                    const uint32_t dn = (*dw & 0xFFFFFu) + 1u;  // (max_depth < 2^20: rt_capi.cpp validate)
+                    *dw = dn | (self_bits << 20);
                     done = (int)dn >= L.max_depth;
                 } else
 #endif
@@ -2200,7 +2236,33 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
         const v3 po{lane_read(ray.o.x, own), lane_read(ray.o.y, own), lane_read(ray.o.z, own)};
         const v3 pd{lane_read(ray.d.x, own), lane_read(ray.d.y, own), lane_read(ray.d.z, own)};
         const int pav = lane_read(avoid_in, own);
+#if RT_PT_BATCH_SEL
+        {
+            // the Kuchkuda test for list position i (CUDAPathTracer.cu:258-345) as lane selects: lanes past
+            // `count` test list position 0 (valid) and every test is evaluated, so no divergent branches
+            // (their exec-mask saves and restores are scalar instructions, this kernel's co-bound). The
+            // acceptance keeps the reference's comparisons, NaN cases included: the edge tests are
+            // `!(e < 0)`, which holds for NaN; the key of a rejected pair is ~0, a no-op for atomicMin.
+            const int idx = tri_list[act ? i : 0u];
+            const float4* T = reinterpret_cast<const float4*>(ktris + idx);
+            const float4 q0 = T[0], q1 = T[1], q2 = T[2], q3 = T[3];
+            const v3 nn{q0.x, q0.y, q0.z};
+            const float k = dot(nn, pd);
+            const float sd = fdiv(q0.w - dot(nn, po), k);
+            const v3 hit = add(scale(pd, sd), po);
+            const bool in = !(dot(v3{q1.x, q1.y, q1.z}, hit) - q1.w < 0.0f) &
+                            !(dot(v3{q2.x, q2.y, q2.z}, hit) - q2.w < 0.0f) &
+                            !(dot(v3{q3.x, q3.y, q3.z}, hit) - q3.w < 0.0f);
+            const bool ok = act & (pav != idx) & (k != 0.0f) & (sd > 0.0f) & (sd > 1e-3f) & in;  // NUDGE_FACTOR
+            const v3 df = sub(po, hit);
+            const float hz = df.x * df.x + df.y * df.y + df.z * df.z;  // distancesq
+            const unsigned long long key = ((unsigned long long)__float_as_uint(hz) << 32) | i;
+            atomicMin(&keys[own], ok ? key : ~0ull);
+        }
+        if (false) {
+#else
         if (act) {
+#endif
             // the Kuchkuda test for list position i (CUDAPathTracer.cu:258-345)
             const int idx = tri_list[i];
             if (pav != idx) {
@@ -2738,7 +2800,7 @@ uint32_t kernel_build_flags() {
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
-    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1
+    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1 || RT_PT_BATCH_SEL != 1 || RT_MESH_SELF != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)

@@ -31,6 +31,73 @@ inline v3 rotate_y(v3 v, float r) {
 }
 }  // namespace
 
+// A brute-force mesh the kernels may skip for rays that start on its own surface (rt_kernel.hip
+// mesh_run, RT_MESH_SELF): a convex polyhedral shell whose face planes meet at angles of at least
+// 30 degrees and whose parallel faces are apart. A ray that leaves such a mesh outward from a point
+// well inside a face (closest_hit's caller checks both, with margins) stays outside every face
+// plane it could cross from the front, so TriangleMesh::hit (TriangleMesh.cu:34-117, which culls
+// back faces) accepts none of its triangles at t >= tMin: the geometric argument is in DESIGN §4.
+// Computed in double from the triangles the kernel tests (their precomputed normals and v0).
+bool convex_shell(const TriRec* t, size_t nt) {
+    if (nt < 4) return false;
+    struct P { double n[3], d; };
+    std::vector<P> pl(nt);
+    std::vector<double> vs;  // every vertex
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    for (size_t i = 0; i < nt; ++i) {
+        const TriRec& r = t[i];
+        const double v0[3] = {r.v0x, r.v0y, r.v0z}, e1[3] = {r.e1x, r.e1y, r.e1z}, e2[3] = {r.e2x, r.e2y, r.e2z};
+        const double n[3] = {r.nx, r.ny, r.nz};
+        if (!std::isfinite(n[0]) || !std::isfinite(n[1]) || !std::isfinite(n[2])) return false;
+        const double len = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        if (!(std::fabs(len - 1.0) < 1e-5)) return false;
+        for (int a = 0; a < 3; ++a) pl[i].n[a] = n[a] / len;
+        pl[i].d = pl[i].n[0] * v0[0] + pl[i].n[1] * v0[1] + pl[i].n[2] * v0[2];
+        for (int k = 0; k < 3; ++k)
+            for (int a = 0; a < 3; ++a) {
+                const double x = v0[a] + (k == 1 ? e1[a] : k == 2 ? e2[a] : 0.0);
+                vs.push_back(x);
+                lo[a] = std::min(lo[a], x);
+                hi[a] = std::max(hi[a], x);
+            }
+    }
+    const double scale = std::sqrt((hi[0] - lo[0]) * (hi[0] - lo[0]) + (hi[1] - lo[1]) * (hi[1] - lo[1]) +
+                                   (hi[2] - lo[2]) * (hi[2] - lo[2]));
+    if (!(scale > 0.0) || !std::isfinite(scale)) return false;
+    // the kernel's margins (1e-3 of a triangle's height from its edges) must dwarf the rounding of a hit
+    // point: every triangle at least 1e-2 high relative to the mesh's largest coordinate (and to 1)
+    double maxabs = 1.0, hmin = 1e300;
+    for (double x : vs) maxabs = std::max(maxabs, std::fabs(x));
+    for (size_t i = 0; i < nt; ++i) {
+        const TriRec& r = t[i];
+        const double e1[3] = {r.e1x, r.e1y, r.e1z}, e2[3] = {r.e2x, r.e2y, r.e2z};
+        const double e3[3] = {e2[0] - e1[0], e2[1] - e1[1], e2[2] - e1[2]};
+        const double cx = e1[1] * e2[2] - e1[2] * e2[1], cy = e1[2] * e2[0] - e1[0] * e2[2],
+                     cz = e1[0] * e2[1] - e1[1] * e2[0];
+        const double area2 = std::sqrt(cx * cx + cy * cy + cz * cz);
+        auto len = [](const double* e) { return std::sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]); };
+        const double longest = std::max(len(e1), std::max(len(e2), len(e3)));
+        hmin = std::min(hmin, area2 / longest);
+    }
+    if (!(hmin >= 1e-2 * maxabs)) return false;
+    for (size_t i = 0; i < nt; ++i)  // every vertex on or behind every triangle's plane (outward normals)
+        for (size_t k = 0; k < vs.size(); k += 3)
+            if (pl[i].n[0] * vs[k] + pl[i].n[1] * vs[k + 1] + pl[i].n[2] * vs[k + 2] - pl[i].d > 1e-6 * scale)
+                return false;
+    for (size_t i = 0; i < nt; ++i)
+        for (size_t j = i + 1; j < nt; ++j) {
+            const double c = pl[i].n[0] * pl[j].n[0] + pl[i].n[1] * pl[j].n[1] + pl[i].n[2] * pl[j].n[2];
+            if (c > 1.0 - 1e-9) {  // the same face: coplanar
+                if (std::fabs(pl[i].d - pl[j].d) > 1e-6 * scale) return false;
+            } else if (c < -1.0 + 1e-9) {  // opposite faces: apart
+                if (std::fabs(pl[i].d + pl[j].d) < 1e-3 * scale) return false;
+            } else if (c * c > 0.75) {  // planes within 30 degrees of each other
+                return false;
+            }
+        }
+    return true;
+}
+
 TriRec make_triangle(v3 p0, v3 p1, v3 p2) {
     v3 e1 = sub(p1, p0);
     v3 e2 = sub(p2, p0);
@@ -396,6 +463,9 @@ std::string HostScene::flatten() {
                 tri_orig[pair0 + 2 * t] = (uint32_t)order[t];
                 tri_orig[pair0 + 2 * (size_t)order[t] + 1] = r.u0 + (uint32_t)t;
             }
+            // f[9] (brute-force meshes): 1 = a convex shell the kernels skip for rays leaving its surface
+            const uint32_t convex = nt <= kBvhMinTris && RT_MESH_SELF && convex_shell(&tris[r.u0], nt) ? 1u : 0u;
+            memcpy(&r.f[9], &convex, 4);
         }
         objs.push_back(r);
     }

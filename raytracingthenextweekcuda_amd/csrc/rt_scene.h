@@ -50,7 +50,8 @@ struct alignas(16) ObjRec {
     //        orientation's axes a, b (XY: x, y; YZ: y, z; XZ: x, z)
     // mesh: boundsMin xyz, boundsMax xyz (computeMeshAABB, main.cu:261-281), f[6] = the bits of
     //       ceil(2^32 / triangle count) (the brute-force compaction's division), f[7] = mesh-run
-    //       length (brute force), f[8] = root child-pair reference (BVH meshes)
+    //       length (brute force), f[8] = root child-pair reference (BVH meshes), f[9] = 1 (as u32 bits)
+    //       for a brute-force mesh that is a convex shell (rt_scene.cpp convex_shell, RT_MESH_SELF)
     float f[10];
 };
 constexpr uint32_t kNoBvh = 0xFFFFFFFFu;
@@ -101,6 +102,9 @@ struct alignas(16) WideNode {
     uint32_t n, pad[3];
 };
 static_assert(sizeof(WideNode) == 128, "WideNode must be 128 B");
+#ifndef RT_MESH_SELF
+#define RT_MESH_SELF 1  // skip convex brute-force meshes for rays leaving their surface (0: A/B)
+#endif
 #ifndef RT_MESH_WIDE
 #define RT_MESH_WIDE 0  // 1: rayColor mesh BVHs as 4-wide nodes (A/B: slower than child pairs)
 #endif
