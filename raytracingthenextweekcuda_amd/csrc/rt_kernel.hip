@@ -285,6 +285,17 @@ __device__ __forceinline__ uint64_t stamp() {
 #define RT_STAMP(var)
 #define RT_ACC(slot, a, b)
 #endif
+// RT_STAMPS: the BVH traversals count their loop trips (slot 3) and the lanes with work in them (slot 6):
+// their lane utilisation (tools/stamps_breakdown.py)
+#ifdef RT_STAMPS
+#define RT_TM_PARAM , uint64_t* tm
+#define RT_TM_ARG , tm
+#define RT_TRIP_COUNT(busy) (tm[3] += 1, tm[6] += (uint64_t)__popcll(__ballot(busy)))
+#else
+#define RT_TM_PARAM
+#define RT_TM_ARG
+#define RT_TRIP_COUNT(busy) ((void)0)
+#endif
 
 // A constant materialised at its use (the empty asm makes each call a fresh VGPR):
 // the register allocator otherwise keeps shared constant tuples - a zero vector,
@@ -381,7 +392,7 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
                                                const BvhNode* __restrict__ nodes, uint32_t root, uint32_t base,
                                                bool want, v3 o, v3 d, v3 inv, Hit& h, int32_t obj,
                                                uint32_t order, uint32_t* wstack, WaveLds& W, int lane,
-                                               Counters& cnt, int cap) {
+                                               Counters& cnt, int cap RT_TM_PARAM) {
     const uint64_t wm = __ballot(want);
     if (wm == 0) return;
     key_reset(W.key[lane]);
@@ -413,6 +424,7 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
     };
     for (;;) {
         if (__ballot(has || sp > bot) == 0) break;
+        RT_TRIP_COUNT(has || sp > bot);
         // steal: pair the r-th idle lane with the r-th lane that has a spare reference
         const bool idle = !has && sp == bot;
         const bool spare = sp - bot >= (has ? 1 : 2);
@@ -857,7 +869,7 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
                                                      const BvhNode* __restrict__ nodes, uint32_t root,
                                                      bool live, const Ray& ray, v3 inv, float inva, Hit& h,
                                                      uint32_t* wstack, WaveLds& W, int lane, Counters& cnt,
-                                                     int cap) {
+                                                     int cap RT_TM_PARAM) {
     if (__ballot(live) == 0) return;
     key_reset(W.key[lane]);
     const v3 o = ray.o;
@@ -894,6 +906,7 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
     };
     for (;;) {
         if (__ballot(has || sp > 0) == 0) break;
+        RT_TRIP_COUNT(has || sp > 0);
         if (!has && sp > 0) {
             cur = wstack[(--sp) * 64 + lane];
             has = true;
@@ -1193,7 +1206,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                               ob.order, stack - lane, W, lane, cnt, S.stack_cap);
 #else
                 mesh_bvh_pairs(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0, want, o, d, inv, h, i,
-                               ob.order, stack - lane, W, lane, cnt, S.stack_cap);
+                               ob.order, stack - lane, W, lane, cnt, S.stack_cap RT_TM_ARG);
 #endif
             }
         } else if ((kMed || (kBvh && kSph)) && ob.type == kObjMedium) {
@@ -1202,7 +1215,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             cand(live ? medium_candidate(ob, o, d, rng) : __builtin_nanf(""), false);
         } else if (kBvh && (kParts & 2) != 0) {  // kObjSphereGroup
             sphere_group_batched(S.objs, S.nodes, __float_as_uint(ob.f[8]), live, ray, inv, inva, h, stack - lane, W, lane,
-                                 cnt, S.stack_cap);
+                                 cnt, S.stack_cap RT_TM_ARG);
         }
         if constexpr (kMed) h.merge_seq<kOrd>(tc, ob.order, tsph, i, -1);  // NaN: no candidate
     };
@@ -1324,7 +1337,7 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #define RT_PT_WAVES 6
 #endif
 #ifndef RT_PT_BATCH_SEL
-#define RT_PT_BATCH_SEL 1  // pathTrace's batched Kuchkuda test as lane selects (0: nested branches; A/B)
+#define RT_PT_BATCH_SEL 0  // 1: pathTrace's batched Kuchkuda test as lane selects (A/B: neutral, spills 20 B)
 #endif
 #ifdef RT_WAVES_PER_EU
 #undef RT_BVH_WAVES
@@ -1809,7 +1822,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
 #ifdef RT_STAMPS
         tm[4] += 1;                                  // loop trips (per wave)
         tm[5] += (uint64_t)__popcll(__ballot(live));  // lanes tracing a segment this trip
-        tm[6] += (uint64_t)__popcll(__ballot(valid)); // lanes that own a pixel
+        if (!kBvh) tm[6] += (uint64_t)__popcll(__ballot(valid)); // lanes that own a pixel (BVH kernels: slot 6 counts traversal lanes)
 #endif
 
         const v3 inv = rcp_exact(ray.d);
@@ -2800,7 +2813,7 @@ uint32_t kernel_build_flags() {
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
-    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1 || RT_PT_BATCH_SEL != 1 || RT_MESH_SELF != 1
+    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1 || RT_PT_BATCH_SEL != 0 || RT_MESH_SELF != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)

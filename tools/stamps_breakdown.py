@@ -27,6 +27,12 @@ for scene in sys.argv[1:] or ["cornellbox1"]:
     trips = max(d[4], 1)
     print(f"{scene}: kernel {st['kernel_ms']:.3f} ms, {st['segments']} segments, {d[4]} wave-trips, "
           f"{d[5] / (64 * trips):.3f} of lane-trips live")
+    bvh = st["variant"] in (4, 5, 6, 7, 11)  # RT_VARIANT_BVH_*: slots 3 and 6 count the traversal loop
     for k, name in ((7, "queue+steal"), (0, "camera"), (1, "closest hit"), (3, "  of which mesh compaction"),
                     (2, "shading")):
+        if bvh and k == 3:
+            continue
         print(f"  {name:28s} {d[k] / tot:6.3f} of stamped cycles, {d[k] / trips:8.1f} cycles per wave-trip")
+    if bvh and d[3]:
+        print(f"  BVH traversal: {d[3] / trips:.1f} loop trips per wave-trip, lane utilisation "
+              f"{d[6] / (64 * d[3]):.3f} (lanes with a subtree or stack entry per trip)")
