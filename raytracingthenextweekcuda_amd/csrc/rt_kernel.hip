@@ -244,6 +244,16 @@ struct WaveLds {
     uint16_t ring[128];          // pair ids that passed the backface cull, awaiting the full test
 };
 
+// The sphere-group traversal's per-lane state that outlives a loop trip (RT_GROUP_RESUME): a lane whose
+// traversal is still running when the wave leaves it keeps its reference, stack depth and (t, ~order)
+// minimum here and resumes in the next trip (the member stack stays in the LDS stacks).
+struct GroupLds {
+    unsigned long long key[64];  // per-ray (t bits << 32 | ~order) minimum over accepted members
+    int32_t src[64];             // the member that set it
+    uint32_t cur[64];            // pair index or leaf reference to continue from
+    uint32_t st[64];             // bit 31: pending; bit 8: `has`; bits 0-7: stack depth
+};
+
 // Event counters of one wave, laid out to keep the VGPR file free for the traversal:
 // amounts that differ per lane stay per lane (node visits, BVH-leaf triangle tests);
 // events counted at wave-uniform points (segments, mesh-box tests, brute-force
@@ -865,18 +875,40 @@ __device__ __forceinline__ float sphere_candidate(const ObjRec& ob, v3 o, v3 d, 
 // (t, ~order) over the accepted members (t <= the ray's closestSoFar) is all the group adds
 // to the ray's Hit: merging that one candidate gives what merging every member would. The
 // lane whose pair set the final minimum records the member (orders are unique) in W.src.
+#ifndef RT_GROUP_RESUME
+#define RT_GROUP_RESUME 1  // sphere groups: leave the traversal to its last few lanes, resume next trip (0: A/B)
+#endif
+#ifndef RT_GROUP_MIN_TRIPS
+#define RT_GROUP_MIN_TRIPS 4   // traversal trips before the wave may leave it
+#endif
+#ifndef RT_GROUP_EXIT_LANES
+#define RT_GROUP_EXIT_LANES 16  // the wave leaves once at most this many lanes still traverse
+#endif
+// kResume (the sphere-group-only kernel, RT_GROUP_RESUME): once at most RT_GROUP_EXIT_LANES lanes of
+// the wave are still traversing (after RT_GROUP_MIN_TRIPS trips), the wave stops: it tests the pairs it
+// has queued, and the unfinished lanes keep their state in `gl` and skip shading. In the next loop trip
+// they resume, while the lanes that finished shade and start their next segments, which then traverse
+// beside them. A wave would otherwise run every trip until its deepest ray is done, with the other
+// lanes idle. A resumed lane re-scans the objects before the group (the same closestSoFar), keeps its
+// (t, ~order) minimum and prunes against it, so its candidate set and result are the single pass's.
+template <bool kResume>
 __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ objs,
                                                      const BvhNode* __restrict__ nodes, uint32_t root,
                                                      bool live, const Ray& ray, v3 inv, float inva, Hit& h,
                                                      uint32_t* wstack, WaveLds& W, int lane, Counters& cnt,
-                                                     int cap RT_TM_PARAM) {
+                                                     int cap, GroupLds* gl RT_TM_PARAM) {
     if (__ballot(live) == 0) return;
-    key_reset(W.key[lane]);
+    unsigned long long* K = kResume ? gl->key : W.key;
+    int32_t* SRC = kResume ? gl->src : W.src;
+    const uint32_t st0 = kResume ? gl->st[lane] : 0u;
+    const bool resume = kResume && live && (st0 >> 31) != 0u;
+    if (live && !resume) key_reset(K[lane]);
     const v3 o = ray.o;
     float best = h.t;  // pruning bound: the ray's closestSoFar, then its best member so far
-    uint32_t cur = root;  // pair index or leaf reference (root: the group's root pair)
-    bool has = live;
-    int sp = 0;
+    if (resume) best = fminf(best, __uint_as_float((uint32_t)(K[lane] >> 32)));
+    uint32_t cur = resume ? gl->cur[lane] : root;  // pair index or leaf reference (root: the group's root pair)
+    bool has = resume ? ((st0 >> 8) & 1u) != 0u : live;
+    int sp = resume ? (int)(st0 & 0xFFu) : 0;
     uint32_t qtail = 0, qdone = 0;
     constexpr uint32_t kQ = (uint32_t)kMaxRun * 64u;
     __builtin_amdgcn_wave_barrier();
@@ -896,16 +928,18 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
             const float t = sphere_candidate(ob, po, pd, ptime, pinva);
             if (t <= pt0) {
                 mine = ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)(~ob.order);
-                atomicMin(&W.key[own], mine);
+                atomicMin(&K[own], mine);
             }
         }
         __builtin_amdgcn_wave_barrier();
-        if (mine != ~0ull && W.key[own] == mine) W.src[own] = (int32_t)k;  // (t, order) is unique
+        if (mine != ~0ull && K[own] == mine) SRC[own] = (int32_t)k;  // (t, order) is unique
         qdone += count;
         __builtin_amdgcn_wave_barrier();
     };
-    for (;;) {
-        if (__ballot(has || sp > 0) == 0) break;
+    for (int trip = 0;; ++trip) {
+        const uint64_t bm = __ballot(has || sp > 0);
+        if (bm == 0) break;
+        if (kResume && trip >= RT_GROUP_MIN_TRIPS && __popcll(bm) <= RT_GROUP_EXIT_LANES) break;
         RT_TRIP_COUNT(has || sp > 0);
         if (!has && sp > 0) {
             cur = wstack[(--sp) * 64 + lane];
@@ -955,16 +989,22 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
                 do {
                     batch(64u);
                 } while (qtail - qdone >= 64u);
-                if (has || sp > 0) best = fminf(best, __uint_as_float((uint32_t)(W.key[lane] >> 32)));
+                if (has || sp > 0) best = fminf(best, __uint_as_float((uint32_t)(K[lane] >> 32)));
             }
         }
     }
     if (qtail > qdone) batch(qtail - qdone);
     __builtin_amdgcn_wave_barrier();
-    if (live) {
-        const unsigned long long key = W.key[lane];
+    bool pend = false;
+    if constexpr (kResume) {
+        pend = live && (has || sp > 0);
+        gl->cur[lane] = cur;
+        gl->st[lane] = pend ? (0x80000000u | ((uint32_t)has << 8) | (uint32_t)sp) : 0u;
+    }
+    if (live && !pend) {
+        const unsigned long long key = K[lane];
         if (key != ~0ull) {
-            const int32_t k = W.src[lane];
+            const int32_t k = SRC[lane];
             h.merge(__uint_as_float((uint32_t)(key >> 32)), ~(uint32_t)(key & 0xFFFFFFFFu), true, k, -1);
         }
     }
@@ -1116,7 +1156,7 @@ __device__ __forceinline__ float plane_axial(const ObjRec& ob, v3 o, v3 d) {
 template <bool kBvh, bool kMed = false, bool kSph = true, int kParts = 3>
 __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v3 inv, bool live,
                                            Rng& rng, WaveLds& W, uint32_t* stack, int lane,
-                                           Counters& cnt, int skip
+                                           Counters& cnt, int skip, GroupLds* gl
 #ifdef RT_STAMPS
                                            , uint64_t* tm
 #endif
@@ -1214,8 +1254,9 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             // media to the kMed variant, so its register allocation need not cover this test)
             cand(live ? medium_candidate(ob, o, d, rng) : __builtin_nanf(""), false);
         } else if (kBvh && (kParts & 2) != 0) {  // kObjSphereGroup
-            sphere_group_batched(S.objs, S.nodes, __float_as_uint(ob.f[8]), live, ray, inv, inva, h, stack - lane, W, lane,
-                                 cnt, S.stack_cap RT_TM_ARG);
+            sphere_group_batched<kBvh && kParts == 2 && RT_GROUP_RESUME>(S.objs, S.nodes, __float_as_uint(ob.f[8]), live,
+                                                                         ray, inv, inva, h, stack - lane, W, lane, cnt,
+                                                                         S.stack_cap, gl RT_TM_ARG);
         }
         if constexpr (kMed) h.merge_seq<kOrd>(tc, ob.order, tsph, i, -1);  // NaN: no candidate
     };
@@ -1654,6 +1695,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
     __shared__ WaveLds lds[kBW];
     // camera slots: the linear-scan kernels only (the traversal kernels' LDS holds their stacks)
     constexpr bool kCamPf = !kBvh;
+    // resumable sphere-group traversal (the sphere-group-only kernel)
+    constexpr bool kResume = kBvh && kParts == 2 && RT_GROUP_RESUME;
+    __shared__ GroupLds glds[kResume ? kBW : 1];
     __shared__ CamSlots cslots[kCamPf ? kBW : 1];
     // traversal stacks (kBvh): kBW x L.stack_depth x 64 lanes, sized per scene at launch
     extern __shared__ uint32_t dyn_stacks[];
@@ -1665,6 +1709,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         W.grp_s[lane] = 0;
         W.grp_m[lane] = 0;
     }
+    if (kResume) glds[wave].st[lane] = 0u;
     uint32_t* stack = kBvh ? dyn_stacks + (size_t)wave * (L.stack_depth + kStackSpare) * 64 + lane : nullptr;
 
     // Lane layout: SP = lanes_per_pixel adjacent lanes share one pixel and split
@@ -1831,20 +1876,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         int skip = -1;
         if constexpr (kCamPf && RT_MESH_SELF && RT_DEPTH_LDS)
             skip = (int)(reinterpret_cast<const uint32_t*>(&cslots[wave].c[lane])[3] >> 20) - 1;
-        const Hit h = closest_hit<kBvh, kMed, kSph, kParts>(S, ray, inv, live, rng, W, stack, lane, cnt, skip
+        const Hit h = closest_hit<kBvh, kMed, kSph, kParts>(S, ray, inv, live, rng, W, stack, lane, cnt, skip,
+                                                            kResume ? &glds[wave] : nullptr
 #ifdef RT_STAMPS
                                         , tm
 #endif
         );
         RT_STAMP(t_c);
         RT_ACC(1, t_b, t_c);
-        cnt.segs += (uint32_t)__popcll(__ballot(live));
+        // a lane whose sphere-group traversal continues next trip (kResume) neither counts nor shades yet
+        const bool pend = kResume && live && (glds[kResume ? wave : 0].st[lane] >> 31) != 0u;
+        cnt.segs += (uint32_t)__popcll(__ballot(live && !pend));
         if (kBvh && __ballot(cnt.grp != 0)) {  // drain the 16-bit sphere-group counts
             W.grp_s[lane] += cnt.grp & 0xFFFFu;
             W.grp_m[lane] += cnt.grp >> 16;
             cnt.grp = 0;
         }
-        if (!live) continue;
+        if (!live || pend) continue;
 
         bool done;
         v3 contrib;
@@ -2813,7 +2861,8 @@ uint32_t kernel_build_flags() {
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
-    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1 || RT_PT_BATCH_SEL != 0 || RT_MESH_SELF != 1
+    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1 || RT_PT_BATCH_SEL != 0 || RT_MESH_SELF != 1 || RT_GROUP_RESUME != 1 || \
+    RT_GROUP_MIN_TRIPS != 4 || RT_GROUP_EXIT_LANES != 16
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)
