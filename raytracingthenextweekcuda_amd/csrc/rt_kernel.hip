@@ -882,7 +882,7 @@ __device__ __forceinline__ float sphere_candidate(const ObjRec& ob, v3 o, v3 d, 
 #define RT_GROUP_MIN_TRIPS 4   // traversal trips before the wave may leave it
 #endif
 #ifndef RT_GROUP_EXIT_LANES
-#define RT_GROUP_EXIT_LANES 16  // the wave leaves once at most this many lanes still traverse
+#define RT_GROUP_EXIT_LANES 8  // the wave leaves once at most this many lanes still traverse
 #endif
 // kResume (the sphere-group-only kernel, RT_GROUP_RESUME): once at most RT_GROUP_EXIT_LANES lanes of
 // the wave are still traversing (after RT_GROUP_MIN_TRIPS trips), the wave stops: it tests the pairs it
@@ -2862,7 +2862,7 @@ uint32_t kernel_build_flags() {
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
     RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1 || RT_PT_BATCH_SEL != 0 || RT_MESH_SELF != 1 || RT_GROUP_RESUME != 1 || \
-    RT_GROUP_MIN_TRIPS != 4 || RT_GROUP_EXIT_LANES != 16
+    RT_GROUP_MIN_TRIPS != 4 || RT_GROUP_EXIT_LANES != 8
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)
