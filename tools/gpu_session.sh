@@ -3,6 +3,7 @@
 #   TESTS=1   pytest -m gpu + smoke()
 #   BENCH=1   the default bench line (config 2, frame overlap, CPU baseline)
 #   SCENES    bench lines of these workloads (no CPU baseline); ALT = A/B libraries run after each
+#   SCENES_CPU  bench lines of these workloads with their CPU baseline
 #   VALU      SQ_INSTS_VALU (+ lane utilisation, wait shares) and SQ_INSTS_SALU passes of these workloads (--no-overlap,
 #             BENCH_ARGS appended: --in-flight-layout for the timed layout), for profiles/valu_issue.json
 #   PROBE=1   tools/valu_probe under SQ counters with 64 and 16 active lanes (lane-utilisation calibration)
@@ -34,6 +35,10 @@ if [ "${BENCH:-0}" = "1" ]; then
   timeout -k 10 300 python bench.py > "$O/bench.log" 2>&1
   stop_if_fatal $? bench
 fi
+for sc in ${SCENES_CPU:-}; do  # bench lines WITH the CPU baseline (the oracle on this box's host cores)
+  timeout -k 10 420 python bench.py --scene $sc ${BENCH_ARGS:-} > "$O/bench_$sc.log" 2>&1
+  stop_if_fatal $? bench_$sc
+done
 for sc in ${SCENES:-}; do
  for rep in $(seq 1 ${REPS:-1}); do  # REPS > 1: the A/B round repeated, logs suffixed _r<rep>
   sfx=""; [ "${REPS:-1}" -gt 1 ] && sfx="_r$rep"
