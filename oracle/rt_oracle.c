@@ -36,7 +36,7 @@
  * Deliberate, documented deviations from the reference:
  *  1. cuRAND XORWOW is replaced by a counter-based stream per (pixel, sample):
  *     Philox4x32-10 (key = (seed, pixel), counter = (sample, 0, 0, 0)) seeds
- *     xoshiro128** 1.1; uniforms use curand's (0,1] mapping x*2^-32 + 2^-33.
+ *     xoshiro128+ 1.0; uniforms use curand's (0,1] mapping x*2^-32 + 2^-33.
  *     cuRAND itself is not in this image: parity with the reference's random
  *     stream is "unpinned" by construction.
  *  2. randomInUnitDisk draws x before y (the reference's order is unspecified).
@@ -118,7 +118,8 @@ static void philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]
 
 /* Stand-in for curandState: one stream per (seed, pixel, sample).
  * Philox4x32-10(key = (seed, pixel), counter = (sample, 0, 0, 0)) seeds a
- * xoshiro128** 1.1 generator (Blackman & Vigna, 2018) for the sample's draws. */
+ * xoshiro128+ 1.0 generator (Blackman & Vigna, 2018) for the sample's draws; the
+ * float mapping keeps its upper 24 bits, the use the authors recommend it for. */
 typedef struct {
     uint32_t s[4];
 } RandState;
@@ -131,9 +132,9 @@ static void rand_init(RandState* st, uint32_t seed, uint32_t pixel, uint32_t sam
     if ((st->s[0] | st->s[1] | st->s[2] | st->s[3]) == 0u) st->s[0] = 0x9E3779B9u;
 }
 
-static uint32_t xoshiro128ss(RandState* st) {
+static uint32_t xoshiro128p(RandState* st) {
     uint32_t* s = st->s;
-    const uint32_t result = rotl32(s[1] * 5u, 7) * 9u;
+    const uint32_t result = s[0] + s[3];
     const uint32_t t = s[1] << 9;
     s[2] ^= s[0];
     s[3] ^= s[1];
@@ -146,7 +147,7 @@ static uint32_t xoshiro128ss(RandState* st) {
 
 /* curand_uniform: (0, 1] (curand's _curand_uniform mapping). */
 static float curand_uniform_(RandState* s) {
-    uint32_t x = xoshiro128ss(s);
+    uint32_t x = xoshiro128p(s);
     const float inv = 2.3283064e-10f;
     return (float)x * inv + (inv / 2.0f);
 }

@@ -66,11 +66,15 @@ RT_HD float maxf_(float a, float b) { return a > b ? a : b; }
 // RNG, replacing cuRAND XORWOW (curand_init main.cu:127, curand_uniform
 // Utils.h:44-51). Counter-based at sample granularity: Philox4x32-10 (Salmon
 // et al., SC'11; Random123 constants) with key = (seed, pixel) and counter =
-// (sample, 0, 0, 0) yields 128 bits that seed a xoshiro128** 1.1 stream
+// (sample, 0, 0, 0) yields 128 bits that seed a xoshiro128+ 1.0 stream
 // (Blackman & Vigna) for that sample's draws. Every (pixel, sample) stream is
-// random-access and independent of launch geometry; a draw costs ~12 full-rate
+// random-access and independent of launch geometry; a draw costs 8 full-rate
 // integer ops, so divergent call sites (rejection loops) stay cheap. Uniforms
-// use curand's (0, 1] mapping x * 2^-32 + 2^-33.
+// use curand's (0, 1] mapping x * 2^-32 + 2^-33, which keeps the output's upper 24
+// bits - the bits the authors recommend xoshiro128+ for (float generation). Round 5
+// replaced xoshiro128** (whose output scrambler, rotl(s1 * 5, 7) * 9, cost three more
+// instructions per draw; RT_XOSHIRO_SS keeps it for A/B timing builds, which then
+// no longer match the restatement).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kPhiloxM0 = 0xD2511F53u;
 constexpr uint32_t kPhiloxM1 = 0xCD9E8D57u;
@@ -133,7 +137,11 @@ struct Rng {
         if ((s0 | s1 | s2 | s3) == 0u) s0 = kPhiloxW0;  // xoshiro's all-zero state is invalid
     }
     RT_HD uint32_t next_u32() {
+#ifdef RT_XOSHIRO_SS
         const uint32_t r = rotl32(s1 * 5u, 7) * 9u;
+#else
+        const uint32_t r = s0 + s3;
+#endif
         const uint32_t t = s1 << 9;
         s2 ^= s0;
         s3 ^= s1;

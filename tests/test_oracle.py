@@ -24,14 +24,14 @@ def test_philox_kat(ctr, key, out):
     assert orc.philox(ctr, key) == out
 
 
-def _xoshiro128ss(state, n):
-    """xoshiro128** 1.1 (Blackman & Vigna), restated in Python."""
+def _xoshiro128p(state, n):
+    """xoshiro128+ 1.0 (Blackman & Vigna), restated in Python."""
     s = list(state)
     M = 0xFFFFFFFF
     rotl = lambda x, k: ((x << k) | (x >> (32 - k))) & M
     out = []
     for _ in range(n):
-        out.append((rotl((s[1] * 5) & M, 7) * 9) & M)
+        out.append((s[0] + s[3]) & M)
         t = (s[1] << 9) & M
         s[2] ^= s[0]
         s[3] ^= s[1]
@@ -44,9 +44,9 @@ def _xoshiro128ss(state, n):
 
 def test_uniform_stream_layout_and_range():
     """Stream of (seed, pixel, sample): Philox4x32-10(counter=(sample,0,0,0),
-    key=(seed,pixel)) seeds xoshiro128**; uniforms use curand's (0,1] map."""
+    key=(seed,pixel)) seeds xoshiro128+; uniforms use curand's (0,1] map."""
     u = orc.uniforms(1984, 12345, 7, 9)
-    words = _xoshiro128ss(orc.philox([7, 0, 0, 0], [1984, 12345]), 9)
+    words = _xoshiro128p(orc.philox([7, 0, 0, 0], [1984, 12345]), 9)
     inv = np.float32(2.0 ** -32)
     expect = np.float32(words) * inv + inv / np.float32(2)
     assert np.array_equal(u, expect.astype(np.float32))
