@@ -126,6 +126,32 @@ __device__ __forceinline__ v3 moving_center(const float* f, float time) {
     return add(c0, scale(sub(c1, c0), (time - f[6]) / (f[7] - f[6])));
 }
 
+#ifndef RT_TRI_MIN
+#define RT_TRI_MIN 1  // 0: the acceptance tests as compares and lane-mask ANDs (A/B)
+#endif
+#ifndef RT_RUN_SEL
+#define RT_RUN_SEL 1  // 0: mesh_run's cull loop with exec-mask branches (A/B)
+#endif
+// TriangleMesh.cu:74-105's acceptance of a Moller-Trumbore solution: t >= FLT_EPSILON, t >= tMin
+// (implied by the first for every t: tMin > FLT_EPSILON), b1, b2 and 1 - b1 - b2 >= FLT_EPSILON.
+// Returns t if all hold, else NaN.
+__device__ __forceinline__ float tri_accept(float t, float b1, float b2) {
+    const float u = 1.0f - b1 - b2;
+#if RT_TRI_MIN
+    // x >= c iff x - (the float below c) > 0, for every float x with gradual underflow (the difference
+    // of two distinct floats is never rounded to zero; +-inf and NaN compare the same way). The four
+    // differences meet in gfx950's NaN-propagating minimum (v_minimum3_f32): it is > 0 iff every
+    // condition holds, with no lane-mask ANDs (scalar instructions, a co-bound of these kernels).
+    const float m = __builtin_elementwise_minimum(
+        __builtin_elementwise_minimum(t - 0x1.0624dcp-10f /* the float below kTMin */, b1 - 0x1.fffffep-24f),
+        __builtin_elementwise_minimum(b2 - 0x1.fffffep-24f /* the float below FLT_EPSILON */, u - 0x1.fffffep-24f));
+    return m > 0.0f ? t : __builtin_nanf("");
+#else
+    const bool ok = (t >= kFltEpsilon) & (t >= kTMin) & (b1 >= kFltEpsilon) & (b2 >= kFltEpsilon) & (u >= kFltEpsilon);
+    return ok ? t : __builtin_nanf("");
+#endif
+}
+
 // One triangle of TriangleMesh::hit (TriangleMesh.cu:40-108) without the
 // closestSoFar comparison: returns t if every other acceptance test passes,
 // else NaN (compares false with anything). The caller applies closestSoFar.
@@ -141,15 +167,11 @@ __device__ __forceinline__ float tri_t(const TriRec& tr, v3 o, v3 d) {
     float t = coef * dot(s2, e2);
     float b1 = coef * dot(s1, s);
     float b2 = coef * dot(s2, d);
-    // every test evaluated and the lane masks and-ed (no short-circuit branches: the same result)
-    const bool ok = (t >= kFltEpsilon) & (t >= kTMin) & (b1 >= kFltEpsilon) & (b2 >= kFltEpsilon) &
-                    ((1.0f - b1 - b2) >= kFltEpsilon);
-    return ok ? t : kNo;
+    return tri_accept(t, b1, b2);
 }
 
 // tri_t for a pair already known to pass the backface cull.
 __device__ __forceinline__ float tri_t_culled(const TriRec& tr, v3 o, v3 d) {
-    const float kNo = __builtin_nanf("");
     v3 e1{tr.e1x, tr.e1y, tr.e1z}, e2{tr.e2x, tr.e2y, tr.e2z};
     v3 s = sub(o, v3{tr.v0x, tr.v0y, tr.v0z});
     v3 s1 = cross(d, e2);
@@ -158,10 +180,7 @@ __device__ __forceinline__ float tri_t_culled(const TriRec& tr, v3 o, v3 d) {
     float t = coef * dot(s2, e2);
     float b1 = coef * dot(s1, s);
     float b2 = coef * dot(s2, d);
-    // every test evaluated and the lane masks and-ed (no short-circuit branches: the same result)
-    const bool ok = (t >= kFltEpsilon) & (t >= kTMin) & (b1 >= kFltEpsilon) & (b2 >= kFltEpsilon) &
-                    ((1.0f - b1 - b2) >= kFltEpsilon);
-    return ok ? t : kNo;
+    return tri_accept(t, b1, b2);
 }
 
 // Closest-hit state with the reference's sequential tie rule (hit(),
@@ -805,11 +824,18 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
     const uint32_t total = nslot * m;
     const float t0 = h.t;
     uint32_t queued = 0, tested = 0;  // wave-uniform ring positions (phase 1: cull, phase 2: full test)
+#if RT_RUN_SEL
+    // the pair's ray slot r = p / m as a multiply-high (magic = 0 for m = 1, where r = p): no branch per batch
+    const uint32_t onem = m == 1u ? 0xFFFFFFFFu : 0u;  // wave-uniform
+    auto slot_of = [&](uint32_t p) { return __umulhi(p, magic) | (p & onem); };
+#else
+    auto slot_of = [&](uint32_t p) { return m > 1u ? __umulhi(p, magic) : p; };
+#endif
     auto full_test = [&](uint32_t count) {
         const uint32_t i = tested + (uint32_t)lane;
         const bool act = (uint32_t)lane < count;
         const uint32_t p = act ? (uint32_t)W.ring[i & 127u] : 0u;
-        const uint32_t r = m > 1u ? __umulhi(p, magic) : p;
+        const uint32_t r = slot_of(p);
         const uint32_t e = W.slot[r];
         const int src = (int)(e & 63u);
         const uint32_t tri = (e >> 6) + (p - r * m);
@@ -826,14 +852,29 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
         const uint32_t p = p0 + (uint32_t)lane;
         const bool act = p < total;
         const uint32_t pc = act ? p : 0u;  // inactive lanes read pair 0 (valid) and keep nothing
-        const uint32_t r = m > 1u ? __umulhi(pc, magic) : pc;
+        const uint32_t r = slot_of(pc);
         const uint32_t e = W.slot[r];
         const int src = (int)(e & 63u);
         const v3 rd{lane_read(d.x, src), lane_read(d.y, src), lane_read(d.z, src)};
         const TriRec& tr = tris[(e >> 6) + (pc - r * m)];
+#if RT_RUN_SEL
+        // every lane loads its normal and writes a ring entry (no exec-mask branches: scalar instructions);
+        // the lanes that keep nothing write position queued + 63, past the keepers' [queued, queued + K) for
+        // K <= 63 and outside the pending [tested, queued), which holds fewer than 64 entries here
+        const float dn = dot(rd, v3{tr.nx, tr.ny, tr.nz});
+        // lanes past `total` compare +inf: one compare whose mask is the ballot (act & !(...) would be a
+        // scalar AND, then a VALU round trip for the ballot); a NaN dn keeps, as !(dn > eps) does
+        float lim = act ? -kInf : kInf;
+        asm volatile("" : "+v"(lim));
+        const bool keep = !(fmaxf(dn, lim) > kFltEpsilon);  // TriangleMesh.cu:72
+        const uint64_t km = __ballot(keep);
+        // (a non-keeper's rank is <= K <= 63, so rank | 63 = 63)
+        W.ring[(queued + ((uint32_t)lane_rank(km) | (keep ? 0u : 63u))) & 127u] = (uint16_t)p;
+#else
         const bool keep = act && !(dot(rd, v3{tr.nx, tr.ny, tr.nz}) > kFltEpsilon);  // TriangleMesh.cu:72
         const uint64_t km = __ballot(keep);
         if (keep) W.ring[(queued + (uint32_t)lane_rank(km)) & 127u] = (uint16_t)p;
+#endif
         queued += (uint32_t)__popcll(km);
         __builtin_amdgcn_wave_barrier();
         if (queued - tested >= 64u) full_test(64u);
@@ -2862,7 +2903,7 @@ uint32_t kernel_build_flags() {
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
     RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1 || RT_PT_BATCH_SEL != 0 || RT_MESH_SELF != 1 || RT_GROUP_RESUME != 1 || \
-    RT_GROUP_MIN_TRIPS != 4 || RT_GROUP_EXIT_LANES != 8
+    RT_GROUP_MIN_TRIPS != 4 || RT_GROUP_EXIT_LANES != 8 || RT_TRI_MIN != 1 || RT_RUN_SEL != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)
