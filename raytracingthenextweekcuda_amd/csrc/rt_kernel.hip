@@ -152,6 +152,34 @@ __device__ __forceinline__ float tri_accept(float t, float b1, float b2) {
 #endif
 }
 
+// RN(1 / b) for |b| in [2^-126, 2^126); Markstein's RN(a / b) from it (callers bound the domain)
+__device__ __forceinline__ float rcp_nr(float b) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
+}
+__device__ __forceinline__ float div_y(float a, float b, float y) {
+    const float q0 = a * y;
+    return __builtin_fmaf(__builtin_fmaf(-b, q0, a), y, q0);
+}
+
+#ifndef RT_TRI_RCP
+#define RT_TRI_RCP 1  // 0: the Moller-Trumbore 1 / det as the IEEE division expansion (A/B)
+#endif
+// TriangleMesh.cu:84's 1.0f / det, correctly rounded, for the brute-force meshes' batched tests (all 64 lanes at once; the
+// batched tests): v_rcp_f32 + one Newton step is RN(1 / b) for every |b| in [2^-126, 2^126) (exhaustive GPU
+// check, tools/div_check.hip); a wave with any other det (zero, subnormal, huge, inf, NaN) takes the IEEE
+// division.
+__device__ __forceinline__ float tri_rcp(float det) {
+#if RT_TRI_RCP
+    float y = rcp_nr(det);
+    const float a = fabsf(det);
+    if (__builtin_expect(__ballot(!(a >= 0x1p-126f && a < 0x1p126f)) != 0, 0)) y = fdiv(1.0f, det);
+    return y;
+#else
+    return fdiv(1.0f, det);
+#endif
+}
+
 // One triangle of TriangleMesh::hit (TriangleMesh.cu:40-108) without the
 // closestSoFar comparison: returns t if every other acceptance test passes,
 // else NaN (compares false with anything). The caller applies closestSoFar.
@@ -163,7 +191,7 @@ __device__ __forceinline__ float tri_t(const TriRec& tr, v3 o, v3 d) {
     v3 s = sub(o, v3{tr.v0x, tr.v0y, tr.v0z});
     v3 s1 = cross(d, e2);
     v3 s2 = cross(s, e1);
-    float coef = fdiv(1.0f, dot(s1, e1));
+    const float coef = fdiv(1.0f, dot(s1, e1));  // (tri_rcp's guard costs the BVH kernels registers)
     float t = coef * dot(s2, e2);
     float b1 = coef * dot(s1, s);
     float b2 = coef * dot(s2, d);
@@ -171,12 +199,13 @@ __device__ __forceinline__ float tri_t(const TriRec& tr, v3 o, v3 d) {
 }
 
 // tri_t for a pair already known to pass the backface cull.
+template <bool kRcp>
 __device__ __forceinline__ float tri_t_culled(const TriRec& tr, v3 o, v3 d) {
     v3 e1{tr.e1x, tr.e1y, tr.e1z}, e2{tr.e2x, tr.e2y, tr.e2z};
     v3 s = sub(o, v3{tr.v0x, tr.v0y, tr.v0z});
     v3 s1 = cross(d, e2);
     v3 s2 = cross(s, e1);
-    float coef = fdiv(1.0f, dot(s1, e1));
+    const float coef = kRcp ? tri_rcp(dot(s1, e1)) : fdiv(1.0f, dot(s1, e1));
     float t = coef * dot(s2, e2);
     float b1 = coef * dot(s1, s);
     float b2 = coef * dot(s2, d);
@@ -352,14 +381,6 @@ __device__ __forceinline__ float fresh_f32(float v) {
 #ifndef RT_DIV_NR
 #define RT_DIV_NR 1  // 0: IEEE divisions in the plane test and Lambertian's normalize (A/B)
 #endif
-__device__ __forceinline__ float rcp_nr(float b) {
-    const float y0 = __builtin_amdgcn_rcpf(b);
-    return __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
-}
-__device__ __forceinline__ float div_y(float a, float b, float y) {
-    const float q0 = a * y;
-    return __builtin_fmaf(__builtin_fmaf(-b, q0, a), y, q0);
-}
 
 // __shfl(v, src, 64) without HIP's lane-id arithmetic: ds_bpermute reads lane (address / 4) mod 64,
 // the same lane __shfl picks. HIP's version derives its own lane id (mbcnt) for the width mask,
@@ -799,7 +820,9 @@ __device__ __forceinline__ ObjRec load_obj(const ObjRec* __restrict__ objs, int 
 // `skip`: the object index of a convex mesh the lane's ray starts on and leaves (render_kernel, RT_MESH_SELF;
 // -1: none): its triangles cannot accept the ray (rt_scene.cpp convex_shell), so the lane takes no ray slot
 // for it. The event counters still count the reference's AABB passes and triangle tests.
-template <bool kOrdered>
+// kLin (the linear-scan kernels): the branch-free cull loop and 1 / det through tri_rcp. In the BVH kernels
+// both cost registers (the sphere-group kernel spilled), so those keep the exec-mask form.
+template <bool kOrdered, bool kLin>
 __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
                                          int i0, uint32_t g, uint32_t m, uint32_t magic, bool live, v3 o, v3 d,
                                          v3 inv, Hit& h, Counters& cnt, WaveLds& W, int lane, int skip) {
@@ -824,13 +847,10 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
     const uint32_t total = nslot * m;
     const float t0 = h.t;
     uint32_t queued = 0, tested = 0;  // wave-uniform ring positions (phase 1: cull, phase 2: full test)
-#if RT_RUN_SEL
-    // the pair's ray slot r = p / m as a multiply-high (magic = 0 for m = 1, where r = p): no branch per batch
+    constexpr bool kSel = kLin && RT_RUN_SEL;
+    // the pair's ray slot r = p / m as a multiply-high (kSel: magic = 0 for m = 1, where r = p; no branch)
     const uint32_t onem = m == 1u ? 0xFFFFFFFFu : 0u;  // wave-uniform
-    auto slot_of = [&](uint32_t p) { return __umulhi(p, magic) | (p & onem); };
-#else
-    auto slot_of = [&](uint32_t p) { return m > 1u ? __umulhi(p, magic) : p; };
-#endif
+    auto slot_of = [&](uint32_t p) { return kSel ? (__umulhi(p, magic) | (p & onem)) : m > 1u ? __umulhi(p, magic) : p; };
     auto full_test = [&](uint32_t count) {
         const uint32_t i = tested + (uint32_t)lane;
         const bool act = (uint32_t)lane < count;
@@ -844,7 +864,7 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
         const float rt0 = lane_read(t0, src);
         // inactive lanes test the pair of slot 0 (a valid triangle) and drop the result: no divergent
         // branch around the loads
-        const float t = tri_t_culled(tris[tri], ro, rd);
+        const float t = tri_t_culled<kLin>(tris[tri], ro, rd);
         if (act && t <= rt0) atomicMin(&W.key[src], ((unsigned long long)__float_as_uint(t) << 32) | tri);
         tested += count;
     };
@@ -857,7 +877,7 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
         const int src = (int)(e & 63u);
         const v3 rd{lane_read(d.x, src), lane_read(d.y, src), lane_read(d.z, src)};
         const TriRec& tr = tris[(e >> 6) + (pc - r * m)];
-#if RT_RUN_SEL
+        if constexpr (kSel) {
         // every lane loads its normal and writes a ring entry (no exec-mask branches: scalar instructions);
         // the lanes that keep nothing write position queued + 63, past the keepers' [queued, queued + K) for
         // K <= 63 and outside the pending [tested, queued), which holds fewer than 64 entries here
@@ -870,12 +890,13 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
         const uint64_t km = __ballot(keep);
         // (a non-keeper's rank is <= K <= 63, so rank | 63 = 63)
         W.ring[(queued + ((uint32_t)lane_rank(km) | (keep ? 0u : 63u))) & 127u] = (uint16_t)p;
-#else
+        queued += (uint32_t)__popcll(km);
+        } else {
         const bool keep = act && !(dot(rd, v3{tr.nx, tr.ny, tr.nz}) > kFltEpsilon);  // TriangleMesh.cu:72
         const uint64_t km = __ballot(keep);
         if (keep) W.ring[(queued + (uint32_t)lane_rank(km)) & 127u] = (uint16_t)p;
-#endif
         queued += (uint32_t)__popcll(km);
+        }
         __builtin_amdgcn_wave_barrier();
         if (queued - tested >= 64u) full_test(64u);
     }
@@ -1275,7 +1296,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 const uint32_t g = __float_as_uint(ob.f[7]);  // run length (0: inside a run)
                 RT_STAMP(t_m0);
                 if (g != 0u)
-                    mesh_run<kOrd>(S.objs, S.tris, i, g, ob.u1, __float_as_uint(ob.f[6]), live, o, d, inv, h, cnt, W,
+                    mesh_run<kOrd, !kBvh>(S.objs, S.tris, i, g, ob.u1, __float_as_uint(ob.f[6]), live, o, d, inv, h, cnt, W,
                                    lane, skip);
                 RT_STAMP(t_m1);
                 RT_ACC(3, t_m0, t_m1);
@@ -2903,7 +2924,7 @@ uint32_t kernel_build_flags() {
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
     RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1 || RT_PT_BATCH_SEL != 0 || RT_MESH_SELF != 1 || RT_GROUP_RESUME != 1 || \
-    RT_GROUP_MIN_TRIPS != 4 || RT_GROUP_EXIT_LANES != 8 || RT_TRI_MIN != 1 || RT_RUN_SEL != 1
+    RT_GROUP_MIN_TRIPS != 4 || RT_GROUP_EXIT_LANES != 8 || RT_TRI_MIN != 1 || RT_RUN_SEL != 1 || RT_TRI_RCP != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)
