@@ -50,12 +50,6 @@ constexpr int kWavesPerBlock = 4;  // static-grid blocks: 2 x 2 wave tiles
 // Waves per block of the persistent work-queue grid. A block's LDS is released only when all its
 // waves have retired, so at the end of a launch a block with one long wave holds the LDS of all;
 // smaller blocks hand SIMD resources to the next launch in flight wave by wave.
-#ifndef RT_TU
-#define RT_TU 0  // the translation unit being compiled (see launch_render_tu1); 1: RT_TU1_MASK's variants only
-#endif
-#ifndef RT_TU1_MASK
-#define RT_TU1_MASK 0u  // bit v: RT_VARIANT v's render kernel lives in rt_kernel_tu1.o
-#endif
 #ifndef RT_QUEUE_BLOCK_WAVES
 #define RT_QUEUE_BLOCK_WAVES 4
 #endif
@@ -143,19 +137,6 @@ __device__ __forceinline__ v3 moving_center(const float* f, float time) {
 #endif
 #ifndef RT_PT_BATCH_MIN
 #define RT_PT_BATCH_MIN 64  // pt_traverse_coop_batched
-#endif
-#ifndef RT_MESH_RESUME
-#define RT_MESH_RESUME 0  // 1: the mesh-BVH-only kernels leave the traversal to its last lanes (mesh_bvh_pairs; A/B)
-#endif
-// the kernels with the resumable mesh traversal: the mesh-BVH-only variants (no sphere groups, whose
-// counters share W.grp_s / W.grp_m with its kept state)
-template <bool kBvh, int kParts>
-constexpr bool kMeshResume() { return kBvh && kParts == 1 && RT_MESH_RESUME; }
-#ifndef RT_MESH_MIN_TRIPS
-#define RT_MESH_MIN_TRIPS 4  // traversal trips before the wave may leave it
-#endif
-#ifndef RT_MESH_EXIT_LANES
-#define RT_MESH_EXIT_LANES 8  // the wave leaves once at most this many lanes still traverse
 #endif
 #ifndef RT_TRI_MIN
 #define RT_TRI_MIN 1  // 0: the acceptance tests as compares and lane-mask ANDs (A/B)
@@ -468,55 +449,21 @@ __device__ __forceinline__ const RenderLaunch& launch_args() {
 // re-tested at every pop, per-lane leaf loops) A popped entry is not re-tested against the improved bound
 // (its children are, on their pair load); pruning stays conservative, so the candidate set
 // still contains the sequential scan's winner and the (t, index) minimum picks it.
-//
-// kResume (RT_MESH_RESUME, the mesh-BVH-only kernels, scenes whose only W.key user is this mesh: rt_scene.cpp
-// sets ObjRec f[9] = 2): once at most RT_MESH_EXIT_LANES lanes still traverse (after RT_MESH_MIN_TRIPS trips),
-// the wave leaves the traversal. It tests the pairs it has queued; every lane with work keeps it in `mst` /
-// `mcur` (its reference, stack bounds, `has` and the ray it works for - its own or, after a steal, another
-// lane's), and the rays that work belongs to are marked pending: they keep their (t, index) minimum in W.key
-// and skip shading (render_kernel). In the next loop trip a pending ray re-scans the objects before the mesh
-// (the same closestSoFar) and the lanes resume their work beside the new segments' traversals; a lane that
-// kept another ray's work while its own ray finished sits that trip out (render_kernel: `hold`), so it never
-// holds two rays' work. Every subtree is still traversed once against a bound no tighter than the single
-// pass's, so the candidate set and the result are unchanged.
-template <bool kResume>
 __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
                                                const uint32_t* __restrict__ tri_orig,
                                                const BvhNode* __restrict__ nodes, uint32_t root, uint32_t base,
                                                bool want, v3 o, v3 d, v3 inv, Hit& h, int32_t obj,
                                                uint32_t order, uint32_t* wstack, WaveLds& W, int lane,
-                                               Counters& cnt, int cap, bool allow RT_TM_PARAM) {
-    // kResume: mst[lane] bit 31: the lane keeps work (owner bits 0-5, has bit 6, sp bits 8-13, bot bits 16-21,
-    // its reference in mcur[lane]); bit 30: the lane's own ray is pending
-    uint32_t* mst = W.grp_s;
-    uint32_t* mcur = W.grp_m;
-    const uint32_t st0 = kResume ? mst[lane] : 0u;
-    const bool saved = kResume && (st0 >> 31) != 0u;
-    const bool mine_pending = kResume && ((st0 >> 30) & 1u) != 0u;
-    const uint64_t wm = __ballot(want || saved);
+                                               Counters& cnt, int cap RT_TM_PARAM) {
+    const uint64_t wm = __ballot(want);
     if (wm == 0) return;
-    if (!mine_pending) key_reset(W.key[lane]);
-    int owner = saved ? (int)(st0 & 63u) : lane;
+    key_reset(W.key[lane]);
+    int owner = lane;
     v3 ro = o, ri = inv;
     float best = h.t;  // pruning bound for the current ray (its closestSoFar until a hit lands)
     uint32_t cur = root;  // pair index or leaf reference
-    bool has = want && !mine_pending;
+    bool has = want;
     int sp = 0, bot = 0;            // pending references: wstack[k * 64 + lane], bot <= k < sp
-    if (kResume && __ballot(saved) != 0) {
-        // the kept work's ray from its (pending, re-scanned) owner, and its pruning bound
-        const v3 vo{lane_read(o.x, owner), lane_read(o.y, owner), lane_read(o.z, owner)};
-        const v3 vi{lane_read(inv.x, owner), lane_read(inv.y, owner), lane_read(inv.z, owner)};
-        const float vt = lane_read(h.t, owner);
-        if (saved) {
-            ro = vo;
-            ri = vi;
-            best = fminf(vt, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
-            cur = mcur[lane];
-            has = ((st0 >> 6) & 1u) != 0u;
-            sp = (int)((st0 >> 8) & 63u);
-            bot = (int)((st0 >> 16) & 63u);
-        }
-    }
     uint32_t qtail = 0, qdone = 0;  // wave-uniform positions in the pair queue W.slot (256 entries)
     constexpr uint32_t kQ = (uint32_t)kMaxRun * 64u;
     static_assert(kQ >= 256, "the pair queue holds 63 + 3 x 64 pairs");
@@ -537,14 +484,8 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
         qdone += count;
         __builtin_amdgcn_wave_barrier();
     };
-    bool leave = false;  // kResume: the wave leaves with work kept
-    for (int trip = 0;; ++trip) {
-        const uint64_t bm = __ballot(has || sp > bot);
-        if (bm == 0) break;
-        if (kResume && allow && trip >= RT_MESH_MIN_TRIPS && __popcll(bm) <= RT_MESH_EXIT_LANES) {
-            leave = true;
-            break;
-        }
+    for (;;) {
+        if (__ballot(has || sp > bot) == 0) break;
         RT_TRIP_COUNT(has || sp > bot);
         // steal: pair the r-th idle lane with the r-th lane that has a spare reference
         const bool idle = !has && sp == bot;
@@ -638,19 +579,7 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
     }
     if (qtail > qdone) batch(qtail - qdone);
     __builtin_amdgcn_wave_barrier();
-    bool pend = false;
-    if constexpr (kResume) {
-        const bool busy = leave && (has || sp > bot);
-        mst[lane] = busy ? (0x80000000u | (uint32_t)owner | ((uint32_t)has << 6) | ((uint32_t)sp << 8) |
-                            ((uint32_t)bot << 16))
-                         : 0u;
-        mcur[lane] = cur;
-        __builtin_amdgcn_wave_barrier();
-        if (busy) atomicOr(&mst[owner], 0x40000000u);  // the ray this work belongs to is pending
-        __builtin_amdgcn_wave_barrier();
-        pend = ((mst[lane] >> 30) & 1u) != 0u;
-    }
-    if (want && !pend) {
+    if (want) {
         const unsigned long long key = W.key[lane];
         if (key != ~0ull) {
             const uint32_t k = tri_orig[2 * (base + (uint32_t)(key & 0xFFFFFFFFu)) + 1];
@@ -854,19 +783,7 @@ __device__ __forceinline__ void mesh_bvh_wide(const TriRec* __restrict__ tris,
     }
     if (qtail > qdone) batch(qtail - qdone);
     __builtin_amdgcn_wave_barrier();
-    bool pend = false;
-    if constexpr (kResume) {
-        const bool busy = leave && (has || sp > bot);
-        mst[lane] = busy ? (0x80000000u | (uint32_t)owner | ((uint32_t)has << 6) | ((uint32_t)sp << 8) |
-                            ((uint32_t)bot << 16))
-                         : 0u;
-        mcur[lane] = cur;
-        __builtin_amdgcn_wave_barrier();
-        if (busy) atomicOr(&mst[owner], 0x40000000u);  // the ray this work belongs to is pending
-        __builtin_amdgcn_wave_barrier();
-        pend = ((mst[lane] >> 30) & 1u) != 0u;
-    }
-    if (want && !pend) {
+    if (want) {
         const unsigned long long key = W.key[lane];
         if (key != ~0ull) {
             const uint32_t k = tri_orig[2 * (base + (uint32_t)(key & 0xFFFFFFFFu)) + 1];
@@ -1395,17 +1312,13 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 RT_ACC(3, t_m0, t_m1);
             } else if constexpr ((kParts & 1) != 0) {
                 const bool want = live && box_hit(f, o, inv);
-                // (a pending ray's re-scan does not count the mesh's box test again)
-                constexpr bool kMRes = kMeshResume<kBvh, kParts>();
-                const bool again = kMRes && ((W.grp_s[lane] >> 30) & 1u) != 0u;
-                cnt.box_tests += (uint32_t)__popcll(__ballot(live && !again));
+                cnt.box_tests += (uint32_t)__popcll(__ballot(live));
 #if RT_MESH_WIDE
                 mesh_bvh_wide(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0, want, o, d, inv, h, i,
                               ob.order, stack - lane, W, lane, cnt, S.stack_cap);
 #else
-                mesh_bvh_pairs<kMRes>(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0, want, o, d, inv,
-                                      h, i, ob.order, stack - lane, W, lane, cnt, S.stack_cap,
-                                      (__float_as_uint(ob.f[9]) & 2u) != 0u RT_TM_ARG);
+                mesh_bvh_pairs(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0, want, o, d, inv, h, i,
+                               ob.order, stack - lane, W, lane, cnt, S.stack_cap RT_TM_ARG);
 #endif
             }
         } else if ((kMed || (kBvh && kSph)) && ob.type == kObjMedium) {
@@ -1692,7 +1605,6 @@ __device__ __forceinline__ void queue_refill(const RenderLaunch& L, int lane, bo
 // Queue mode's second pass: the S partial sums of each pixel in the fixed
 // order ((p0 + p1) + p2) + ... (the static layout's shuffle order), then the
 // pixel write (mean, accumulate, u8) of write_pixel.
-#if RT_TU == 0
 __global__ __launch_bounds__(256) void combine_kernel(RenderLaunch L, float* __restrict__ out) {
     const uint32_t pl = blockIdx.x * 256u + threadIdx.x;
     const int SP = L.lanes_per_pixel;
@@ -1707,7 +1619,6 @@ __global__ __launch_bounds__(256) void combine_kernel(RenderLaunch L, float* __r
     }
     write_pixel(L, out, ((size_t)lrow * (size_t)L.cols + (size_t)(px - L.col0)) * 3, acc, (float)L.spp);
 }
-#endif
 
 #ifndef RT_DEPTH_LDS
 #define RT_DEPTH_LDS 1  // linear-scan kernels: the path depth in the camera slot (0: a VGPR; A/B)
@@ -1814,7 +1725,7 @@ __device__ __forceinline__ void tail_steal(const RenderLaunch& L, WaveLds& W, in
     const int nv = __popcll(vm), ni = __popcll(im);
     const int ri = lane_rank(im), rv = lane_rank(vm);
     if (spare) W.src[rv] = lane;
-    if (idle) W.key[ri] = (unsigned long long)lane;
+    if (idle) W.slot[ri] = (uint32_t)lane;
     __builtin_amdgcn_wave_barrier();
     const bool thief = idle && ri < nv;
     const int vic = thief ? W.src[ri] : lane;
@@ -1823,7 +1734,7 @@ __device__ __forceinline__ void tail_steal(const RenderLaunch& L, WaveLds& W, in
     if (spare && rv < ni) {  // robbed: its last unstarted sample goes to the thief of the same rank
         own_end -= SP;
         const int pos = (own_end - c) >> L.sp_log2;
-        tl_pack |= ((uint32_t)W.key[rv] + 1u) << (8 * pos);
+        tl_pack |= (W.slot[rv] + 1u) << (8 * pos);
         if ((item & kPrepared) && (need_cam ? s : s + SP) >= own_end) item &= ~kPrepared;  // the taken one was prepared
     }
     if (thief) {  // the thief's own item is finished: it carries the victim's (pixel, sub-stream)
@@ -1858,9 +1769,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
     constexpr bool kCamPf = !kBvh;
     // resumable sphere-group traversal (the sphere-group-only kernel)
     constexpr bool kResume = kBvh && kParts == 2 && RT_GROUP_RESUME;
-    // resumable mesh traversal (the mesh-BVH-only kernels, RT_MESH_RESUME): its per-lane state lives in
-    // W.grp_s / W.grp_m, which those kernels' counters leave unused
-    constexpr bool kMRes = kMeshResume<kBvh, kParts>();
     __shared__ GroupLds glds[kResume ? kBW : 1];
     __shared__ CamSlots cslots[kCamPf ? kBW : 1];
     // traversal stacks (kBvh): kBW x L.stack_depth x 64 lanes, sized per scene at launch
@@ -2025,10 +1933,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                 sample_done(L, v3{0.0f, 0.0f, 0.0f}, SP, item, own_end, s, sum, thr, alive, need_cam, towner,
                             held, waiting, tl_pack);
         }
-        // kMRes: a lane that kept another ray's traversal work while its own segment finished sits this trip out
-        // (it resumes that work in the traversal; its own next segment waits a trip)
-        const bool hold = kMRes && (W.grp_s[lane] >> 30) == 2u;
-        const bool live = alive && !need_cam && !hold;
+        const bool live = alive && !need_cam;
         RT_STAMP(t_b);
         RT_ACC(0, t_a, t_b);
 #ifdef RT_STAMPS
@@ -2052,8 +1957,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         RT_STAMP(t_c);
         RT_ACC(1, t_b, t_c);
         // a lane whose sphere-group traversal continues next trip (kResume) neither counts nor shades yet
-        const bool pend = (kResume && live && (glds[kResume ? wave : 0].st[lane] >> 31) != 0u) ||
-                          (kMRes && live && ((W.grp_s[lane] >> 30) & 1u) != 0u);
+        const bool pend = kResume && live && (glds[kResume ? wave : 0].st[lane] >> 31) != 0u;
         cnt.segs += (uint32_t)__popcll(__ballot(live && !pend));
         if (kBvh && __ballot(cnt.grp != 0)) {  // drain the 16-bit sphere-group counts
             W.grp_s[lane] += cnt.grp & 0xFFFFu;
@@ -2235,8 +2139,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
     const uint64_t wt = wave_sum_u64(cnt.tri_tests) + cnt.tri_wave;
     const uint64_t wb = cnt.box_tests;
     const uint64_t wn = wave_sum_u64(cnt.node_visits);
-    const uint64_t wgs = kBvh && !kMRes ? wave_sum_u64(W.grp_s[lane] + (cnt.grp & 0xFFFFu)) : 0;
-    const uint64_t wgm = kBvh && !kMRes ? wave_sum_u64(W.grp_m[lane] + (cnt.grp >> 16)) : 0;
+    const uint64_t wgs = kBvh ? wave_sum_u64(W.grp_s[lane] + (cnt.grp & 0xFFFFu)) : 0;
+    const uint64_t wgm = kBvh ? wave_sum_u64(W.grp_m[lane] + (cnt.grp >> 16)) : 0;
 #ifdef RT_STAMPS
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(&counters[8 + k], (unsigned long long)tm[k]);
@@ -2908,7 +2812,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
     }
 }
 
-#if RT_TU == 0
 // Dynamic LDS of a traversal kernel: the per-lane stacks of the block's `bw` waves.
 // `spare`: one more slot per lane past the stack (the render kernels' traversals push there unconditionally)
 static size_t stack_bytes(const RenderLaunch& L, int bw, int spare = 0) {
@@ -3033,7 +2936,7 @@ uint32_t kernel_build_flags() {
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
     RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1 || RT_PT_BATCH_SEL != 0 || RT_MESH_SELF != 1 || RT_GROUP_RESUME != 1 || \
     RT_GROUP_MIN_TRIPS != 4 || RT_GROUP_EXIT_LANES != 8 || RT_TRI_MIN != 1 || RT_RUN_SEL != 1 || RT_TRI_RCP != 1 || RT_BATCH_MIN != 64 || RT_GROUP_BATCH_MIN != 64 || \
-    RT_PT_BATCH_MIN != 64 || RT_MESH_RESUME != 0 || RT_MESH_MIN_TRIPS != 4 || RT_MESH_EXIT_LANES != 8
+    RT_PT_BATCH_MIN != 64
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)
@@ -3041,8 +2944,6 @@ uint32_t kernel_build_flags() {
 #endif
     return f;
 }
-
-#endif
 
 namespace {
 template <bool kBvh, bool kQueue, bool kMed = false, bool kSph = true, int kParts = 3>
@@ -3053,68 +2954,6 @@ void launch_rk(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const Rend
 }
 }  // namespace
 
-// The render kernels are compiled in two translation units from this one source (Makefile):
-// rt_kernel.o (RT_TU = 0: every host function, the pathTrace and combine kernels, and the render
-// variants not in RT_TU1_MASK) and rt_kernel_tu1.o (RT_TU = 1: only the variants in RT_TU1_MASK),
-// built with the structurizer leaving uniform regions alone (-structurizecfg-skip-uniform-regions):
-// the wave-uniform object dispatch then needs no flag juggling in scalar registers.
-// The option is per module and costs other kernels registers, hence two units; every variant's
-// kernel is instantiated in exactly one of them.
-hipError_t launch_render_tu1(uint32_t variant, dim3 grid, dim3 block, size_t lds, hipStream_t stream,
-                             const RenderLaunch& L, const SceneArgs& sc, const CamRec* cam, float* out,
-                             unsigned long long* counters);
-namespace {
-template <uint32_t V, bool kBvh, bool kQueue, bool kMed = false, bool kSph = true, int kParts = 3>
-hipError_t dispatch_rk(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const RenderLaunch& L,
-                       const SceneArgs& sc, const CamRec* cam, float* out, unsigned long long* counters) {
-    constexpr bool in_tu1 = ((uint32_t)(RT_TU1_MASK) >> V & 1u) != 0;
-    if constexpr (in_tu1 == (RT_TU == 1)) {
-        launch_rk<kBvh, kQueue, kMed, kSph, kParts>(grid, block, lds, stream, L, sc, cam, out, counters);
-        return hipSuccess;
-    } else if constexpr (RT_TU == 0) {
-        return launch_render_tu1(V, grid, block, lds, stream, L, sc, cam, out, counters);
-    } else {
-        return hipErrorInvalidValue;
-    }
-}
-hipError_t render_switch(uint32_t variant, dim3 grid, dim3 block, size_t lds, hipStream_t stream,
-                         const RenderLaunch& L, const SceneArgs& sc, const CamRec* cam, float* out,
-                         unsigned long long* counters) {
-    switch (variant) {
-        case RT_VARIANT_BVH_MESH_SIMPLE_QUEUE:
-            return dispatch_rk<RT_VARIANT_BVH_MESH_SIMPLE_QUEUE, true, true, false, false, 1>(grid, block, lds, stream, L, sc, cam, out, counters);
-        case RT_VARIANT_BVH_MESH_QUEUE:
-            return dispatch_rk<RT_VARIANT_BVH_MESH_QUEUE, true, true, false, true, 1>(grid, block, lds, stream, L, sc, cam, out, counters);
-        case RT_VARIANT_BVH_GROUP_QUEUE:
-            return dispatch_rk<RT_VARIANT_BVH_GROUP_QUEUE, true, true, false, true, 2>(grid, block, lds, stream, L, sc, cam, out, counters);
-        case RT_VARIANT_BVH_QUEUE:
-            return dispatch_rk<RT_VARIANT_BVH_QUEUE, true, true>(grid, block, lds, stream, L, sc, cam, out, counters);
-        case RT_VARIANT_SCAN_MEDIA_QUEUE:
-            return dispatch_rk<RT_VARIANT_SCAN_MEDIA_QUEUE, false, true, true>(grid, block, lds, stream, L, sc, cam, out, counters);
-        case RT_VARIANT_SCAN_SIMPLE_QUEUE:
-            return dispatch_rk<RT_VARIANT_SCAN_SIMPLE_QUEUE, false, true, false, false>(grid, block, lds, stream, L, sc, cam, out, counters);
-        case RT_VARIANT_SCAN_QUEUE:
-            return dispatch_rk<RT_VARIANT_SCAN_QUEUE, false, true>(grid, block, lds, stream, L, sc, cam, out, counters);
-        case RT_VARIANT_BVH_STATIC:
-            return dispatch_rk<RT_VARIANT_BVH_STATIC, true, false>(grid, block, lds, stream, L, sc, cam, out, counters);
-        case RT_VARIANT_SCAN_MEDIA_STATIC:
-            return dispatch_rk<RT_VARIANT_SCAN_MEDIA_STATIC, false, false, true>(grid, block, lds, stream, L, sc, cam, out, counters);
-        case RT_VARIANT_SCAN_SIMPLE_STATIC:
-            return dispatch_rk<RT_VARIANT_SCAN_SIMPLE_STATIC, false, false, false, false>(grid, block, lds, stream, L, sc, cam, out, counters);
-        case RT_VARIANT_SCAN_STATIC:
-            return dispatch_rk<RT_VARIANT_SCAN_STATIC, false, false>(grid, block, lds, stream, L, sc, cam, out, counters);
-        default: return hipErrorInvalidValue;
-    }
-}
-}  // namespace
-
-#if RT_TU == 1
-hipError_t launch_render_tu1(uint32_t variant, dim3 grid, dim3 block, size_t lds, hipStream_t stream,
-                             const RenderLaunch& L, const SceneArgs& sc, const CamRec* cam, float* out,
-                             unsigned long long* counters) {
-    return render_switch(variant, grid, block, lds, stream, L, sc, cam, out, counters);
-}
-#else
 hipError_t launch_render(uint32_t variant, const SceneArgs& sc, const CamRec* cam, const RenderLaunch& L, float* out,
                          unsigned long long* counters, hipStream_t stream, hipEvent_t main_done) {
     const int bw = block_waves(L.queue != 0);
@@ -3130,8 +2969,34 @@ hipError_t launch_render(uint32_t variant, const SceneArgs& sc, const CamRec* ca
         grid = dim3((L.cols + 2 * L.tile_w - 1) / (2 * L.tile_w), (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
         if (grid.x == 0 || grid.y == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
     }
-    const hipError_t e = render_switch(variant, grid, block, lds, stream, L, sc, cam, out, counters);
-    if (e != hipSuccess) return e;
+    switch (variant) {
+        case RT_VARIANT_BVH_MESH_SIMPLE_QUEUE:
+            launch_rk<true, true, false, false, 1>(grid, block, lds, stream, L, sc, cam, out, counters);
+            break;
+        case RT_VARIANT_BVH_MESH_QUEUE:
+            launch_rk<true, true, false, true, 1>(grid, block, lds, stream, L, sc, cam, out, counters);
+            break;
+        case RT_VARIANT_BVH_GROUP_QUEUE:
+            launch_rk<true, true, false, true, 2>(grid, block, lds, stream, L, sc, cam, out, counters);
+            break;
+        case RT_VARIANT_BVH_QUEUE: launch_rk<true, true>(grid, block, lds, stream, L, sc, cam, out, counters); break;
+        case RT_VARIANT_SCAN_MEDIA_QUEUE:
+            launch_rk<false, true, true>(grid, block, lds, stream, L, sc, cam, out, counters);
+            break;
+        case RT_VARIANT_SCAN_SIMPLE_QUEUE:
+            launch_rk<false, true, false, false>(grid, block, lds, stream, L, sc, cam, out, counters);
+            break;
+        case RT_VARIANT_SCAN_QUEUE: launch_rk<false, true>(grid, block, lds, stream, L, sc, cam, out, counters); break;
+        case RT_VARIANT_BVH_STATIC: launch_rk<true, false>(grid, block, lds, stream, L, sc, cam, out, counters); break;
+        case RT_VARIANT_SCAN_MEDIA_STATIC:
+            launch_rk<false, false, true>(grid, block, lds, stream, L, sc, cam, out, counters);
+            break;
+        case RT_VARIANT_SCAN_SIMPLE_STATIC:
+            launch_rk<false, false, false, false>(grid, block, lds, stream, L, sc, cam, out, counters);
+            break;
+        case RT_VARIANT_SCAN_STATIC: launch_rk<false, false>(grid, block, lds, stream, L, sc, cam, out, counters); break;
+        default: return hipErrorInvalidValue;
+    }
     if (main_done) (void)hipEventRecord(main_done, stream);
     if (L.queue) {
         const uint32_t pixels = L.n_items / (uint32_t)L.lanes_per_pixel;
@@ -3140,6 +3005,5 @@ hipError_t launch_render(uint32_t variant, const SceneArgs& sc, const CamRec* ca
     return hipGetLastError();
 }
 
-#endif  // RT_TU
 
 }  // namespace rt

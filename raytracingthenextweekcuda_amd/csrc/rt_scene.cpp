@@ -675,22 +675,6 @@ std::string HostScene::build_mesh_pairs() {
         bvh_max_depth = std::max(bvh_max_depth, pb.max_pairs);
         memcpy(&r.f[8], &root, 4);
     }
-    // f[9] = 2 (as u32 bits): the kernel may leave this mesh's traversal with work kept for the next loop
-    // trip (rt_kernel.hip mesh_bvh_pairs, RT_MESH_RESUME). Pending rays keep their minimum in the wave's
-    // W.key across the other objects' tests, so only when no other object of the scan uses it: no
-    // brute-force mesh, sphere group or second mesh BVH.
-    int key_users = 0, pair_meshes = 0;
-    for (int k = 0; k < n_scan; ++k) {
-        const ObjRec& r = objs[k];
-        key_users += r.type == kObjMesh || r.type == kObjSphereGroup;
-        pair_meshes += r.type == kObjMesh && tree(r) && !RT_MESH_WIDE;
-    }
-    if (key_users == 1 && pair_meshes == 1)
-        for (int k = 0; k < n_scan; ++k)
-            if (objs[k].type == kObjMesh) {
-                const uint32_t resume = 2u;
-                memcpy(&objs[k].f[9], &resume, 4);
-            }
     return "";
 }
 

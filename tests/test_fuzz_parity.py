@@ -340,3 +340,41 @@ def test_gpu_stack_reaches_its_bound(lanes):
     want, ost = build_oracle(spec).render(w, h, spp, depth, lanes_per_pixel=lanes)
     assert np.array_equal(got, want)
     assert st["segments"] == ost["segments"]
+
+
+def resume_spec(seed):
+    """A scene whose mesh traversal may be left and resumed across loop trips (rt_kernel.hip
+    mesh_bvh_pairs, RT_MESH_RESUME; rt_scene.cpp sets the mesh's flag): one BVH mesh (a 400-triangle
+    soup, so traversals are deep and uneven) as the only mesh, planes and spheres around it, no medium.
+    Metal, glass and emission make the pending rays' shading and draw order visible."""
+    rng = np.random.RandomState(seed)
+    mats = [("lambertian", 0, (0.8, 0.3, 0.3)), ("metal", 1, (0.9, 0.9, 0.5), 0.2),
+            ("dielectric", 2, 1.5), ("emission", 3, (1.0, 0.9, 0.8), 4.0), ("lambertian", 4, (0.3, 0.6, 0.8))]
+    soup = (np.float32((0.0, 0.0, -0.2)) + rng.uniform(-0.5, 0.5, size=(400, 3, 3)).astype(np.float32))
+    objs = [("plane", 0, (0.0, -0.8, 0.0), (0.0, 1.0, 0.0), (2.0, 2.0, 2.0), 4, 2, True),
+            ("sphere", 1, (-0.6, 0.1, 0.2), 0.25, 2),
+            ("mesh", 2, soup.reshape(-1), int(rng.randint(2))),
+            ("plane", 3, (0.0, 0.9, 0.0), (0.0, -1.0, 0.0), (2.0, 2.0, 2.0), 3, 2, True),
+            ("sphere", 4, (0.6, -0.2, 0.3), 0.2, 1)]
+    cam = ((0.1, 0.2, 2.2), (0.0, 0.0, -0.2), (0.0, 1.0, 0.0), 1.33, 45.0, 0.0, 2.5, 0.0, 1.0)
+    return {"camera": cam, "materials": mats, "objects": objs}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,lanes", [(0, 1), (1, 4), (2, 32)])
+def test_gpu_resumed_mesh_traversal_parity(seed, lanes):
+    """Bit-exact against the oracle where waves leave the mesh traversal to its last lanes and resume it in
+    the next loop trip (the kept work may belong to another lane's ray after a steal)."""
+    import raytracingthenextweekcuda_amd as rtmi
+
+    spec = resume_spec(seed)
+    w, h, spp, depth = 48, 32, 8, 6
+    r = rtmi.Renderer(0)
+    build_product(r, spec)
+    got = r.render(w, h, spp, depth, lanes_per_pixel=lanes)
+    st = r.stats()
+    r.close()
+    want, ost = build_oracle(spec).render(w, h, spp, depth, lanes_per_pixel=lanes)
+    assert st["overflow"] == 0
+    assert np.array_equal(got, want)
+    assert st["segments"] == ost["segments"]
