@@ -954,6 +954,9 @@ __device__ __forceinline__ float sphere_candidate(const ObjRec& ob, v3 o, v3 d, 
 #ifndef RT_GROUP_MIN_TRIPS
 #define RT_GROUP_MIN_TRIPS 4   // traversal trips before the wave may leave it
 #endif
+#ifndef RT_GROUP_SEL
+#define RT_GROUP_SEL 1  // the sphere-group trip's pop, push and leaf steps as lane selects (0: branches; A/B)
+#endif
 #ifndef RT_GROUP_EXIT_LANES
 #define RT_GROUP_EXIT_LANES 8  // the wave leaves once at most this many lanes still traverse
 #endif
@@ -1014,6 +1017,42 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
         if (bm == 0) break;
         if (kResume && trip >= RT_GROUP_MIN_TRIPS && __popcll(bm) <= RT_GROUP_EXIT_LANES) break;
         RT_TRIP_COUNT(has || sp > 0);
+#if RT_GROUP_SEL
+        {  // pop as lane selects (the read of slot 0 by lanes that do not pop is discarded)
+            const bool pop = !has && sp > 0;
+            const uint32_t v = wstack[(pop ? sp - 1 : 0) * 64 + lane];
+            cur = pop ? v : cur;
+            sp -= pop ? 1 : 0;
+            has = has || pop;
+        }
+        if (has && !(cur & kLeafRef)) {
+            const BvhNode nl = nodes[2 * (size_t)cur], nr = nodes[2 * (size_t)cur + 1];
+            cnt.node_visits += 2;
+            float tl, tr;
+            const bool hl = node_hit(nl, o, inv, best, tl);
+            const bool hr = node_hit(nr, o, inv, best, tr);
+            // as lane selects; a lane that does not push writes the spare slot `cap` (never read)
+            const bool both = hl && hr, lf = tl <= tr;
+            const bool ovf = both && sp + 1 > cap;
+            if (__builtin_expect(__ballot(ovf) != 0, 0))
+                if (ovf) cnt.overflow();
+            const bool push = both && !ovf;
+            wstack[(push ? sp : cap) * 64 + lane] = lf ? nr.a : nl.a;
+            sp = ovf ? 0 : sp + (push ? 1 : 0);
+            cur = both ? (lf ? nl.a : nr.a) : (hl ? nl.a : nr.a);
+            has = (hl || hr) && !ovf;
+        }
+        uint32_t lk = 0, ln = 0;
+        {
+            const bool leaf = has && (cur & kLeafRef);
+            const uint32_t nt = ((cur >> 27) & 15u) + 1u;
+            lk = cur & 0x07FFFFFFu;
+            ln = leaf ? (nt < 3u ? nt : 3u) : 0u;
+            cur = leaf && nt > 3u ? (kLeafRef | ((nt - 4u) << 27) | (lk + 3u)) : cur;
+            has = has && !(leaf && nt <= 3u);
+        }
+#else
+        RT_TRIP_COUNT(has || sp > 0);
         if (!has && sp > 0) {
             cur = wstack[(--sp) * 64 + lane];
             has = true;
@@ -1052,6 +1091,7 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
             else
                 has = false;
         }
+#endif
         const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
         if (b1) {
             const uint32_t at = qtail + (uint32_t)(lane_rank(b1) + lane_rank(b2) + lane_rank(b3));
@@ -1450,7 +1490,7 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #define RT_PT_WAVES 6
 #endif
 #ifndef RT_PT_BATCH_SEL
-#define RT_PT_BATCH_SEL 0  // 1: pathTrace's batched Kuchkuda test as lane selects (A/B: neutral, spills 20 B)
+#define RT_PT_BATCH_SEL 1  // pathTrace's batched Kuchkuda test as lane selects (0: nested branches; A/B)
 #endif
 #ifdef RT_WAVES_PER_EU
 #undef RT_BVH_WAVES
@@ -2934,9 +2974,9 @@ uint32_t kernel_build_flags() {
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
     RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
-    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1 || RT_PT_BATCH_SEL != 0 || RT_MESH_SELF != 1 || RT_GROUP_RESUME != 1 || \
+    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1 || RT_PT_BATCH_SEL != 1 || RT_MESH_SELF != 1 || RT_GROUP_RESUME != 1 || \
     RT_GROUP_MIN_TRIPS != 4 || RT_GROUP_EXIT_LANES != 8 || RT_TRI_MIN != 1 || RT_RUN_SEL != 1 || RT_TRI_RCP != 1 || RT_BATCH_MIN != 64 || RT_GROUP_BATCH_MIN != 64 || \
-    RT_PT_BATCH_MIN != 64
+    RT_PT_BATCH_MIN != 64 || RT_GROUP_SEL != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)
