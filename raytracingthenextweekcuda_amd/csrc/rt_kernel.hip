@@ -1480,6 +1480,9 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #ifndef RT_NOSPH_WAVES
 #define RT_NOSPH_WAVES 7
 #endif
+#ifndef RT_BVH_MESH_WAVES
+#define RT_BVH_MESH_WAVES 5  // the mesh-BVH-only kernel with the full material set (Suzanne; 96 VGPRs fit 5)
+#endif
 #ifndef RT_GROUP_WAVES
 #define RT_GROUP_WAVES 5
 #endif
@@ -1499,6 +1502,7 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #undef RT_NOSPH_WAVES
 #undef RT_GROUP_WAVES
 #undef RT_BVH_SIMPLE_WAVES
+#undef RT_BVH_MESH_WAVES
 #undef RT_PT_WAVES
 #define RT_BVH_WAVES RT_WAVES_PER_EU
 #define RT_SCAN_WAVES RT_WAVES_PER_EU
@@ -1506,11 +1510,13 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #define RT_NOSPH_WAVES RT_WAVES_PER_EU
 #define RT_GROUP_WAVES RT_WAVES_PER_EU
 #define RT_BVH_SIMPLE_WAVES RT_WAVES_PER_EU
+#define RT_BVH_MESH_WAVES RT_WAVES_PER_EU
 #define RT_PT_WAVES RT_WAVES_PER_EU
 #endif
 template <bool kBvh, bool kMed = false, bool kSph = true, int kParts = 3>
 constexpr int render_waves() {
-    return kBvh ? (kParts == 2 ? RT_GROUP_WAVES : (kSph ? RT_BVH_WAVES : RT_BVH_SIMPLE_WAVES))
+    return kBvh ? (kParts == 2 ? RT_GROUP_WAVES
+                               : (kSph ? (kParts == 1 ? RT_BVH_MESH_WAVES : RT_BVH_WAVES) : RT_BVH_SIMPLE_WAVES))
                 : (kMed ? RT_MED_WAVES : (kSph ? RT_SCAN_WAVES : RT_NOSPH_WAVES));
 }
 
@@ -2425,10 +2431,11 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
             const float k = dot(nn, pd);
             const float sd = fdiv(q0.w - dot(nn, po), k);
             const v3 hit = add(scale(pd, sd), po);
-            const bool in = !(dot(v3{q1.x, q1.y, q1.z}, hit) - q1.w < 0.0f) &
-                            !(dot(v3{q2.x, q2.y, q2.z}, hit) - q2.w < 0.0f) &
-                            !(dot(v3{q3.x, q3.y, q3.z}, hit) - q3.w < 0.0f);
-            const bool ok = act & (pav != idx) & (k != 0.0f) & (sd > 0.0f) & (sd > 1e-3f) & in;  // NUDGE_FACTOR
+            // the three edge tests !(e < 0) as one: fminf drops a NaN e, which passes its own test, and the
+            // minimum of the others is < 0 iff one of them fails (all NaN: NaN, which passes)
+            const float emin = fminf(fminf(dot(v3{q1.x, q1.y, q1.z}, hit) - q1.w, dot(v3{q2.x, q2.y, q2.z}, hit) - q2.w),
+                                     dot(v3{q3.x, q3.y, q3.z}, hit) - q3.w);
+            const bool ok = act && (pav != idx) && (k != 0.0f) && (sd > 1e-3f) && !(emin < 0.0f);  // NUDGE_FACTOR (sd > 0 implied)
             const v3 df = sub(po, hit);
             const float hz = df.x * df.x + df.y * df.y + df.z * df.z;  // distancesq
             const unsigned long long key = ((unsigned long long)__float_as_uint(hz) << 32) | i;
@@ -2972,7 +2979,7 @@ uint32_t kernel_build_flags() {
     f |= 2u;  // RT_BUILD_STAMPS
 #endif
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
-    RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || \
+    RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || RT_BVH_MESH_WAVES != 5 || \
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
     RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1 || RT_PT_BATCH_SEL != 1 || RT_MESH_SELF != 1 || RT_GROUP_RESUME != 1 || \
     RT_GROUP_MIN_TRIPS != 4 || RT_GROUP_EXIT_LANES != 8 || RT_TRI_MIN != 1 || RT_RUN_SEL != 1 || RT_TRI_RCP != 1 || RT_BATCH_MIN != 64 || RT_GROUP_BATCH_MIN != 64 || \
