@@ -393,6 +393,9 @@ __device__ __forceinline__ float fresh_f32(float v) {
 #ifndef RT_DIV_NR
 #define RT_DIV_NR 1  // 0: IEEE divisions in the plane test and Lambertian's normalize (A/B)
 #endif
+#ifndef RT_SCATTER_NR
+#define RT_SCATTER_NR 1  // Lambertian's scattered direction normalized by Markstein quotients (0: IEEE; A/B)
+#endif
 
 // __shfl(v, src, 64) without HIP's lane-id arithmetic: ds_bpermute reads lane (address / 4) mod 64,
 // the same lane __shfl picks. HIP's version derives its own lane id (mbcnt) for the width mask,
@@ -2060,8 +2063,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                 v3 u = normalize(rp);
 #endif
                 v3 sd = add(n, u);
-                if ((fabsf(sd.x) < 1e-8f) && (fabsf(sd.y) < 1e-8f) && (fabsf(sd.z) < 1e-8f)) sd = n;
+                const bool degen = (fabsf(sd.x) < 1e-8f) && (fabsf(sd.y) < 1e-8f) && (fabsf(sd.z) < 1e-8f);
+                if (degen) sd = n;
+#if RT_DIV_NR && RT_SCATTER_NR
+                {
+                    // normalize(sd) by Markstein quotients. Outside the degenerate case |sd| >= 1e-8 (and <= 2), so
+                    // the norm is in the domain; a component is in it when it is +0 (sd = n + u is never -0: u has
+                    // no -0 components, n + u cancels to +0) or at least 2^-100 in magnitude (its quotient then at
+                    // least 2^-101). A wave with a degenerate lane (sd = n may hold -0) or a component in
+                    // (0, 2^-100) takes the IEEE divisions.
+                    const float ns = fsqrt(sd.x * sd.x + sd.y * sd.y + sd.z * sd.z);
+                    const float ys = rcp_nr(ns);
+                    nd = v3{div_y(sd.x, ns, ys), div_y(sd.y, ns, ys), div_y(sd.z, ns, ys)};
+                    // |c| in (0, 2^-100) iff bits(|c|) - 1 < bits(2^-100) - 1 (unsigned; +0 wraps)
+                    const uint32_t tiny = __builtin_elementwise_min(
+                        __builtin_elementwise_min((__float_as_uint(sd.x) & 0x7FFFFFFFu) - 1u,
+                                                  (__float_as_uint(sd.y) & 0x7FFFFFFFu) - 1u),
+                        (__float_as_uint(sd.z) & 0x7FFFFFFFu) - 1u);
+                    const bool ieee = degen || tiny < 0x0D7FFFFFu;
+                    if (__builtin_expect(__ballot(ieee) != 0, 0))
+                        if (ieee) nd = normalize(sd);
+                }
+#else
                 nd = normalize(sd);
+#endif
                 att = v3{m.a0, m.a1, m.a2};
                 scattered = true;
             } else if (kSph && m.type == 1u) {
@@ -2983,7 +3008,7 @@ uint32_t kernel_build_flags() {
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
     RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1 || RT_PT_BATCH_SEL != 1 || RT_MESH_SELF != 1 || RT_GROUP_RESUME != 1 || \
     RT_GROUP_MIN_TRIPS != 4 || RT_GROUP_EXIT_LANES != 8 || RT_TRI_MIN != 1 || RT_RUN_SEL != 1 || RT_TRI_RCP != 1 || RT_BATCH_MIN != 64 || RT_GROUP_BATCH_MIN != 64 || \
-    RT_PT_BATCH_MIN != 64 || RT_GROUP_SEL != 1
+    RT_PT_BATCH_MIN != 64 || RT_GROUP_SEL != 1 || RT_SCATTER_NR != 1
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)
