@@ -138,6 +138,18 @@ __device__ __forceinline__ v3 moving_center(const float* f, float time) {
 #ifndef RT_PT_BATCH_MIN
 #define RT_PT_BATCH_MIN 64  // pt_traverse_coop_batched
 #endif
+#ifndef RT_MESH_DEFER
+#define RT_MESH_DEFER 1  // the mesh-BVH-only kernels defer a traversal only a few rays want (0: never; A/B)
+#endif
+#ifndef RT_DEFER_MIN
+#define RT_DEFER_MIN 32  // ... when fewer than this many lanes want it
+#endif
+// The mesh-BVH-only kernels (no sphere groups, whose counters use W.grp_s / W.grp_m: here they hold the
+// per-lane deferral bits) may defer a traversal that only a few lanes want (RT_MESH_DEFER): those rays skip
+// shading and scan again in the next loop trip, beside the rays that want the mesh then. A wave never
+// defers twice in a row, so a deferred ray is traced in the next trip.
+template <bool kBvh, int kParts>
+constexpr bool kMeshDefer() { return kBvh && kParts == 1 && RT_MESH_DEFER; }
 #ifndef RT_TRI_MIN
 #define RT_TRI_MIN 1  // 0: the acceptance tests as compares and lane-mask ANDs (A/B)
 #endif
@@ -1355,7 +1367,19 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 RT_ACC(3, t_m0, t_m1);
             } else if constexpr ((kParts & 1) != 0) {
                 const bool want = live && box_hit(f, o, inv);
-                cnt.box_tests += (uint32_t)__popcll(__ballot(live));
+                constexpr bool kDef = kMeshDefer<kBvh, kParts>();
+                // W.grp_s bit 0: this lane's ray was deferred last trip (its re-scan counts no box test again);
+                // bit 1: deferred in this trip
+                const bool again = kDef && (W.grp_s[lane] & 1u) != 0u;
+                cnt.box_tests += (uint32_t)__popcll(__ballot(live && !again));
+                if constexpr (kDef) {
+                    const int nw = __popcll(__ballot(want));
+                    if ((__float_as_uint(ob.f[9]) & 2u) != 0u && nw > 0 && nw < RT_DEFER_MIN &&
+                        __ballot(again) == 0) {
+                        if (want) W.grp_s[lane] |= 2u;
+                        return;  // (this object's visit: the rest of the scan goes on)
+                    }
+                }
 #if RT_MESH_WIDE
                 mesh_bvh_wide(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0, want, o, d, inv, h, i,
                               ob.order, stack - lane, W, lane, cnt, S.stack_cap);
@@ -1818,6 +1842,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
     constexpr bool kCamPf = !kBvh;
     // resumable sphere-group traversal (the sphere-group-only kernel)
     constexpr bool kResume = kBvh && kParts == 2 && RT_GROUP_RESUME;
+    constexpr bool kDef = kMeshDefer<kBvh, kParts>();  // deferrable mesh traversal (W.grp_s bits 0-1)
     __shared__ GroupLds glds[kResume ? kBW : 1];
     __shared__ CamSlots cslots[kCamPf ? kBW : 1];
     // traversal stacks (kBvh): kBW x L.stack_depth x 64 lanes, sized per scene at launch
@@ -1983,6 +2008,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                             held, waiting, tl_pack);
         }
         const bool live = alive && !need_cam;
+        if constexpr (kDef) W.grp_s[lane] = (W.grp_s[lane] >> 1) & 1u;  // bit 0: deferred on the last trip
         RT_STAMP(t_b);
         RT_ACC(0, t_a, t_b);
 #ifdef RT_STAMPS
@@ -2006,7 +2032,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         RT_STAMP(t_c);
         RT_ACC(1, t_b, t_c);
         // a lane whose sphere-group traversal continues next trip (kResume) neither counts nor shades yet
-        const bool pend = kResume && live && (glds[kResume ? wave : 0].st[lane] >> 31) != 0u;
+        const bool pend = (kResume && live && (glds[kResume ? wave : 0].st[lane] >> 31) != 0u) ||
+                          (kDef && live && (W.grp_s[lane] & 2u) != 0u);
         cnt.segs += (uint32_t)__popcll(__ballot(live && !pend));
         if (kBvh && __ballot(cnt.grp != 0)) {  // drain the 16-bit sphere-group counts
             W.grp_s[lane] += cnt.grp & 0xFFFFu;
@@ -2210,8 +2237,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
     const uint64_t wt = wave_sum_u64(cnt.tri_tests) + cnt.tri_wave;
     const uint64_t wb = cnt.box_tests;
     const uint64_t wn = wave_sum_u64(cnt.node_visits);
-    const uint64_t wgs = kBvh ? wave_sum_u64(W.grp_s[lane] + (cnt.grp & 0xFFFFu)) : 0;
-    const uint64_t wgm = kBvh ? wave_sum_u64(W.grp_m[lane] + (cnt.grp >> 16)) : 0;
+    const uint64_t wgs = kBvh && !kDef ? wave_sum_u64(W.grp_s[lane] + (cnt.grp & 0xFFFFu)) : 0;
+    const uint64_t wgm = kBvh && !kDef ? wave_sum_u64(W.grp_m[lane] + (cnt.grp >> 16)) : 0;
 #ifdef RT_STAMPS
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(&counters[8 + k], (unsigned long long)tm[k]);
@@ -3008,7 +3035,8 @@ uint32_t kernel_build_flags() {
     RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
     RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1 || RT_PT_BATCH_SEL != 1 || RT_MESH_SELF != 1 || RT_GROUP_RESUME != 1 || \
     RT_GROUP_MIN_TRIPS != 4 || RT_GROUP_EXIT_LANES != 8 || RT_TRI_MIN != 1 || RT_RUN_SEL != 1 || RT_TRI_RCP != 1 || RT_BATCH_MIN != 64 || RT_GROUP_BATCH_MIN != 64 || \
-    RT_PT_BATCH_MIN != 64 || RT_GROUP_SEL != 1 || RT_SCATTER_NR != 1
+    RT_PT_BATCH_MIN != 64 || RT_GROUP_SEL != 1 || RT_SCATTER_NR != 1 || RT_MESH_DEFER != 1 || \
+    RT_DEFER_MIN != 32
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)

@@ -675,6 +675,22 @@ std::string HostScene::build_mesh_pairs() {
         bvh_max_depth = std::max(bvh_max_depth, pb.max_pairs);
         memcpy(&r.f[8], &root, 4);
     }
+    // f[9] = 2 (as u32 bits): the kernel may defer this mesh's traversal for its few wanting rays to the next
+    // loop trip (rt_kernel.hip RT_MESH_DEFER). A deferred ray scans the list again, so only when no object of
+    // the scan draws from the ray's stream (a participating medium) or counts its tests per scan (a
+    // brute-force mesh), and this is the scan's only mesh (no sphere group either).
+    int meshes = 0, others = 0;
+    for (int k = 0; k < n_scan; ++k) {
+        const ObjRec& r = objs[k];
+        meshes += r.type == kObjMesh;
+        others += r.type == kObjMedium || r.type == kObjSphereGroup || (r.type == kObjMesh && !tree(r));
+    }
+    if (meshes == 1 && others == 0 && !RT_MESH_WIDE)
+        for (int k = 0; k < n_scan; ++k)
+            if (objs[k].type == kObjMesh) {
+                const uint32_t defer = 2u;
+                memcpy(&objs[k].f[9], &defer, 4);
+            }
     return "";
 }
 

@@ -51,7 +51,8 @@ struct alignas(16) ObjRec {
     // mesh: boundsMin xyz, boundsMax xyz (computeMeshAABB, main.cu:261-281), f[6] = the bits of
     //       ceil(2^32 / triangle count) (the brute-force compaction's division), f[7] = mesh-run
     //       length (brute force), f[8] = root child-pair reference (BVH meshes), f[9] = 1 (as u32 bits)
-    //       for a brute-force mesh that is a convex shell (rt_scene.cpp convex_shell, RT_MESH_SELF)
+    //       for a brute-force mesh that is a convex shell (rt_scene.cpp convex_shell, RT_MESH_SELF), 2 for a BVH
+//       mesh whose traversal the kernel may defer to the next loop trip (build_mesh_pairs, RT_MESH_DEFER)
     float f[10];
 };
 constexpr uint32_t kNoBvh = 0xFFFFFFFFu;
