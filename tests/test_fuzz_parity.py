@@ -343,10 +343,11 @@ def test_gpu_stack_reaches_its_bound(lanes):
 
 
 def resume_spec(seed):
-    """A scene whose mesh traversal may be left and resumed across loop trips (rt_kernel.hip
-    mesh_bvh_pairs, RT_MESH_RESUME; rt_scene.cpp sets the mesh's flag): one BVH mesh (a 400-triangle
-    soup, so traversals are deep and uneven) as the only mesh, planes and spheres around it, no medium.
-    Metal, glass and emission make the pending rays' shading and draw order visible."""
+    """A scene whose mesh traversal the kernel may defer to the next loop trip when few rays of a wave
+    want it (rt_kernel.hip RT_MESH_DEFER; rt_scene.cpp build_mesh_pairs sets the mesh's flag): one BVH
+    mesh (a 400-triangle soup, so traversals are deep and uneven) as the scan's only mesh, planes and
+    spheres around it, no medium. Metal, glass and emission make the deferred rays' shading and draw
+    order visible."""
     rng = np.random.RandomState(seed)
     mats = [("lambertian", 0, (0.8, 0.3, 0.3)), ("metal", 1, (0.9, 0.9, 0.5), 0.2),
             ("dielectric", 2, 1.5), ("emission", 3, (1.0, 0.9, 0.8), 4.0), ("lambertian", 4, (0.3, 0.6, 0.8))]
@@ -363,8 +364,8 @@ def resume_spec(seed):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed,lanes", [(0, 1), (1, 4), (2, 32)])
 def test_gpu_resumed_mesh_traversal_parity(seed, lanes):
-    """Bit-exact against the oracle where waves leave the mesh traversal to its last lanes and resume it in
-    the next loop trip (the kept work may belong to another lane's ray after a steal)."""
+    """Bit-exact against the oracle where waves defer a mesh traversal few of their rays want to the next
+    loop trip (the deferred rays scan again and shade a trip later; segment counts unchanged)."""
     import raytracingthenextweekcuda_amd as rtmi
 
     spec = resume_spec(seed)
