@@ -138,30 +138,20 @@ __device__ __forceinline__ v3 moving_center(const float* f, float time) {
 #ifndef RT_PT_BATCH_MIN
 #define RT_PT_BATCH_MIN 64  // pt_traverse_coop_batched
 #endif
-#ifndef RT_MESH_DEFER
-#define RT_MESH_DEFER 1  // the mesh-BVH-only kernels defer a traversal only a few rays want (0: never; A/B)
-#endif
 #ifndef RT_DEFER_MIN
-#define RT_DEFER_MIN 32  // ... when fewer than this many lanes want it
+#define RT_DEFER_MIN 32  // the mesh-BVH-only kernels defer a traversal when fewer than this many lanes want it
 #endif
 // The mesh-BVH-only kernels (no sphere groups, whose counters use W.grp_s / W.grp_m: here they hold the
-// per-lane deferral bits) may defer a traversal that only a few lanes want (RT_MESH_DEFER): those rays skip
-// shading and scan again in the next loop trip, beside the rays that want the mesh then. A wave never
-// defers twice in a row, so a deferred ray is traced in the next trip.
+// per-lane deferral bits) defer a traversal that only a few lanes want: those rays skip shading and scan
+// again in the next loop trip, beside the rays that want the mesh then. A wave never defers twice in a row,
+// so a deferred ray is traced in the next trip.
 template <bool kBvh, int kParts>
-constexpr bool kMeshDefer() { return kBvh && kParts == 1 && RT_MESH_DEFER; }
-#ifndef RT_TRI_MIN
-#define RT_TRI_MIN 1  // 0: the acceptance tests as compares and lane-mask ANDs (A/B)
-#endif
-#ifndef RT_RUN_SEL
-#define RT_RUN_SEL 1  // 0: mesh_run's cull loop with exec-mask branches (A/B)
-#endif
+constexpr bool kMeshDefer() { return kBvh && kParts == 1; }
 // TriangleMesh.cu:74-105's acceptance of a Moller-Trumbore solution: t >= FLT_EPSILON, t >= tMin
 // (implied by the first for every t: tMin > FLT_EPSILON), b1, b2 and 1 - b1 - b2 >= FLT_EPSILON.
 // Returns t if all hold, else NaN.
 __device__ __forceinline__ float tri_accept(float t, float b1, float b2) {
     const float u = 1.0f - b1 - b2;
-#if RT_TRI_MIN
     // x >= c iff x - (the float below c) > 0, for every float x with gradual underflow (the difference
     // of two distinct floats is never rounded to zero; +-inf and NaN compare the same way). The four
     // differences meet in gfx950's NaN-propagating minimum (v_minimum3_f32): it is > 0 iff every
@@ -170,10 +160,6 @@ __device__ __forceinline__ float tri_accept(float t, float b1, float b2) {
         __builtin_elementwise_minimum(t - 0x1.0624dcp-10f /* the float below kTMin */, b1 - 0x1.fffffep-24f),
         __builtin_elementwise_minimum(b2 - 0x1.fffffep-24f /* the float below FLT_EPSILON */, u - 0x1.fffffep-24f));
     return m > 0.0f ? t : __builtin_nanf("");
-#else
-    const bool ok = (t >= kFltEpsilon) & (t >= kTMin) & (b1 >= kFltEpsilon) & (b2 >= kFltEpsilon) & (u >= kFltEpsilon);
-    return ok ? t : __builtin_nanf("");
-#endif
 }
 
 // RN(1 / b) for |b| in [2^-126, 2^126); Markstein's RN(a / b) from it (callers bound the domain)
@@ -186,22 +172,15 @@ __device__ __forceinline__ float div_y(float a, float b, float y) {
     return __builtin_fmaf(__builtin_fmaf(-b, q0, a), y, q0);
 }
 
-#ifndef RT_TRI_RCP
-#define RT_TRI_RCP 1  // 0: the Moller-Trumbore 1 / det as the IEEE division expansion (A/B)
-#endif
 // TriangleMesh.cu:84's 1.0f / det, correctly rounded, for the brute-force meshes' batched tests (all 64 lanes at once; the
 // batched tests): v_rcp_f32 + one Newton step is RN(1 / b) for every |b| in [2^-126, 2^126) (exhaustive GPU
 // check, tools/div_check.hip); a wave with any other det (zero, subnormal, huge, inf, NaN) takes the IEEE
 // division.
 __device__ __forceinline__ float tri_rcp(float det) {
-#if RT_TRI_RCP
     float y = rcp_nr(det);
     const float a = fabsf(det);
     if (__builtin_expect(__ballot(!(a >= 0x1p-126f && a < 0x1p126f)) != 0, 0)) y = fdiv(1.0f, det);
     return y;
-#else
-    return fdiv(1.0f, det);
-#endif
 }
 
 // One triangle of TriangleMesh::hit (TriangleMesh.cu:40-108) without the
@@ -316,7 +295,7 @@ struct WaveLds {
     uint16_t ring[128];          // pair ids that passed the backface cull, awaiting the full test
 };
 
-// The sphere-group traversal's per-lane state that outlives a loop trip (RT_GROUP_RESUME): a lane whose
+// The sphere-group traversal's per-lane state that outlives a loop trip (kResume): a lane whose
 // traversal is still running when the wave leaves it keeps its reference, stack depth and (t, ~order)
 // minimum here and resumes in the next trip (the member stack stays in the LDS stacks).
 struct GroupLds {
@@ -399,31 +378,14 @@ __device__ __forceinline__ float fresh_f32(float v) {
 // |a/b| in [2^-121, 2^125) (Markstein's theorem; the same check draws 4.3e9 random pairs of that
 // domain: no mismatch). Callers use them only where their operands provably lie in these domains,
 // or fall back to the IEEE division for the wave.
-#ifndef RT_RCP_NR
-#define RT_RCP_NR 1  // 0: IEEE divisions for the inverse direction (A/B)
-#endif
-#ifndef RT_DIV_NR
-#define RT_DIV_NR 1  // 0: IEEE divisions in the plane test and Lambertian's normalize (A/B)
-#endif
-#ifndef RT_SCATTER_NR
-#define RT_SCATTER_NR 1  // Lambertian's scattered direction normalized by Markstein quotients (0: IEEE; A/B)
-#endif
 
 // __shfl(v, src, 64) without HIP's lane-id arithmetic: ds_bpermute reads lane (address / 4) mod 64,
 // the same lane __shfl picks. HIP's version derives its own lane id (mbcnt) for the width mask,
 // a value the register allocator kept live across the persistent loop - and spilled to scratch.
-#ifndef RT_LANE_READ
-#define RT_LANE_READ 1  // 0: HIP's __shfl (A/B)
-#endif
-#if RT_LANE_READ
 __device__ __forceinline__ int lane_read(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
 __device__ __forceinline__ float lane_read(float v, int src) {
     return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
 }
-#else
-__device__ __forceinline__ int lane_read(int v, int src) { return __shfl(v, src, 64); }
-__device__ __forceinline__ float lane_read(float v, int src) { return __shfl(v, src, 64); }
-#endif
 
 // Sets an LDS 64-bit minimum slot to +inf (all ones).
 __device__ __forceinline__ void key_reset(unsigned long long& k) {
@@ -604,210 +566,6 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
     __builtin_amdgcn_wave_barrier();
 }
 
-#if RT_MESH_WIDE
-// The batched mesh traversal over 4-wide nodes (rt_scene.cpp WideBuilder: the binary SAH tree with
-// adjacent levels collapsed). An inner step is one aligned 128 B node load and four
-// box tests; the hit children are ordered by entry distance (the key's two low bits carry the child
-// slot, so one unsigned sort network orders keys and slots together), the nearest becomes the lane's
-// reference and the others wait in ONE stack entry: the node and their slots, nearest first. A pop
-// takes the entry's next child (one 4 B load of its reference) and keeps the entry while children
-// remain, so a lane holds at most one entry per wide level: the LDS stacks are no deeper than the
-// binary tree's (round 4 pushed every other child and needed 27 entries for the bunny against 18,
-// which cost a block per CU). Thieves take the next child of a victim's oldest entry. Leaves,
-// batched triangle tests, pruning and the (t, index) minimum are those of mesh_bvh_pairs, so the
-// candidate set - and the image - is the binary tree's.
-__device__ __forceinline__ void mesh_bvh_wide(const TriRec* __restrict__ tris,
-                                              const uint32_t* __restrict__ tri_orig,
-                                              const BvhNode* __restrict__ nodes, uint32_t root, uint32_t base,
-                                              bool want, v3 o, v3 d, v3 inv, Hit& h, int32_t obj,
-                                              uint32_t order, uint32_t* wstack, WaveLds& W, int lane,
-                                              Counters& cnt, int cap) {
-    const uint64_t wm = __ballot(want);
-    if (wm == 0) return;
-    key_reset(W.key[lane]);
-    int owner = lane;
-    v3 ro = o, ri = inv;
-    float best = h.t;
-    uint32_t cur = root;  // wide node index or leaf reference
-    bool has = want;
-    int sp = 0, bot = 0;
-    uint32_t qtail = 0, qdone = 0;
-    constexpr uint32_t kQ = (uint32_t)kMaxRun * 64u;
-    constexpr uint32_t kNodeMask = (1u << kWideNodeBits) - 1u;
-    constexpr uint32_t kKeyInf = 0x7F800000u;  // +inf: a missed child
-    const uint32_t* nref = reinterpret_cast<const uint32_t*>(nodes);  // child refs: word 32 q + 24 + slot
-    // an entry whose next child exists for every lane (reads by lanes whose own entry is not used)
-    const uint32_t e_safe = (root & kNodeMask) | (1u << 29);
-    __builtin_amdgcn_wave_barrier();
-    auto batch = [&](uint32_t count) {
-        const bool act = (uint32_t)lane < count;
-        const uint32_t e = act ? W.slot[(qdone + (uint32_t)lane) & (kQ - 1)] : 0u;
-        const uint32_t k = e >> 6;
-        const int own = (int)(e & 63u);
-        const v3 po{lane_read(o.x, own), lane_read(o.y, own), lane_read(o.z, own)};
-        const v3 pd{lane_read(d.x, own), lane_read(d.y, own), lane_read(d.z, own)};
-        const float pt0 = lane_read(h.t, own);
-        const float t = tri_t(tris[k], po, pd);
-        if (act && t <= pt0)
-            atomicMin(&W.key[own], ((unsigned long long)__float_as_uint(t) << 32) | tri_orig[2 * k]);
-        qdone += count;
-        __builtin_amdgcn_wave_barrier();
-    };
-    // the entry without its next child (0: none left)
-    auto rest_of = [&](uint32_t e) -> uint32_t {
-        const uint32_t n = e >> 29;
-        return n > 1u ? ((e & kNodeMask) | (((e >> (kWideNodeBits + 2)) & 15u) << kWideNodeBits) | ((n - 1u) << 29))
-                      : 0u;
-    };
-    auto next_ref = [&](uint32_t e) -> uint32_t {
-        return nref[32u * (e & kNodeMask) + 24u + ((e >> kWideNodeBits) & 3u)];
-    };
-    for (;;) {
-        if (__ballot(has || sp > bot) == 0) break;
-        // steal: the r-th idle lane takes the next child of the oldest entry of the r-th lane with a spare one
-        const bool idle = !has && sp == bot;
-        const bool spare = sp - bot >= (has ? 1 : 2);
-        const uint64_t im = __ballot(idle), vm = __ballot(spare);
-        if (im != 0 && vm != 0) {
-            const int nv = __popcll(vm), ni = __popcll(im);
-            if (spare) W.src[lane_rank(vm)] = lane;
-            __builtin_amdgcn_wave_barrier();
-            const bool thief = idle && lane_rank(im) < nv;
-            const int vr = W.src[lane_rank(im)];
-            const int vic = thief ? vr : lane;
-            const int vt = lane_read(bot, vic);
-            auto take = [&](float& x) {
-                const float v = lane_read(x, vic);
-                if (thief) x = v;
-            };
-            {
-                const int v_owner = lane_read(owner, vic);
-                if (thief) owner = v_owner;
-            }
-            take(ro.x); take(ro.y); take(ro.z);
-            take(ri.x); take(ri.y); take(ri.z);
-            take(best);
-            const bool robbed = spare && lane_rank(vm) < ni;
-            {
-                const uint32_t ve = wstack[vt * 64 + vic];  // the victim's oldest entry (a valid slot for every lane)
-                const uint32_t vref = next_ref(thief ? ve : e_safe);
-                const float kb = __uint_as_float((uint32_t)(W.key[owner] >> 32));
-                cur = thief ? vref : cur;
-                best = thief ? fminf(best, kb) : best;
-                sp = thief ? 0 : sp;
-                has = has || thief;
-                // the victim drops the child its thief took: the entry shrinks, or is gone
-                const uint32_t mine = wstack[bot * 64 + lane];
-                const uint32_t rest = rest_of(mine);
-                wstack[(robbed && rest ? bot : cap) * 64 + lane] = rest;
-                bot = thief ? 0 : bot + (robbed && !rest ? 1 : 0);
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-        {  // pop the newest entry's next child (the entry stays while children remain)
-            const bool pop = !has && sp > bot;
-            if (__ballot(pop) != 0) {
-                const uint32_t e = wstack[(pop ? sp - 1 : 0) * 64 + lane];
-                const uint32_t r = next_ref(pop ? e : e_safe);
-                const uint32_t rest = rest_of(e);
-                const float kb = __uint_as_float((uint32_t)(W.key[owner] >> 32));
-                wstack[(pop && rest ? sp - 1 : cap) * 64 + lane] = rest;
-                cur = pop ? r : cur;
-                best = pop ? fminf(best, kb) : best;
-                sp -= pop && !rest ? 1 : 0;
-                has = has || pop;
-            }
-            const bool empty = !has && sp == bot;
-            sp = empty ? 0 : sp;
-            bot = empty ? 0 : bot;
-        }
-        if (has && !(cur & kLeafRef)) {
-            const float4* q = reinterpret_cast<const float4*>(nodes + 4 * (size_t)cur);
-            const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
-            const uint4 rf = reinterpret_cast<const uint4*>(q)[6];
-            cnt.node_visits += 4;
-            const float bound = best * 1.00001f + 1e-30f;
-            // entry distance of each child with its slot in the two low bits (+inf: missed; an empty
-            // slot, lo = hi = +inf, never yields a finite entry)
-            auto key = [&](float x0, float y0, float z0, float x1, float y1, float z1, uint32_t slot) {
-                const float tx0 = (x0 - ro.x) * ri.x, tx1 = (x1 - ro.x) * ri.x;
-                const float ty0 = (y0 - ro.y) * ri.y, ty1 = (y1 - ro.y) * ri.y;
-                const float tz0 = (z0 - ro.z) * ri.z, tz1 = (z1 - ro.z) * ri.z;
-                const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-                const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-                const uint32_t kb = tn <= fminf(tf, bound) ? __float_as_uint(tn) : kKeyInf;
-                return (kb & ~3u) | slot;
-            };
-            uint32_t k0 = key(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, 0u);
-            uint32_t k1 = key(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, 1u);
-            uint32_t k2 = key(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, 2u);
-            uint32_t k3 = key(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, 3u);
-            // sorting network (0,1) (2,3) (0,2) (1,3) (1,2): ascending entry distance, then slot
-            auto cx = [](uint32_t& a, uint32_t& b) {
-                const uint32_t lo = a < b ? a : b;
-                b = a < b ? b : a;
-                a = lo;
-            };
-            cx(k0, k1);
-            cx(k2, k3);
-            cx(k0, k2);
-            cx(k1, k3);
-            cx(k1, k2);
-            const uint32_t nh = (uint32_t)(k0 < kKeyInf) + (uint32_t)(k1 < kKeyInf) + (uint32_t)(k2 < kKeyInf) +
-                                (uint32_t)(k3 < kKeyInf);
-            const uint32_t s0 = k0 & 3u;
-            const uint32_t r01 = (s0 & 1u) ? rf.y : rf.x, r23 = (s0 & 1u) ? rf.w : rf.z;
-            const uint32_t near = (s0 & 2u) ? r23 : r01;
-            const uint32_t entry = cur | (((k1 & 3u) | ((k2 & 3u) << 2) | ((k3 & 3u) << 4)) << kWideNodeBits) |
-                                   ((nh - 1u) << 29);
-            const bool more = nh >= 2u;
-            const bool ovf = more && sp + 1 > cap;
-            if (__builtin_expect(__ballot(ovf) != 0, 0))
-                if (ovf) cnt.overflow();
-            const bool push = more && !ovf;
-            wstack[(push ? sp : cap) * 64 + lane] = entry;
-            sp = ovf ? 0 : sp + (push ? 1 : 0);
-            bot = ovf ? 0 : bot;
-            cur = near;
-            has = nh > 0u && !ovf;
-        }
-        uint32_t lk = 0, ln = 0;
-        {
-            const bool leaf = has && (cur & kLeafRef);
-            const uint32_t nt = ((cur >> 27) & 15u) + 1u;
-            lk = cur & 0x07FFFFFFu;
-            ln = leaf ? (nt < 3u ? nt : 3u) : 0u;
-            cur = leaf && nt > 3u ? (kLeafRef | ((nt - 4u) << 27) | (lk + 3u)) : cur;
-            has = has && !(leaf && nt <= 3u);
-            cnt.tri_tests += ln;
-        }
-        const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
-        if (b1) {
-            const uint32_t at = qtail + (uint32_t)(lane_rank(b1) + lane_rank(b2) + lane_rank(b3));
-            const uint32_t tag = (uint32_t)owner;
-            for (uint32_t j = 0; j < ln; ++j) W.slot[(at + j) & (kQ - 1)] = ((lk + j) << 6) | tag;
-            qtail += (uint32_t)(__popcll(b1) + __popcll(b2) + __popcll(b3));
-            __builtin_amdgcn_wave_barrier();
-            if (qtail - qdone >= 64u) {
-                do {
-                    batch(64u);
-                } while (qtail - qdone >= 64u);
-                if (has || sp > bot) best = fminf(best, __uint_as_float((uint32_t)(W.key[owner] >> 32)));
-            }
-        }
-    }
-    if (qtail > qdone) batch(qtail - qdone);
-    __builtin_amdgcn_wave_barrier();
-    if (want) {
-        const unsigned long long key = W.key[lane];
-        if (key != ~0ull) {
-            const uint32_t k = tri_orig[2 * (base + (uint32_t)(key & 0xFFFFFFFFu)) + 1];
-            h.merge(__uint_as_float((uint32_t)(key >> 32)), order, false, obj, (int32_t)k);
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-}
-#endif
 
 // One object record (64 B) as a single wave-uniform scalar load; the same
 // helper serves per-lane loads of sphere-group members.
@@ -843,7 +601,7 @@ __device__ __forceinline__ ObjRec load_obj(const ObjRec* __restrict__ objs, int 
 // consecutive meshes are consecutive in `tris` (their bases rise with scan order), so
 // the per-lane minimum of (t, global triangle index) over the run is the candidate the
 // sequential hit() keeps: smallest t, then the earliest mesh, then its lowest triangle.
-// `skip`: the object index of a convex mesh the lane's ray starts on and leaves (render_kernel, RT_MESH_SELF;
+// `skip`: the object index of a convex mesh the lane's ray starts on and leaves (render_kernel, the convex-shell skip;
 // -1: none): its triangles cannot accept the ray (rt_scene.cpp convex_shell), so the lane takes no ray slot
 // for it. The event counters still count the reference's AABB passes and triangle tests.
 // kLin (the linear-scan kernels): the branch-free cull loop and 1 / det through tri_rcp. In the BVH kernels
@@ -873,7 +631,7 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
     const uint32_t total = nslot * m;
     const float t0 = h.t;
     uint32_t queued = 0, tested = 0;  // wave-uniform ring positions (phase 1: cull, phase 2: full test)
-    constexpr bool kSel = kLin && RT_RUN_SEL;
+    constexpr bool kSel = kLin;
     // the pair's ray slot r = p / m as a multiply-high (kSel: magic = 0 for m = 1, where r = p; no branch)
     const uint32_t onem = m == 1u ? 0xFFFFFFFFu : 0u;  // wave-uniform
     auto slot_of = [&](uint32_t p) { return kSel ? (__umulhi(p, magic) | (p & onem)) : m > 1u ? __umulhi(p, magic) : p; };
@@ -963,19 +721,13 @@ __device__ __forceinline__ float sphere_candidate(const ObjRec& ob, v3 o, v3 d, 
 // (t, ~order) over the accepted members (t <= the ray's closestSoFar) is all the group adds
 // to the ray's Hit: merging that one candidate gives what merging every member would. The
 // lane whose pair set the final minimum records the member (orders are unique) in W.src.
-#ifndef RT_GROUP_RESUME
-#define RT_GROUP_RESUME 1  // sphere groups: leave the traversal to its last few lanes, resume next trip (0: A/B)
-#endif
 #ifndef RT_GROUP_MIN_TRIPS
 #define RT_GROUP_MIN_TRIPS 4   // traversal trips before the wave may leave it
-#endif
-#ifndef RT_GROUP_SEL
-#define RT_GROUP_SEL 1  // the sphere-group trip's pop, push and leaf steps as lane selects (0: branches; A/B)
 #endif
 #ifndef RT_GROUP_EXIT_LANES
 #define RT_GROUP_EXIT_LANES 8  // the wave leaves once at most this many lanes still traverse
 #endif
-// kResume (the sphere-group-only kernel, RT_GROUP_RESUME): once at most RT_GROUP_EXIT_LANES lanes of
+// kResume (the sphere-group-only kernel): once at most RT_GROUP_EXIT_LANES lanes of
 // the wave are still traversing (after RT_GROUP_MIN_TRIPS trips), the wave stops: it tests the pairs it
 // has queued, and the unfinished lanes keep their state in `gl` and skip shading. In the next loop trip
 // they resume, while the lanes that finished shade and start their next segments, which then traverse
@@ -1032,7 +784,6 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
         if (bm == 0) break;
         if (kResume && trip >= RT_GROUP_MIN_TRIPS && __popcll(bm) <= RT_GROUP_EXIT_LANES) break;
         RT_TRIP_COUNT(has || sp > 0);
-#if RT_GROUP_SEL
         {  // pop as lane selects (the read of slot 0 by lanes that do not pop is discarded)
             const bool pop = !has && sp > 0;
             const uint32_t v = wstack[(pop ? sp - 1 : 0) * 64 + lane];
@@ -1066,47 +817,6 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
             cur = leaf && nt > 3u ? (kLeafRef | ((nt - 4u) << 27) | (lk + 3u)) : cur;
             has = has && !(leaf && nt <= 3u);
         }
-#else
-        RT_TRIP_COUNT(has || sp > 0);
-        if (!has && sp > 0) {
-            cur = wstack[(--sp) * 64 + lane];
-            has = true;
-        }
-        if (has && !(cur & kLeafRef)) {
-            const BvhNode nl = nodes[2 * (size_t)cur], nr = nodes[2 * (size_t)cur + 1];
-            cnt.node_visits += 2;
-            float tl, tr;
-            const bool hl = node_hit(nl, o, inv, best, tl);
-            const bool hr = node_hit(nr, o, inv, best, tr);
-            if (hl && hr) {
-                if (sp + 1 > cap) {
-                    cnt.overflow();
-                    has = false;
-                    sp = 0;
-                } else {
-                    const bool left_first = tl <= tr;
-                    wstack[(sp++) * 64 + lane] = left_first ? nr.a : nl.a;
-                    cur = left_first ? nl.a : nr.a;
-                }
-            } else if (hl) {
-                cur = nl.a;
-            } else if (hr) {
-                cur = nr.a;
-            } else {
-                has = false;
-            }
-        }
-        uint32_t lk = 0, ln = 0;
-        if (has && (cur & kLeafRef)) {
-            const uint32_t nt = ((cur >> 27) & 15u) + 1u;
-            lk = cur & 0x07FFFFFFu;
-            ln = nt < 3u ? nt : 3u;
-            if (nt > 3u)
-                cur = kLeafRef | ((nt - 4u) << 27) | (lk + 3u);
-            else
-                has = false;
-        }
-#endif
         const uint64_t b1 = __ballot(ln >= 1u), b2 = __ballot(ln >= 2u), b3 = __ballot(ln >= 3u);
         if (b1) {
             const uint32_t at = qtail + (uint32_t)(lane_rank(b1) + lane_rank(b2) + lane_rank(b3));
@@ -1219,12 +929,6 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
 // each updating the Hit state). Both were measured slower on the other scenes.
 // kParts (BVH kernels): 1 = the scene has BVH meshes, 2 = sphere groups; the other traversal is
 // not compiled in (rt_capi.cpp picks the variant from the committed scene).
-#ifndef RT_PLANE_AXIAL
-#define RT_PLANE_AXIAL 1  // 0: every plane through the general dot products (A/B)
-#endif
-#ifndef RT_PLANE_MIN
-#define RT_PLANE_MIN 1  // axial planes: the six conditions as one float minimum (0: compares and ANDs; A/B)
-#endif
 template <int K>
 __device__ __forceinline__ float axis(v3 v) {
     return K == 0 ? v.x : K == 1 ? v.y : v.z;
@@ -1246,7 +950,6 @@ __device__ __forceinline__ float plane_axial(const ObjRec& ob, v3 o, v3 d) {
     // max(|den| * 1, den) = |den|; max(|den| * 0, den) > tMin iff den > tMin (+0 or NaN against den,
     // and fmaxf returns den for a NaN first operand); a NaN den fails both. No scalar select.
     const float num = (f[K] - axis<K>(o)) * nk;
-#if RT_PLANE_MIN
     // t matters only where proceed holds (then |den| > tMin): a wave with any |num| or |den| >= 2^100
     // takes the IEEE division (closest_hit's general plane argues the domain)
     float t = div_y(num, den, rcp_nr(den));
@@ -1264,20 +967,6 @@ __device__ __forceinline__ float plane_axial(const ObjRec& ob, v3 o, v3 d) {
     const float m = fminf(fminf(fminf(pa - f[6], f[7] - pa), fminf(pb - f[8], f[9] - pb)),
                           fminf(p1, t - 0x1.0624dcp-10f /* the float below kTMin */));
     return m > 0.0f ? t : __builtin_nanf("");
-#else
-    const bool proceed = fmaxf(fabsf(den) * __uint_as_float(ob.u1), den) > kTMin;
-#if RT_DIV_NR
-    float t = div_y(num, den, rcp_nr(den));  // domain and fallback: closest_hit's general plane
-    if (__builtin_expect(__ballot(proceed && !(fmaxf(fabsf(num), fabsf(den)) < 0x1p100f)) != 0, 0))
-        t = fdiv(num, den);
-#else
-    const float t = fdiv(num, den);
-#endif
-    const float pa = axis<A>(o) + axis<A>(d) * t;
-    const float pb = axis<B>(o) + axis<B>(d) * t;
-    const bool in = (pa > f[6]) & (pa < f[7]) & (pb > f[8]) & (pb < f[9]);
-    return (proceed & (t >= kTMin) & in) ? t : __builtin_nanf("");
-#endif
 }
 
 template <bool kBvh, bool kMed = false, bool kSph = true, int kParts = 3>
@@ -1311,11 +1000,11 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
         // wave-uniform dispatch on the record type; the reference's scenes are mostly axial planes
         const uint32_t ty = ob.type;
         auto is = [&](uint32_t k) { return ty == k; };
-        if (RT_PLANE_AXIAL && is(kObjPlaneAxial + 2)) {
+        if (is(kObjPlaneAxial + 2)) {
             cand(plane_axial<1, 0, 2>(ob, o, d), false);  // XZ
-        } else if (RT_PLANE_AXIAL && is(kObjPlaneAxial + 1)) {
+        } else if (is(kObjPlaneAxial + 1)) {
             cand(plane_axial<0, 1, 2>(ob, o, d), false);  // YZ
-        } else if (RT_PLANE_AXIAL && is(kObjPlaneAxial)) {
+        } else if (is(kObjPlaneAxial)) {
             cand(plane_axial<2, 0, 1>(ob, o, d), false);  // XY
         } else if (is_plane(ob.type)) {
             // Plane::hit (Plane.cu:4-52); t is only used when `proceed` holds.
@@ -1323,7 +1012,6 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             const float den = dot(nrm, d);
             const bool proceed = ob.u1 ? (fabsf(den) > kTMin) : (den > kTMin);
             const float num = dot(sub(v3{f[0], f[1], f[2]}, o), nrm);
-#if RT_DIV_NR
             // t matters only where `proceed` holds, i.e. |den| > tMin, and then only through
             // t >= tMin and the comparisons after it. Markstein's quotient is exact for |num|, |den| in
             // [2^-100, 2^100) and |t| >= 2^-121; a smaller |num| or |t| is below tMin either way. A
@@ -1332,9 +1020,6 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
             float t = div_y(num, den, rcp_nr(den));
             if (__builtin_expect(__ballot(proceed && !(fmaxf(fabsf(num), fabsf(den)) < 0x1p100f)) != 0, 0))
                 t = fdiv(num, den);
-#else
-            const float t = fdiv(num, den);
-#endif
             // the hit point's two in-plane coordinates (ray.at(t) per component), tested
             // against the bounds rt_scene.cpp precomputed with Plane::hit's float ops
             float pa, pb;
@@ -1380,20 +1065,15 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                         return;  // (this object's visit: the rest of the scan goes on)
                     }
                 }
-#if RT_MESH_WIDE
-                mesh_bvh_wide(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0, want, o, d, inv, h, i,
-                              ob.order, stack - lane, W, lane, cnt, S.stack_cap);
-#else
                 mesh_bvh_pairs(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0, want, o, d, inv, h, i,
                                ob.order, stack - lane, W, lane, cnt, S.stack_cap RT_TM_ARG);
-#endif
             }
         } else if ((kMed || (kBvh && kSph)) && ob.type == kObjMedium) {
             // (the general linear-scan kernel never sees a medium: launch_render sends scenes with
             // media to the kMed variant, so its register allocation need not cover this test)
             cand(live ? medium_candidate(ob, o, d, rng) : __builtin_nanf(""), false);
         } else if (kBvh && (kParts & 2) != 0) {  // kObjSphereGroup
-            sphere_group_batched<kBvh && kParts == 2 && RT_GROUP_RESUME>(S.objs, S.nodes, __float_as_uint(ob.f[8]), live,
+            sphere_group_batched<kBvh && kParts == 2>(S.objs, S.nodes, __float_as_uint(ob.f[8]), live,
                                                                          ray, inv, inva, h, stack - lane, W, lane, cnt,
                                                                          S.stack_cap, gl RT_TM_ARG);
         }
@@ -1439,15 +1119,10 @@ __device__ __forceinline__ Ray camera_sample(const CamRec* camp, const RenderLau
     rng.begin(L.seed, pixel, L.sample_offset + (uint32_t)s);
     const float rx = rng.next();
     const float ry = rng.next();
-#if RT_DIV_NR
     // (px + rx) / (W - 1): the numerator is in [2^-33, 2^31] (rx is a u01 draw), the divisor an
     // integer in [1, 2^31], so the quotient is >= 2^-64: Markstein's domain, exact without a guard
     const float dx = div_y((float)px + rx, fw, rcp_nr(fw));
     const float dy = div_y((float)y + ry, fh, rcp_nr(fh));
-#else
-    const float dx = fdiv((float)px + rx, fw);
-    const float dy = fdiv((float)y + ry, fh);
-#endif
     const v3 disk = random_in_unit_disk(rng);
     const v3 rnd = scale(disk, cam.lens_radius);
     const v3 offset = add(scale(cam.right, rnd.x), scale(cam.true_up, rnd.y));
@@ -1465,7 +1140,6 @@ __device__ __forceinline__ Ray camera_sample(const CamRec* camp, const RenderLau
 // (zero, subnormal, huge, inf or NaN: practically never, for normalized directions) takes the IEEE
 // division for its lanes. Called by all lanes of the wave (wave-uniform branch).
 __device__ __forceinline__ v3 rcp_exact(v3 d) {
-#if RT_RCP_NR
     v3 r{rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z)};
     const float lo = fminf(fminf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
     const float hi = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
@@ -1474,9 +1148,6 @@ __device__ __forceinline__ v3 rcp_exact(v3 d) {
     if (__builtin_expect(__ballot(!ok || nan) != 0, 0))
         if (!ok || nan) r = rcp(d);
     return r;
-#else
-    return rcp(d);
-#endif
 }
 
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
@@ -1518,9 +1189,6 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #endif
 #ifndef RT_PT_WAVES
 #define RT_PT_WAVES 6
-#endif
-#ifndef RT_PT_BATCH_SEL
-#define RT_PT_BATCH_SEL 1  // pathTrace's batched Kuchkuda test as lane selects (0: nested branches; A/B)
 #endif
 #ifdef RT_WAVES_PER_EU
 #undef RT_BVH_WAVES
@@ -1693,9 +1361,6 @@ __global__ __launch_bounds__(256) void combine_kernel(RenderLaunch L, float* __r
     write_pixel(L, out, ((size_t)lrow * (size_t)L.cols + (size_t)(px - L.col0)) * 3, acc, (float)L.spp);
 }
 
-#ifndef RT_DEPTH_LDS
-#define RT_DEPTH_LDS 1  // linear-scan kernels: the path depth in the camera slot (0: a VGPR; A/B)
-#endif
 #ifndef RT_CAM_BATCH
 #define RT_CAM_BATCH 32  // lanes lacking a prepared next sample that start a camera pass on their own
 #endif
@@ -1841,7 +1506,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
     // camera slots: the linear-scan kernels only (the traversal kernels' LDS holds their stacks)
     constexpr bool kCamPf = !kBvh;
     // resumable sphere-group traversal (the sphere-group-only kernel)
-    constexpr bool kResume = kBvh && kParts == 2 && RT_GROUP_RESUME;
+    constexpr bool kResume = kBvh && kParts == 2;
     constexpr bool kDef = kMeshDefer<kBvh, kParts>();  // deferrable mesh traversal (W.grp_s bits 0-1)
     __shared__ GroupLds glds[kResume ? kBW : 1];
     __shared__ CamSlots cslots[kCamPf ? kBW : 1];
@@ -1963,15 +1628,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                                                  (float)(L.height - 1));
                     C.a[lane] = float4{cr.o.x, cr.o.y, cr.o.z, cr.d.x};
                     C.b[lane] = float4{cr.d.y, cr.d.z, cr.time, __uint_as_float(r2.s0)};
-#if RT_DEPTH_LDS
                     // (.w holds the lane's path depth, which a tracing lane still needs)
                     uint32_t* cw = reinterpret_cast<uint32_t*>(&C.c[lane]);
                     cw[0] = r2.s1;
                     cw[1] = r2.s2;
                     cw[2] = r2.s3;
-#else
-                    C.c[lane] = uint4{r2.s1, r2.s2, r2.s3, 0u};
-#endif
                     item |= kPrepared;
                 }
             }
@@ -1985,9 +1646,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                 need_cam = false;
                 thr = v3{1.0f, 1.0f, 1.0f};
                 depth = 0;
-#if RT_DEPTH_LDS
                 reinterpret_cast<uint32_t*>(&C.c[lane])[3] = fresh_u32(0u);
-#endif
                 if (L.max_depth <= 0)  // rayColor with BOUNCES = 0 returns black
                     sample_done(L, v3{0.0f, 0.0f, 0.0f}, SP, item, own_end, s, sum, thr, alive, need_cam,
                                 towner, held, waiting, tl_pack);
@@ -2018,10 +1677,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
 #endif
 
         const v3 inv = rcp_exact(ray.d);
-        // RT_MESH_SELF: the convex mesh this segment starts on and leaves (shading below), kept beside the
+        // convex-shell skip: the convex mesh this segment starts on and leaves (shading below), kept beside the
         // path depth in the camera slot's spare word: bits 20-31 = its object index + 1
         int skip = -1;
-        if constexpr (kCamPf && RT_MESH_SELF && RT_DEPTH_LDS)
+        if constexpr (kCamPf)
             skip = (int)(reinterpret_cast<const uint32_t*>(&cslots[wave].c[lane])[3] >> 20) - 1;
         const Hit h = closest_hit<kBvh, kMed, kSph, kParts>(S, ray, inv, live, rng, W, stack, lane, cnt, skip,
                                                             kResume ? &glds[wave] : nullptr
@@ -2076,7 +1735,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             if (m.type == 0u || (kSph && (m.type == 1u || m.type == 4u))) rp = random_in_unit_sphere(rng);
             if (m.type == 0u) {
                 // Lambertian::scatter (Material.cu:3-19).
-#if RT_DIV_NR
                 // normalize(rp) of a randomInUnitSphere draw: each component is 2u - 1 of a u01 draw, so
                 // +0 or at least 2^-24 in magnitude, and |rp| < 1: inside Markstein's domain (a +0
                 // component gives +0, as the IEEE division does) unless rp = 0 (all three draws 1/2,
@@ -2086,13 +1744,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                 v3 u{div_y(rp.x, nrp, yrp), div_y(rp.y, nrp, yrp), div_y(rp.z, nrp, yrp)};
                 if (__builtin_expect(__ballot(!(nrp > 0.0f)) != 0, 0))
                     if (!(nrp > 0.0f)) u = normalize(rp);
-#else
-                v3 u = normalize(rp);
-#endif
                 v3 sd = add(n, u);
                 const bool degen = (fabsf(sd.x) < 1e-8f) && (fabsf(sd.y) < 1e-8f) && (fabsf(sd.z) < 1e-8f);
                 if (degen) sd = n;
-#if RT_DIV_NR && RT_SCATTER_NR
                 {
                     // normalize(sd) by Markstein quotients. Outside the degenerate case |sd| >= 1e-8 (and <= 2), so
                     // the norm is in the domain; a component is in it when it is +0 (sd = n + u is never -0: u has
@@ -2111,9 +1765,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                     if (__builtin_expect(__ballot(ieee) != 0, 0))
                         if (ieee) nd = normalize(sd);
                 }
-#else
-                nd = normalize(sd);
-#endif
                 att = v3{m.a0, m.a1, m.a2};
                 scattered = true;
             } else if (kSph && m.type == 1u) {
@@ -2152,13 +1803,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                 scattered = false;
                 nd = ray.d;
             }
-            // RT_MESH_SELF: a ray that leaves a convex brute-force mesh (rt_scene.cpp convex_shell) outward from a
+            // convex-shell skip: a ray that leaves a convex brute-force mesh (rt_scene.cpp convex_shell) outward from a
             // point well inside a face cannot be accepted by any of its triangles: the next segment
             // skips that mesh. Margins: the hit at least 1e-3 (barycentric) inside its triangle's three edges,
             // the new direction at least 1e-3 (cosine) off the face's plane. Only a skip is decided here; the
             // triangles of every other object are tested as before.
             uint32_t self_bits = 0u;
-#if RT_MESH_SELF && RT_DEPTH_LDS
             if constexpr (kCamPf) {
                 const bool cand = scattered && h.tri >= 0 && h.obj < 4094 && ob.type == kObjMesh &&
                                   (__float_as_uint(f[9]) & 1u) != 0u;
@@ -2174,11 +1824,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                     self_bits = ok ? (uint32_t)h.obj + 1u : 0u;
                 }
             }
-#endif
             if (scattered) {
                 thr = mul(thr, att);
                 ray = Ray{p, nd, ray.time};
-#if RT_DEPTH_LDS
                 if constexpr (kCamPf) {
                     // the linear-scan kernels keep the path depth in the camera slot's spare word (LDS)
                     // instead of a VGPR of the persistent loop (at 7 waves/SIMD the CB1 kernel spilled it)
@@ -2187,7 +1835,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                     *dw = dn | (self_bits << 20);
                     done = (int)dn >= L.max_depth;
                 } else
-#endif
                 {
                     ++depth;
                     done = depth >= L.max_depth;
@@ -2469,7 +2116,6 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
         const v3 po{lane_read(ray.o.x, own), lane_read(ray.o.y, own), lane_read(ray.o.z, own)};
         const v3 pd{lane_read(ray.d.x, own), lane_read(ray.d.y, own), lane_read(ray.d.z, own)};
         const int pav = lane_read(avoid_in, own);
-#if RT_PT_BATCH_SEL
         {
             // the Kuchkuda test for list position i (CUDAPathTracer.cu:258-345) as lane selects: lanes past
             // `count` test list position 0 (valid) and every test is evaluated, so no divergent branches
@@ -2494,9 +2140,6 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
             atomicMin(&keys[own], ok ? key : ~0ull);
         }
         if (false) {
-#else
-        if (act) {
-#endif
             // the Kuchkuda test for list position i (CUDAPathTracer.cu:258-345)
             const int idx = tri_list[i];
             if (pav != idx) {
@@ -2958,6 +2601,8 @@ int queue_blocks(int n_cu, uint32_t variant, const RenderLaunch& L) {
             break;
         default:
             lds = (size_t)bw * sizeof(WaveLds) + stack_bytes(L, bw, kStackSpare);
+            // the sphere-group-only kernel also keeps its resumed traversals' state
+            if (variant == RT_VARIANT_BVH_GROUP_QUEUE) lds += (size_t)bw * sizeof(GroupLds);
     }
     const int fit = (int)((size_t)160 * 1024 / (lds ? lds : 1));
     return n_cu * std::max(1, std::min(4 * waves / bw, fit));
@@ -2977,7 +2622,10 @@ uint32_t select_variant(bool pathtrace, bool queue, bool bvh, bool media, bool f
     if (bvh && bvh_parts == 1 && !full && !media)
         return RT_VARIANT_BVH_MESH_SIMPLE_QUEUE;
     if (bvh && bvh_parts == 1) return RT_VARIANT_BVH_MESH_QUEUE;
-    if (bvh && bvh_parts == 2) return RT_VARIANT_BVH_GROUP_QUEUE;
+    // the sphere-group-only kernel resumes a traversal in the next loop trip, re-scanning the objects
+    // before the group: a medium there would draw again from the ray's stream, so scenes
+    // with media take the general BVH kernel, which traverses each group in one pass
+    if (bvh && bvh_parts == 2 && !media) return RT_VARIANT_BVH_GROUP_QUEUE;
     if (bvh) return RT_VARIANT_BVH_QUEUE;
     if (media) return RT_VARIANT_SCAN_MEDIA_QUEUE;
     if (!full) return RT_VARIANT_SCAN_SIMPLE_QUEUE;
@@ -3024,19 +2672,19 @@ const char* variant_name(uint32_t v) {
 // the shared EXTRA flags, the whole library) was compiled with.
 uint32_t kernel_build_flags() {
     uint32_t f = 0;
-#if defined(RT_ABL_FASTMATH) || defined(RT_ABL_NOREJECT) || defined(RT_ABL_FLOATLOG) || RT_ABL_PHILOX_ROUNDS != 10
+#if defined(RT_ABL_FASTMATH) || defined(RT_ABL_NOREJECT) || defined(RT_ABL_FLOATLOG) || RT_ABL_PHILOX_ROUNDS != 10 || \
+    defined(RT_XOSHIRO_SS)
     f |= 1u;  // RT_BUILD_ABLATION: results differ from the restatement
 #endif
 #ifdef RT_STAMPS
     f |= 2u;  // RT_BUILD_STAMPS
 #endif
-#if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || \
-    RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || RT_BVH_MESH_WAVES != 5 || \
-    RT_PT_WAVES != 6 || defined(RT_U01_MULADD) || RT_CAM_BATCH != 32 || RT_RCP_NR != 1 || RT_DIV_NR != 1 || \
-    RT_QUEUE_BLOCK_WAVES != 4 || RT_PLANE_AXIAL != 1 || RT_LANE_READ != 1 || RT_DEPTH_LDS != 1 || RT_MESH_WIDE != 0 || RT_PLANE_MIN != 1 || RT_PT_BATCH_SEL != 1 || RT_MESH_SELF != 1 || RT_GROUP_RESUME != 1 || \
-    RT_GROUP_MIN_TRIPS != 4 || RT_GROUP_EXIT_LANES != 8 || RT_TRI_MIN != 1 || RT_RUN_SEL != 1 || RT_TRI_RCP != 1 || RT_BATCH_MIN != 64 || RT_GROUP_BATCH_MIN != 64 || \
-    RT_PT_BATCH_MIN != 64 || RT_GROUP_SEL != 1 || RT_SCATTER_NR != 1 || RT_MESH_DEFER != 1 || \
-    RT_DEFER_MIN != 32
+// the remaining knobs: occupancies, the queue's schedule and the numeric thresholds
+#if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || RT_QUEUE_BLOCK_WAVES != 4 || RT_CAM_BATCH != 32 || \
+    defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || \
+    RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || RT_BVH_MESH_WAVES != 5 || RT_PT_WAVES != 6 || \
+    RT_GROUP_MIN_TRIPS != 4 || RT_GROUP_EXIT_LANES != 8 || RT_BATCH_MIN != 64 || RT_GROUP_BATCH_MIN != 64 || \
+    RT_PT_BATCH_MIN != 64 || RT_DEFER_MIN != 32 || defined(RT_U01_MULADD)
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
 #endif
 #if (defined(RT_FIF_ITEMS) && RT_FIF_ITEMS != 16) || (defined(RT_FIF_GROUPS) && RT_FIF_GROUPS != 1)

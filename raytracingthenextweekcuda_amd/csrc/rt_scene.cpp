@@ -32,7 +32,7 @@ inline v3 rotate_y(v3 v, float r) {
 }  // namespace
 
 // A brute-force mesh the kernels may skip for rays that start on its own surface (rt_kernel.hip
-// mesh_run, RT_MESH_SELF): a convex polyhedral shell whose face planes meet at angles of at least
+// mesh_run, the convex-shell skip): a convex polyhedral shell whose face planes meet at angles of at least
 // 30 degrees and whose parallel faces are apart. A ray that leaves such a mesh outward from a point
 // well inside a face (closest_hit's caller checks both, with margins) stays outside every face
 // plane it could cross from the front, so TriangleMesh::hit (TriangleMesh.cu:34-117, which culls
@@ -464,7 +464,7 @@ std::string HostScene::flatten() {
                 tri_orig[pair0 + 2 * (size_t)order[t] + 1] = r.u0 + (uint32_t)t;
             }
             // f[9] (brute-force meshes): 1 = a convex shell the kernels skip for rays leaving its surface
-            const uint32_t convex = nt <= kBvhMinTris && RT_MESH_SELF && convex_shell(&tris[r.u0], nt) ? 1u : 0u;
+            const uint32_t convex = nt <= kBvhMinTris && convex_shell(&tris[r.u0], nt) ? 1u : 0u;
             memcpy(&r.f[9], &convex, 4);
         }
         objs.push_back(r);
@@ -538,95 +538,7 @@ struct PairBuilder {
         return q;
     }
 };
-// 4-wide nodes of one mesh BVH (see HostScene::build_mesh_pairs): each wide node takes its binary
-// node's two children and, while it has fewer than four, replaces the child of largest surface area
-// that is an inner node (or a leaf of more than kLeafRefMax triangles, split in halves under its own
-// box) by that child's two children. Children keep the binary tree's (inflated) boxes, so any
-// traversal's candidate set is the binary tree's. The traversal (rt_kernel.hip mesh_bvh_wide) keeps
-// ONE stack entry per wide node with children left to visit (the node and their slots, nearest
-// first), so a lane holds at most one entry per wide level above it: max_push, the max over
-// root-to-leaf paths of the wide nodes with two or more children, sizes the LDS stacks - never more
-// than the binary tree's pair depth.
-struct WideBuilder {
-    std::vector<BvhNode>& nodes;
-    int max_push = 0;
-    bool empty_leaf = false;
-    bool too_many = false;
-    struct Child {
-        BvhNode box;
-        bool inner;
-        uint32_t node, first, count;
-    };
-    static float area(const BvhNode& b) {
-        const float x = b.hi[0] - b.lo[0], y = b.hi[1] - b.lo[1], z = b.hi[2] - b.lo[2];
-        return x * y + y * z + z * x;
-    }
-    Child child_of(uint32_t i) const {
-        const BvhNode n = nodes[i];
-        if (n.b & 0x80000000u) return Child{n, false, i, n.a, n.b & 0x7FFFFFFFu};
-        return Child{n, true, i, 0u, 0u};
-    }
-    static bool expandable(const Child& c) { return c.inner || c.count > kLeafRefMax; }
-    void expand(const Child& c, Child out[2]) const {
-        if (c.inner) {
-            const BvhNode n = nodes[c.node];
-            out[0] = child_of(n.a);
-            out[1] = child_of(n.b);
-        } else {
-            const uint32_t half = c.count / 2u;
-            out[0] = Child{c.box, false, 0u, c.first, half};
-            out[1] = Child{c.box, false, 0u, c.first + half, c.count - half};
-        }
-    }
-    // `above`: stack entries a lane holds when it reaches this child
-    uint32_t ref(const Child& c, int above) {
-        if (!expandable(c)) {
-            empty_leaf |= c.count == 0u;
-            max_push = std::max(max_push, above);
-            return kLeafRef | ((c.count - 1u) << 27) | c.first;
-        }
-        return wide(c, above);
-    }
-    uint32_t wide(const Child& parent, int above) {
-        Child ch[4];
-        int n = 2;
-        expand(parent, ch);
-        while (n < 4) {
-            int best = -1;
-            for (int k = 0; k < n; ++k)
-                if (expandable(ch[k]) && (best < 0 || area(ch[k].box) > area(ch[best].box))) best = k;
-            if (best < 0) break;
-            Child two[2];
-            expand(ch[best], two);
-            for (int k = n; k > best + 1; --k) ch[k] = ch[k - 1];
-            ch[best] = two[0];
-            ch[best + 1] = two[1];
-            ++n;
-        }
-        while (nodes.size() & 3u) nodes.push_back(BvhNode{});
-        const size_t at = nodes.size();
-        if (at / 4 >= ((size_t)1 << kWideNodeBits)) too_many = true;
-        nodes.resize(at + 4, BvhNode{});
-        const uint32_t q = (uint32_t)(at / 4);
-        WideNode w{};
-        for (int k = 0; k < 4; ++k)
-            for (int a = 0; a < 3; ++a) w.lo[a][k] = w.hi[a][k] = __builtin_huge_valf();  // empty slot
-        w.n = (uint32_t)n;
-        for (int k = 0; k < n; ++k) {
-            for (int a = 0; a < 3; ++a) {
-                w.lo[a][k] = ch[k].box.lo[a];
-                w.hi[a][k] = ch[k].box.hi[a];
-            }
-            w.ref[k] = ref(ch[k], above + 1);  // may grow `nodes`: w is written below
-        }
-        memcpy(&nodes[4 * (size_t)q], &w, sizeof w);
-        return q;
-    }
-    uint32_t root(uint32_t i) {
-        const Child c = child_of(i);
-        return expandable(c) ? wide(c, 0) : ref(c, 0);
-    }
-};
+
 }  // namespace
 
 // The batched traversals (rt_kernel.hip mesh_bvh_pairs, sphere_group_batched) read each inner
@@ -653,18 +565,6 @@ std::string HostScene::build_mesh_pairs() {
     for (int k = 0; k < n_scan; ++k) {
         ObjRec& r = objs[k];
         if (!tree(r)) continue;
-        if (RT_MESH_WIDE && r.type == kObjMesh) {
-            WideBuilder wb{nodes};
-            const uint32_t root = wb.root(r.u2);
-            if (wb.empty_leaf) return "BVH with an empty leaf";
-            if (wb.too_many) return "too many wide BVH nodes (2^23)";
-            if (wb.max_push > kBvhStackDepth)
-                return "wide BVH stack bound " + std::to_string(wb.max_push) + " exceeds the traversal stack (" +
-                       std::to_string(kBvhStackDepth) + ")";
-            bvh_max_depth = std::max(bvh_max_depth, wb.max_push);
-            memcpy(&r.f[8], &root, 4);
-            continue;
-        }
         if (nodes.size() & 1u) nodes.push_back(BvhNode{});
         PairBuilder pb{nodes};
         const uint32_t root = pb.node(r.u2, 0);
@@ -676,7 +576,7 @@ std::string HostScene::build_mesh_pairs() {
         memcpy(&r.f[8], &root, 4);
     }
     // f[9] = 2 (as u32 bits): the kernel may defer this mesh's traversal for its few wanting rays to the next
-    // loop trip (rt_kernel.hip RT_MESH_DEFER). A deferred ray scans the list again, so only when no object of
+    // loop trip (rt_kernel.hip kMeshDefer). A deferred ray scans the list again, so only when no object of
     // the scan draws from the ray's stream (a participating medium) or counts its tests per scan (a
     // brute-force mesh), and this is the scan's only mesh (no sphere group either).
     int meshes = 0, others = 0;
@@ -685,7 +585,7 @@ std::string HostScene::build_mesh_pairs() {
         meshes += r.type == kObjMesh;
         others += r.type == kObjMedium || r.type == kObjSphereGroup || (r.type == kObjMesh && !tree(r));
     }
-    if (meshes == 1 && others == 0 && !RT_MESH_WIDE)
+    if (meshes == 1 && others == 0)
         for (int k = 0; k < n_scan; ++k)
             if (objs[k].type == kObjMesh) {
                 const uint32_t defer = 2u;

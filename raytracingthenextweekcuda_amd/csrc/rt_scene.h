@@ -51,8 +51,8 @@ struct alignas(16) ObjRec {
     // mesh: boundsMin xyz, boundsMax xyz (computeMeshAABB, main.cu:261-281), f[6] = the bits of
     //       ceil(2^32 / triangle count) (the brute-force compaction's division), f[7] = mesh-run
     //       length (brute force), f[8] = root child-pair reference (BVH meshes), f[9] = 1 (as u32 bits)
-    //       for a brute-force mesh that is a convex shell (rt_scene.cpp convex_shell, RT_MESH_SELF), 2 for a BVH
-//       mesh whose traversal the kernel may defer to the next loop trip (build_mesh_pairs, RT_MESH_DEFER)
+    //       for a brute-force mesh that is a convex shell (rt_scene.cpp convex_shell), 2 for a BVH
+//       mesh whose traversal the kernel may defer to the next loop trip (build_mesh_pairs, rt_kernel.hip kMeshDefer)
     float f[10];
 };
 constexpr uint32_t kNoBvh = 0xFFFFFFFFu;
@@ -89,29 +89,6 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 32, "BvhNode must be 32 B");
 
-// 4-wide BVH node of the rayColor mesh traversal (rt_kernel.hip mesh_bvh_wide; built by
-// HostScene::build_mesh_pairs from the binary SAH tree, whose adjacent levels it collapses): up to
-// four children's boxes as SoA rows (lo x, lo y, lo z, hi x, hi y, hi z; four floats each), their
-// references (a wide node index, or a leaf reference as in the child-pair records: kLeafRef |
-// (count - 1) << 27 | first) and the child count. One aligned 128 B line = four BvhNode slots of the
-// node table from an index divisible by four. An empty slot has lo = hi = +inf on every axis, which
-// the box test rejects for any ray.
-struct alignas(16) WideNode {
-    float lo[3][4];
-    float hi[3][4];
-    uint32_t ref[4];
-    uint32_t n, pad[3];
-};
-static_assert(sizeof(WideNode) == 128, "WideNode must be 128 B");
-#ifndef RT_MESH_SELF
-#define RT_MESH_SELF 1  // skip convex brute-force meshes for rays leaving their surface (0: A/B)
-#endif
-#ifndef RT_MESH_WIDE
-#define RT_MESH_WIDE 0  // 1: rayColor mesh BVHs as 4-wide nodes (A/B: slower than child pairs)
-#endif
-// A lane's traversal stack entry over wide nodes: the node (bits 0-22) and the children still to
-// visit, nearest first (2-bit child slots at bits 23-24, 25-26, 27-28; their count at bits 29-30).
-constexpr uint32_t kWideNodeBits = 23;
 
 
 struct alignas(16) MatRec {

@@ -29,7 +29,7 @@ def test_digest_covers_host_sources_header_and_flags():
     for f in ("rt_kernel.hip", "rt_kernel.h", "rt_capi.cpp", "rt_scene.cpp", "rt_multi.cpp", "Makefile",
               "include/rtmi.h"):
         assert f in names, f
-    assert source_digest(CSRC, "-DRT_PLANE_AXIAL=0") != source_digest(CSRC)
+    assert source_digest(CSRC, "-DRT_CAM_BATCH=16") != source_digest(CSRC)
 
 
 def _copy_tree(dst):

@@ -298,10 +298,60 @@ def test_gpu_division_edge_parity(lanes):
     assert st["segments"] == ost["segments"]
 
 
+def groups_with_medium_spec(seed):
+    """24 spheres (a sphere group: >= 16 spheres go behind a BVH) beside a participating medium that sits
+    in the scan BEFORE the group, and one more after it. The sphere-group-only kernel resumes an unfinished
+    group traversal in the next loop trip by re-scanning the objects before the group, which would draw the
+    medium's free-flight distance again from the ray's stream: such scenes must run a kernel
+    that traverses each group in one pass, and match the restatement bit for bit."""
+    rng = np.random.RandomState(seed)
+    mats = [("lambertian", 0, (0.8, 0.3, 0.3)), ("metal", 1, (0.9, 0.9, 0.5), 0.3),
+            ("dielectric", 2, 1.5), ("emission", 3, (1.0, 0.9, 0.8), 4.0), ("lambertian", 4, (0.3, 0.6, 0.8)),
+            ("isotropic", 5, (0.7, 0.7, 0.9))]
+    objs = [("plane", 0, (0.0, -0.8, 0.0), (0.0, 1.0, 0.0), (3.0, 3.0, 3.0), 4, 2, True),
+            ("medium", 1, (0.0, 0.0, 0.0), (0.9, 0.6, 0.9), float(rng.uniform(0.8, 3.0)), 5)]
+    slot = 2
+    for k in range(24):
+        objs.append(("sphere", slot, tuple(rng.uniform(-1.0, 1.0, 3)), float(rng.uniform(0.06, 0.22)), k % 5))
+        slot += 1
+    objs.append(("medium", slot, (0.5, 0.4, -0.3), (0.2, 0.2, 0.2), 4.0, 5))
+    cam = ((0.2, 0.4, 2.7), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 1.33, 50.0, 0.0, 2.5, 0.0, 1.0)
+    return {"camera": cam, "materials": mats, "objects": objs}
+
+
+def test_groups_with_medium_spec_builds_on_host():
+    import raytracingthenextweekcuda_amd as rtmi
+
+    r = rtmi.Renderer(-1)
+    build_product(r, groups_with_medium_spec(0))
+    c = r.object_counts()
+    r.close()
+    assert c["bvh_node"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,lanes", [(0, 1), (1, 8)])
+def test_gpu_sphere_groups_with_medium_parity(seed, lanes):
+    import raytracingthenextweekcuda_amd as rtmi
+
+    spec = groups_with_medium_spec(seed)
+    w, h, spp, depth = 48, 36, 16, 8
+    r = rtmi.Renderer(0)
+    build_product(r, spec)
+    got = r.render(w, h, spp, depth, lanes_per_pixel=lanes)
+    st = r.stats()
+    r.close()
+    assert st["variant_name"] == "render_kernel<true, true, false, true, 3>"  # not the resuming group kernel
+    want, ost = build_oracle(spec).render(w, h, spp, depth, lanes_per_pixel=lanes)
+    assert st["overflow"] == 0
+    assert np.array_equal(got, want)
+    assert st["segments"] == ost["segments"]
+
+
 def deep_leaf_spec():
     """One triangle repeated 260 times: the SAH builder keeps them in one leaf, which build_mesh_pairs
     splits into halves under the same box (260 -> 130 -> 65 -> 33 -> 17 -> 9): five levels of pair
-    records (four levels of 4-wide nodes), every child of every node hit by any ray that hits the box.
+    records, every child of every node hit by any ray that hits the box.
     A lane descending it pushes at every level, so its stack reaches exactly the scene's bound
     (rt_scene_bvh_depth) while its non-pushing steps write the spare slot past it (rt_kernel.hip
     kStackSpare)."""
@@ -319,7 +369,7 @@ def test_deep_leaf_spec_depth():
 
     r = rtmi.Renderer(-1)
     build_product(r, deep_leaf_spec())
-    assert r.bvh_depth() in (4, 5)  # 4-wide nodes (RT_MESH_WIDE, the default) or child pairs
+    assert r.bvh_depth() == 5  # child-pair records: 260 -> 130 -> 65 -> 33 -> 17 -> 9 (leaf references of <= 16)
     r.close()
 
 
@@ -336,7 +386,7 @@ def test_gpu_stack_reaches_its_bound(lanes):
     got = r.render(w, h, spp, depth, lanes_per_pixel=lanes)
     st = r.stats()
     r.close()
-    assert bound in (4, 5) and st["stack_depth"] == bound and st["overflow"] == 0
+    assert bound == 5 and st["stack_depth"] == bound and st["overflow"] == 0
     want, ost = build_oracle(spec).render(w, h, spp, depth, lanes_per_pixel=lanes)
     assert np.array_equal(got, want)
     assert st["segments"] == ost["segments"]
