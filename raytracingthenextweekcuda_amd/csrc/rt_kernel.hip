@@ -1247,11 +1247,13 @@ __device__ __forceinline__ void write_pixel(const RenderLaunch& L, float* __rest
     }
 }
 
-// Partial sums are stored sub-stream major, [c][pixel][3], so the combine pass
-// reads them coalesced.
+// Partial sums are stored item-major, [pixel][c][3] (an item's index is pixel << sp_log2 | c): the lanes of a
+// wave that dequeued together hold consecutive items, so their stores land in a few contiguous lines, and
+// a pixel's S slots, written within a few loop trips of each other, fill whole lines in L2 before they are
+// written back (round 5's sub-stream-major [c][pixel][3] spread a wave's 64 stores over 64 lines: WRITE_SIZE
+// 4.1x the partial-sum bytes on the bunny). combine_kernel reads a pixel's S slots in the fixed order.
 __device__ __forceinline__ void store_partial(const RenderLaunch& L, uint32_t item, v3 sum) {
-    const uint32_t S = (uint32_t)L.lanes_per_pixel;
-    float* p = L.partial + ((size_t)(item & (S - 1)) * L.n_pix + (item >> L.sp_log2)) * 3;
+    float* p = L.partial + (size_t)item * 3;
     p[0] = sum.x;
     p[1] = sum.y;
     p[2] = sum.z;
@@ -1351,11 +1353,10 @@ __global__ __launch_bounds__(256) void combine_kernel(RenderLaunch L, float* __r
     const int SP = L.lanes_per_pixel;
     int c, px, lrow;
     if (pl * (uint32_t)SP >= L.n_items || !queue_item(L, pl * (uint32_t)SP, c, px, lrow)) return;
-    const size_t stride = (size_t)L.n_pix * 3;  // one sub-stream plane
-    const float* p = L.partial + (size_t)pl * 3;
+    const float* p = L.partial + (size_t)pl * (size_t)SP * 3;  // the pixel's S slots, item-major
     v3 acc{p[0], p[1], p[2]};
     for (int j = 1; j < SP; ++j) {
-        p += stride;
+        p += 3;
         acc = add(acc, v3{p[0], p[1], p[2]});
     }
     write_pixel(L, out, ((size_t)lrow * (size_t)L.cols + (size_t)(px - L.col0)) * 3, acc, (float)L.spp);

@@ -75,6 +75,14 @@ for sc in ${TRAFFIC:-}; do
     stop_if_fatal $? pmc_${sc}_$c
   done
 done
+for sc in ${TCC:-}; do  # L2 hit / miss (TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)) and fabric read requests
+  timeout -s KILL 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_REQ_sum --output-format csv -d "$O/pmc_tcc_$sc" -o pmc -- python3 bench.py --scene $sc --steps 1 --warmup 1 --no-cpu-baseline --no-overlap $(lay $sc) > "$O/pmc_tcc_$sc.log" 2>&1
+  stop_if_fatal $? pmc_tcc_$sc
+  for alt in ${TCC_ALT:-}; do
+    RTMI_LIB=raytracingthenextweekcuda_amd/$alt timeout -s KILL 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_REQ_sum --output-format csv -d "$O/pmc_tcc_${sc}_${alt%.so}" -o pmc -- python3 bench.py --scene $sc --steps 1 --warmup 1 --no-cpu-baseline --no-overlap $(lay $sc) > "$O/pmc_tcc_${sc}_${alt%.so}.log" 2>&1
+    stop_if_fatal $? pmc_tcc_${sc}_$alt
+  done
+done
 for sc in ${PROF:-}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$sc" -o run --output-format csv -- python3 bench.py --scene $sc --steps ${PROF_STEPS:-10} --warmup ${PROF_WARMUP:-2} --no-cpu-baseline --no-overlap $(lay $sc) > "$O/prof_$sc.log" 2>&1
   stop_if_fatal $? prof_$sc
