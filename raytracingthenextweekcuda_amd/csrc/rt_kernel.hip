@@ -99,6 +99,42 @@ __device__ __forceinline__ bool node_hit(const BvhNode& n, v3 o, v3 inv, float t
     return tn <= fminf(tf, tmax * 1.00001f + 1e-30f);
 }
 
+// The mesh traversal's slab terms on a QPair grid (rt_scene.h): the plane c + q s of axis a is entered at
+// t(q) = fma(q, A_a, B_a) with A = s * inv (exact: s is a power of two) and B = (c - o) * inv, once per ray.
+// |t(q) - (c + q s - o) inv| <= 2^-22 (|B_a| + kQMax |A_a|) for every grid coordinate q <= kQMax (two roundings
+// in B, one in the fma); E is 4x that bound over the axes, and qpair_hit widens the interval by it, so the
+// test accepts every ray whose exact slab interval meets the grid box - which contains the inflated float
+// box of round 5's 64 B pairs. (inv = +-inf makes A, B, E infinite or NaN: that axis then never culls.)
+struct QRay {
+    v3 A, B;
+    float E;
+};
+__device__ __forceinline__ QRay qray(const float4 fr, v3 o, v3 inv) {
+    QRay r;
+    r.A = v3{fr.w * inv.x, fr.w * inv.y, fr.w * inv.z};
+    r.B = v3{(fr.x - o.x) * inv.x, (fr.y - o.y) * inv.y, (fr.z - o.z) * inv.z};
+    const float q = (float)kQMax;
+    const float m = fmaxf(fmaxf(fabsf(r.B.x) + q * fabsf(r.A.x), fabsf(r.B.y) + q * fabsf(r.A.y)),
+                          fabsf(r.B.z) + q * fabsf(r.A.z));
+    r.E = m * 0x1p-20f;  // 2 x (twice the bound): the interval is widened by E at both ends
+    return r;
+}
+// One child box of a QPair (three words: lo.x | lo.y, lo.z | hi.x, hi.y | hi.z): node_hit's test on the
+// grid box with the interval widened by E; `tmaxe` = the pruning bound (with node_hit's slack) + E.
+__device__ __forceinline__ bool qpair_hit(uint32_t w0, uint32_t w1, uint32_t w2, const QRay& r, float tmaxe,
+                                          float& tnear) {
+    const float tx0 = __builtin_fmaf((float)(w0 & 0xFFFFu), r.A.x, r.B.x);
+    const float ty0 = __builtin_fmaf((float)(w0 >> 16), r.A.y, r.B.y);
+    const float tz0 = __builtin_fmaf((float)(w1 & 0xFFFFu), r.A.z, r.B.z);
+    const float tx1 = __builtin_fmaf((float)(w1 >> 16), r.A.x, r.B.x);
+    const float ty1 = __builtin_fmaf((float)(w2 & 0xFFFFu), r.A.y, r.B.y);
+    const float tz1 = __builtin_fmaf((float)(w2 >> 16), r.A.z, r.B.z);
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    tnear = tn;
+    return tn <= fminf(tf + r.E, tmaxe);
+}
+
 // Sphere::hit / MovingSphere::hit root selection (Sphere.cu:3-37, 39-73). `inva` = 1.0f / dot(d, d), the
 // same IEEE quotient for every sphere a ray tests: the caller forms it once per ray (sphere_inva).
 __device__ __forceinline__ float sphere_inva(v3 d) { return fdiv(1.0f, dot(d, d)); }
@@ -428,15 +464,16 @@ __device__ __forceinline__ const RenderLaunch& launch_args() {
 // still contains the sequential scan's winner and the (t, index) minimum picks it.
 __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
                                                const uint32_t* __restrict__ tri_orig,
-                                               const BvhNode* __restrict__ nodes, uint32_t root, uint32_t base,
-                                               bool want, v3 o, v3 d, v3 inv, Hit& h, int32_t obj,
+                                               const BvhNode* __restrict__ nodes, uint32_t root, uint32_t frame,
+                                               uint32_t base, bool want, v3 o, v3 d, v3 inv, Hit& h, int32_t obj,
                                                uint32_t order, uint32_t* wstack, WaveLds& W, int lane,
                                                Counters& cnt, int cap RT_TM_PARAM) {
     const uint64_t wm = __ballot(want);
     if (wm == 0) return;
     key_reset(W.key[lane]);
     int owner = lane;
-    v3 ro = o, ri = inv;
+    // the ray's slab terms on the mesh's QPair grid (the frame is one wave-uniform 16 B load)
+    QRay qr = qray(*reinterpret_cast<const float4*>(nodes + frame), o, inv);
     float best = h.t;  // pruning bound for the current ray (its closestSoFar until a hit lands)
     uint32_t cur = root;  // pair index or leaf reference
     bool has = want;
@@ -484,8 +521,9 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
                 const int v_owner = lane_read(owner, vic);
                 if (thief) owner = v_owner;
             }
-            take(ro.x); take(ro.y); take(ro.z);
-            take(ri.x); take(ri.y); take(ri.z);
+            take(qr.A.x); take(qr.A.y); take(qr.A.z);
+            take(qr.B.x); take(qr.B.y); take(qr.B.z);
+            take(qr.E);
             take(best);
             {
                 const uint32_t vref = wstack[vt * 64 + vic];  // (a valid slot for every lane)
@@ -511,21 +549,22 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             bot = empty ? 0 : bot;
         }
         if (has && !(cur & kLeafRef)) {
-            const BvhNode nl = nodes[2 * (size_t)cur], nr = nodes[2 * (size_t)cur + 1];
+            const QPair pr = *reinterpret_cast<const QPair*>(nodes + cur);  // one 32 B record
             cnt.node_visits += 2;
             float tl, tr;
-            const bool hl = node_hit(nl, ro, ri, best, tl);
-            const bool hr = node_hit(nr, ro, ri, best, tr);
+            const float tmaxe = best * 1.00001f + 1e-30f + qr.E;
+            const bool hl = qpair_hit(pr.q[0], pr.q[1], pr.q[2], qr, tmaxe, tl);
+            const bool hr = qpair_hit(pr.q[3], pr.q[4], pr.q[5], qr, tmaxe, tr);
             // as lane selects; a lane that does not push writes the spare slot `cap` (never read)
             const bool both = hl && hr, lf = tl <= tr;
             const bool ovf = both && sp + 1 > cap;
             if (__builtin_expect(__ballot(ovf) != 0, 0))
                 if (ovf) cnt.overflow();
             const bool push = both && !ovf;
-            wstack[(push ? sp : cap) * 64 + lane] = lf ? nr.a : nl.a;
+            wstack[(push ? sp : cap) * 64 + lane] = lf ? pr.ref[1] : pr.ref[0];
             sp = ovf ? 0 : sp + (push ? 1 : 0);
             bot = ovf ? 0 : bot;
-            cur = both ? (lf ? nl.a : nr.a) : (hl ? nl.a : nr.a);
+            cur = both ? (lf ? pr.ref[0] : pr.ref[1]) : (hl ? pr.ref[0] : pr.ref[1]);
             has = (hl || hr) && !ovf;
         }
         uint32_t lk = 0, ln = 0;  // this trip's leaf pairs: triangles lk .. lk + ln - 1
@@ -1065,7 +1104,8 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                         return;  // (this object's visit: the rest of the scan goes on)
                     }
                 }
-                mesh_bvh_pairs(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), ob.u0, want, o, d, inv, h, i,
+                mesh_bvh_pairs(S.tris, S.tri_orig, S.nodes, __float_as_uint(ob.f[8]), __float_as_uint(ob.f[6]), ob.u0,
+                               want, o, d, inv, h, i,
                                ob.order, stack - lane, W, lane, cnt, S.stack_cap RT_TM_ARG);
             }
         } else if ((kMed || (kBvh && kSph)) && ob.type == kObjMedium) {

@@ -539,6 +539,97 @@ struct PairBuilder {
     }
 };
 
+
+// Quantized child-pair records of one MESH BVH (rt_scene.h QPair; see HostScene::build_mesh_pairs): the
+// PairBuilder tree, one 32 B slot per pair, boxes on the 16-bit grid of the mesh's frame.
+struct QPairBuilder {
+    std::vector<BvhNode>& nodes;
+    float c[3] = {0.0f, 0.0f, 0.0f};
+    double s = 0.0;  // grid step, a power of two
+    int max_pairs = 0;
+    bool empty_leaf = false;
+    bool bad = false;  // a box off the grid (never, by the frame's construction)
+
+    void extent(uint32_t i, float lo[3], float hi[3]) const {
+        const BvhNode n = nodes[i];
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], n.lo[a]);
+            hi[a] = std::max(hi[a], n.hi[a]);
+        }
+        if (!(n.b & 0x80000000u)) {
+            extent(n.a, lo, hi);
+            extent(n.b, lo, hi);
+        }
+    }
+    // The frame: s = the smallest power of two that puts every box of the tree on a grid of kQMax steps
+    // with two spare steps at each end (and at least 2^-40 of the coordinates' magnitude), c = the boxes'
+    // minimum less two steps, rounded down to a float.
+    void frame(uint32_t root) {
+        float lo[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
+        float hi[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
+        extent(root, lo, hi);
+        double ext = 0.0, mag = 0.0;
+        for (int a = 0; a < 3; ++a) {
+            ext = std::max(ext, (double)hi[a] - (double)lo[a]);
+            mag = std::max(mag, std::max(std::fabs((double)lo[a]), std::fabs((double)hi[a])));
+        }
+        s = std::ldexp(1.0, -126);
+        while (s * (kQMax - 8) < ext || s < mag * 0x1p-40) s *= 2.0;
+        for (int a = 0; a < 3; ++a) {
+            const double want = (double)lo[a] - 2.0 * s;
+            float cf = (float)want;
+            if ((double)cf > want) cf = std::nextafter(cf, -__builtin_huge_valf());
+            c[a] = cf;
+        }
+    }
+    // grid coordinates of a box, one more step outward than its floor / ceil
+    void quantize(const BvhNode& b, uint32_t* q) {
+        uint32_t v[6];
+        for (int a = 0; a < 3; ++a) {
+            const double l = std::floor(((double)b.lo[a] - (double)c[a]) / s) - 1.0;
+            const double h = std::ceil(((double)b.hi[a] - (double)c[a]) / s) + 1.0;
+            if (!(l >= 0.0) || !(h <= (double)kQMax)) bad = true;
+            v[a] = (uint32_t)std::max(0.0, std::min(l, (double)kQMax));
+            v[3 + a] = (uint32_t)std::max(0.0, std::min(h, (double)kQMax));
+        }
+        q[0] = v[0] | v[1] << 16;
+        q[1] = v[2] | v[3] << 16;
+        q[2] = v[4] | v[5] << 16;
+    }
+    uint32_t alloc() {
+        nodes.emplace_back();
+        return (uint32_t)(nodes.size() - 1);
+    }
+    void set(uint32_t q, const BvhNode& l, uint32_t ref_l, const BvhNode& r, uint32_t ref_r) {
+        QPair p{};
+        quantize(l, &p.q[0]);
+        quantize(r, &p.q[3]);
+        p.ref[0] = ref_l;
+        p.ref[1] = ref_r;
+        memcpy(&nodes[q], &p, sizeof p);
+    }
+    uint32_t leaf(const BvhNode& box, uint32_t first, uint32_t count, int above) {
+        if (count <= kLeafRefMax) {
+            empty_leaf |= count == 0u;
+            max_pairs = std::max(max_pairs, above);
+            return kLeafRef | ((count - 1u) << 27) | first;
+        }
+        const uint32_t q = alloc();  // a larger leaf: two halves under the same box
+        const uint32_t half = count / 2u;
+        const uint32_t l = leaf(box, first, half, above + 1), r = leaf(box, first + half, count - half, above + 1);
+        set(q, box, l, box, r);
+        return q;
+    }
+    uint32_t node(uint32_t i, int above) {
+        const BvhNode n = nodes[i];
+        if (n.b & 0x80000000u) return leaf(n, n.a, n.b & 0x7FFFFFFFu, above);
+        const uint32_t q = alloc();
+        const uint32_t l = node(n.a, above + 1), r = node(n.b, above + 1);
+        const BvhNode nl = nodes[n.a], nr = nodes[n.b];
+        set(q, nl, l, nr, r);
+        return q;
+    }
+};
 }  // namespace
 
 // The batched traversals (rt_kernel.hip mesh_bvh_pairs, sphere_group_batched) read each inner
@@ -565,6 +656,26 @@ std::string HostScene::build_mesh_pairs() {
     for (int k = 0; k < n_scan; ++k) {
         ObjRec& r = objs[k];
         if (!tree(r)) continue;
+        if (r.type == kObjMesh) {  // quantized 32 B pairs after the mesh's QFrame (rt_scene.h)
+            QPairBuilder qb{nodes};
+            qb.frame(r.u2);
+            const uint32_t fs = qb.alloc();
+            const uint32_t root = qb.node(r.u2, 0);
+            if (qb.empty_leaf) return "BVH with an empty leaf";
+            if (qb.bad) return "mesh BVH box off its quantization grid";
+            if (qb.max_pairs > kBvhStackDepth)
+                return "BVH pair depth " + std::to_string(qb.max_pairs) + " exceeds the traversal stack (" +
+                       std::to_string(kBvhStackDepth) + ")";
+            if (nodes.size() >= ((size_t)1 << 31)) return "too many BVH nodes (2^31)";
+            QFrame fr{};
+            for (int a = 0; a < 3; ++a) fr.c[a] = qb.c[a];
+            fr.s = (float)qb.s;
+            memcpy(&nodes[fs], &fr, sizeof fr);
+            bvh_max_depth = std::max(bvh_max_depth, qb.max_pairs);
+            memcpy(&r.f[8], &root, 4);
+            memcpy(&r.f[6], &fs, 4);
+            continue;
+        }
         if (nodes.size() & 1u) nodes.push_back(BvhNode{});
         PairBuilder pb{nodes};
         const uint32_t root = pb.node(r.u2, 0);

@@ -49,8 +49,9 @@ struct alignas(16) ObjRec {
     // plane: position xyz, normal xyz, rectangle bounds (lo_a, hi_a, lo_b, hi_b) on the
     //        orientation's axes a, b (XY: x, y; YZ: y, z; XZ: x, z)
     // mesh: boundsMin xyz, boundsMax xyz (computeMeshAABB, main.cu:261-281), f[6] = the bits of
-    //       ceil(2^32 / triangle count) (the brute-force compaction's division), f[7] = mesh-run
-    //       length (brute force), f[8] = root child-pair reference (BVH meshes), f[9] = 1 (as u32 bits)
+    //       ceil(2^32 / triangle count) (the brute-force compaction's division; BVH meshes: the node slot
+    //       of their QFrame), f[7] = mesh-run length (brute force), f[8] = root child-pair reference
+    //       (BVH meshes), f[9] = 1 (as u32 bits)
     //       for a brute-force mesh that is a convex shell (rt_scene.cpp convex_shell), 2 for a BVH
 //       mesh whose traversal the kernel may defer to the next loop trip (build_mesh_pairs, rt_kernel.hip kMeshDefer)
     float f[10];
@@ -88,6 +89,27 @@ struct alignas(16) BvhNode {
     uint32_t b;
 };
 static_assert(sizeof(BvhNode) == 32, "BvhNode must be 32 B");
+
+// Child-pair record of a MESH BVH (rt_kernel.hip mesh_bvh_pairs; rt_scene.cpp QPairBuilder): one 32 B node
+// slot holding both children's boxes as 16-bit grid coordinates of the mesh's frame (origin c, step s = 2^e):
+// box = [c + qlo s, c + qhi s], rounded outward from the inflated float box, so the grid box contains it.
+// q[0..2] = left (lo.x | lo.y << 16, lo.z | hi.x << 16, hi.y | hi.z << 16), q[3..5] = right, then the two
+// references (a pair slot index, or kLeafRef | (count - 1) << 27 | first triangle). Half the 64 B of a
+// float pair, so twice the records per L2 line: the bunny's 2.0 MB of pair records become 1.0 MB.
+struct alignas(32) QPair {
+    uint32_t q[6];
+    uint32_t ref[2];
+};
+static_assert(sizeof(QPair) == 32, "QPair must be 32 B");
+// The frame of a mesh's QPairs, one node slot before its root pair (index in the mesh record's f[6]):
+// c.xyz, s, then zeros.
+struct alignas(32) QFrame {
+    float c[3];
+    float s;
+    uint32_t pad[4];
+};
+static_assert(sizeof(QFrame) == 32, "QFrame must be 32 B");
+constexpr int kQMax = 65535;  // largest grid coordinate
 
 
 
