@@ -795,6 +795,9 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
     constexpr uint32_t kQ = (uint32_t)kMaxRun * 64u;
     __builtin_amdgcn_wave_barrier();
     auto batch = [&](uint32_t count) {
+#ifdef RT_STAMPS_GROUP  // diagnostic: full and partial member batches timed apart (slots 0 and 7), partial pairs (5)
+        RT_STAMP(b0);
+#endif
         const bool act = (uint32_t)lane < count;
         const uint32_t e = act ? W.slot[(qdone + (uint32_t)lane) & (kQ - 1)] : 0u;
         const uint32_t k = e >> 6;
@@ -817,6 +820,15 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
         if (mine != ~0ull && K[own] == mine) SRC[own] = (int32_t)k;  // (t, order) is unique
         qdone += count;
         __builtin_amdgcn_wave_barrier();
+#ifdef RT_STAMPS_GROUP
+        RT_STAMP(b1);
+        if (count == 64u) {
+            tm[0] += b1 - b0;
+        } else {
+            tm[7] += b1 - b0;
+            tm[5] += count;
+        }
+#endif
     };
     for (int trip = 0;; ++trip) {
         const uint64_t bm = __ballot(has || sp > 0);
@@ -1405,6 +1417,10 @@ __global__ __launch_bounds__(256) void combine_kernel(RenderLaunch L, float* __r
 #ifndef RT_CAM_BATCH
 #define RT_CAM_BATCH 32  // lanes lacking a prepared next sample that start a camera pass on their own
 #endif
+// The camera slot's spare word (linear-scan kernels): the path depth (bits 0-19) and the convex-shell skip
+// (bits 20-31).
+constexpr uint32_t kDepthMask = (1u << 20) - 1u;  // (max_depth < 2^20 for these kernels: rt_capi.cpp validate)
+
 // Camera slots: bit 31 of a lane's work-queue item is set while its slot holds the lane's next
 // sample (s if need_cam, else s + SP or the first sample of its group's next member): a flag in a VGPR already live, not a lane mask in SGPRs (the
 // megakernels' scarce registers). Item indices stay below 2^31 (rt_capi.cpp caps them).
@@ -1531,6 +1547,43 @@ __device__ __forceinline__ int global_row_of(const RenderLaunch& L, int lr) {
     return (lb * L.row_world + L.row_rank) * L.row_block + (lr - lb * L.row_block);
 }
 
+// Lambertian::scatter's direction (Material.cu:3-19): normalize(n + normalize(rp)) of a randomInUnitSphere
+// draw rp, with the reference's degenerate-direction fallback to n, by Markstein quotients where exact.
+__device__ __forceinline__ v3 lambert_dir(v3 n, v3 rp) {
+    v3 nd;
+    // normalize(rp) of a randomInUnitSphere draw: each component is 2u - 1 of a u01 draw, so
+    // +0 or at least 2^-24 in magnitude, and |rp| < 1: inside Markstein's domain (a +0
+    // component gives +0, as the IEEE division does) unless rp = 0 (all three draws 1/2,
+    // p = 2^-72), which takes the IEEE division
+    const float nrp = fsqrt(rp.x * rp.x + rp.y * rp.y + rp.z * rp.z);
+    const float yrp = rcp_nr(nrp);
+    v3 u{div_y(rp.x, nrp, yrp), div_y(rp.y, nrp, yrp), div_y(rp.z, nrp, yrp)};
+    if (__builtin_expect(__ballot(!(nrp > 0.0f)) != 0, 0))
+        if (!(nrp > 0.0f)) u = normalize(rp);
+    v3 sd = add(n, u);
+    const bool degen = (fabsf(sd.x) < 1e-8f) && (fabsf(sd.y) < 1e-8f) && (fabsf(sd.z) < 1e-8f);
+    if (degen) sd = n;
+    {
+        // normalize(sd) by Markstein quotients. Outside the degenerate case |sd| >= 1e-8 (and <= 2), so
+        // the norm is in the domain; a component is in it when it is +0 (sd = n + u is never -0: u has
+        // no -0 components, n + u cancels to +0) or at least 2^-100 in magnitude (its quotient then at
+        // least 2^-101). A wave with a degenerate lane (sd = n may hold -0) or a component in
+        // (0, 2^-100) takes the IEEE divisions.
+        const float ns = fsqrt(sd.x * sd.x + sd.y * sd.y + sd.z * sd.z);
+        const float ys = rcp_nr(ns);
+        nd = v3{div_y(sd.x, ns, ys), div_y(sd.y, ns, ys), div_y(sd.z, ns, ys)};
+        // |c| in (0, 2^-100) iff bits(|c|) - 1 < bits(2^-100) - 1 (unsigned; +0 wraps)
+        const uint32_t tiny = __builtin_elementwise_min(
+            __builtin_elementwise_min((__float_as_uint(sd.x) & 0x7FFFFFFFu) - 1u,
+                                      (__float_as_uint(sd.y) & 0x7FFFFFFFu) - 1u),
+            (__float_as_uint(sd.z) & 0x7FFFFFFFu) - 1u);
+        const bool ieee = degen || tiny < 0x0D7FFFFFu;
+        if (__builtin_expect(__ballot(ieee) != 0, 0))
+            if (ieee) nd = normalize(sd);
+    }
+    return nd;
+}
+
 // kSph = false: the variant for simple scenes (CornellBox1; with kBvh the bunny box): planes and
 // meshes with Lambertian and emissive materials only - neither the sphere test, the sphere
 // normals, media nor the metal / dielectric / isotropic scatter is compiled in (rt_capi.cpp
@@ -1639,7 +1692,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             tail_steal(L, W, lane, SP, alive, waiting, held, towner, tl_pack, own_end, s, item, sum, thr, need_cam);
         if (__ballot(alive || waiting || held || (kQueue && !exhausted)) == 0) break;  // wave-uniform exit
         RT_STAMP(t_a);
+#ifndef RT_STAMPS_GROUP
         RT_ACC(7, t_q, t_a);
+#endif
         if constexpr (kCamPf) {
             // Camera slots. A lane starting a sample takes it from its slot when it was prepared;
             // the camera pass (Philox seeding, getRay's draws and arithmetic) runs when some lane
@@ -1707,22 +1762,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                 sample_done(L, v3{0.0f, 0.0f, 0.0f}, SP, item, own_end, s, sum, thr, alive, need_cam, towner,
                             held, waiting, tl_pack);
         }
+        // the camera slot's spare word (linear-scan kernels): path depth, convex-shell skip
+        uint32_t cw = 0u;
+        if constexpr (kCamPf) cw = reinterpret_cast<const uint32_t*>(&cslots[wave].c[lane])[3];
         const bool live = alive && !need_cam;
         if constexpr (kDef) W.grp_s[lane] = (W.grp_s[lane] >> 1) & 1u;  // bit 0: deferred on the last trip
         RT_STAMP(t_b);
+#ifndef RT_STAMPS_GROUP
         RT_ACC(0, t_a, t_b);
+#endif
 #ifdef RT_STAMPS
         tm[4] += 1;                                  // loop trips (per wave)
+#ifndef RT_STAMPS_GROUP
         tm[5] += (uint64_t)__popcll(__ballot(live));  // lanes tracing a segment this trip
+#endif
         if (!kBvh) tm[6] += (uint64_t)__popcll(__ballot(valid)); // lanes that own a pixel (BVH kernels: slot 6 counts traversal lanes)
 #endif
 
         const v3 inv = rcp_exact(ray.d);
         // convex-shell skip: the convex mesh this segment starts on and leaves (shading below), kept beside the
         // path depth in the camera slot's spare word: bits 20-31 = its object index + 1
-        int skip = -1;
-        if constexpr (kCamPf)
-            skip = (int)(reinterpret_cast<const uint32_t*>(&cslots[wave].c[lane])[3] >> 20) - 1;
+        const int skip = kCamPf ? (int)(cw >> 20) - 1 : -1;
         const Hit h = closest_hit<kBvh, kMed, kSph, kParts>(S, ray, inv, live, rng, W, stack, lane, cnt, skip,
                                                             kResume ? &glds[wave] : nullptr
 #ifdef RT_STAMPS
@@ -1776,36 +1836,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             if (m.type == 0u || (kSph && (m.type == 1u || m.type == 4u))) rp = random_in_unit_sphere(rng);
             if (m.type == 0u) {
                 // Lambertian::scatter (Material.cu:3-19).
-                // normalize(rp) of a randomInUnitSphere draw: each component is 2u - 1 of a u01 draw, so
-                // +0 or at least 2^-24 in magnitude, and |rp| < 1: inside Markstein's domain (a +0
-                // component gives +0, as the IEEE division does) unless rp = 0 (all three draws 1/2,
-                // p = 2^-72), which takes the IEEE division
-                const float nrp = fsqrt(rp.x * rp.x + rp.y * rp.y + rp.z * rp.z);
-                const float yrp = rcp_nr(nrp);
-                v3 u{div_y(rp.x, nrp, yrp), div_y(rp.y, nrp, yrp), div_y(rp.z, nrp, yrp)};
-                if (__builtin_expect(__ballot(!(nrp > 0.0f)) != 0, 0))
-                    if (!(nrp > 0.0f)) u = normalize(rp);
-                v3 sd = add(n, u);
-                const bool degen = (fabsf(sd.x) < 1e-8f) && (fabsf(sd.y) < 1e-8f) && (fabsf(sd.z) < 1e-8f);
-                if (degen) sd = n;
-                {
-                    // normalize(sd) by Markstein quotients. Outside the degenerate case |sd| >= 1e-8 (and <= 2), so
-                    // the norm is in the domain; a component is in it when it is +0 (sd = n + u is never -0: u has
-                    // no -0 components, n + u cancels to +0) or at least 2^-100 in magnitude (its quotient then at
-                    // least 2^-101). A wave with a degenerate lane (sd = n may hold -0) or a component in
-                    // (0, 2^-100) takes the IEEE divisions.
-                    const float ns = fsqrt(sd.x * sd.x + sd.y * sd.y + sd.z * sd.z);
-                    const float ys = rcp_nr(ns);
-                    nd = v3{div_y(sd.x, ns, ys), div_y(sd.y, ns, ys), div_y(sd.z, ns, ys)};
-                    // |c| in (0, 2^-100) iff bits(|c|) - 1 < bits(2^-100) - 1 (unsigned; +0 wraps)
-                    const uint32_t tiny = __builtin_elementwise_min(
-                        __builtin_elementwise_min((__float_as_uint(sd.x) & 0x7FFFFFFFu) - 1u,
-                                                  (__float_as_uint(sd.y) & 0x7FFFFFFFu) - 1u),
-                        (__float_as_uint(sd.z) & 0x7FFFFFFFu) - 1u);
-                    const bool ieee = degen || tiny < 0x0D7FFFFFu;
-                    if (__builtin_expect(__ballot(ieee) != 0, 0))
-                        if (ieee) nd = normalize(sd);
-                }
+                nd = lambert_dir(n, rp);
                 att = v3{m.a0, m.a1, m.a2};
                 scattered = true;
             } else if (kSph && m.type == 1u) {
@@ -1872,7 +1903,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                     // the linear-scan kernels keep the path depth in the camera slot's spare word (LDS)
                     // instead of a VGPR of the persistent loop (at 7 waves/SIMD the CB1 kernel spilled it)
                     uint32_t* dw = reinterpret_cast<uint32_t*>(&cslots[wave].c[lane]) + 3;
-                    const uint32_t dn = (*dw & 0xFFFFFu) + 1u;  // (max_depth < 2^20: rt_capi.cpp validate)
+                    const uint32_t dn = (*dw & kDepthMask) + 1u;  // (max_depth < 2^20: rt_capi.cpp validate)
                     *dw = dn | (self_bits << 20);
                     done = (int)dn >= L.max_depth;
                 } else

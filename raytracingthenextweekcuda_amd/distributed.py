@@ -17,6 +17,7 @@ with the gloo backend (tests/test_distributed.py).
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Optional
 
 from .renderer import owned_row_ids, owned_rows
@@ -243,6 +244,12 @@ class RcclRowFrames:
         else:
             self.gparams = Renderer.params(width, self.max_rows, 1, 1, row_block=self.max_rows)
         self.n_submitted = 0
+        # the previous frame's gather (an event on its stream): each gather waits for it, so the
+        # communicator's collectives run in issue order - the same order on every rank - even though
+        # they are enqueued on different streams (no reliance on RCCL ordering one communicator's
+        # operations across streams)
+        self.gather_done = None
+        self.order_gathers = os.environ.get("RTMI_GATHER_ORDER", "1") != "0"  # 0: A/B only
 
     def _gather(self, b, stream_ptr):
         C = self.C
@@ -258,7 +265,12 @@ class RcclRowFrames:
         b = self.n_submitted % len(self.renderers)
         self.n_submitted += 1
         render_into(self.tiles[b], b)
+        if self.gather_done is not None:
+            self.streams[b].wait_event(self.gather_done)
         self._gather(b, self.streams[b].cuda_stream)
+        if self.order_gathers:
+            self.gather_done = self.torch.cuda.Event()
+            self.gather_done.record(self.streams[b])
         if self.frames:
             self.frame = self.frames[b]
 
@@ -272,11 +284,16 @@ class RcclRowFrames:
         """Gathers context 0's tile on the current stream (the isolated frames after the timed
         region); `events` (start, end) are recorded around the collective alone."""
         s = self.torch.cuda.current_stream()
+        if self.gather_done is not None:
+            s.wait_event(self.gather_done)
         if events:
             events[0].record(s)
         self._gather(0, s.cuda_stream)
         if events:
             events[1].record(s)
+        if self.order_gathers:
+            self.gather_done = self.torch.cuda.Event()
+            self.gather_done.record(s)
         if self.frames:
             self.frame = self.frames[0]
         return self.frame if self.rank == 0 else None
