@@ -541,7 +541,17 @@ static rt_status rt_process_triangle_data_impl(rt_ctx* c, const float offset[3],
             if (err != hipSuccess || !bytes) return err;
             return hipMemcpy(*dst, vec.data(), bytes, hipMemcpyHostToDevice);
         };
-        RT_HIP(c, up(&c->d_pt_tris, kt));
+        // the kernel reads the triangles in the DFS list order of its leaf references (the reference's
+        // cudaTriIdxList indirection resolved here): record i is triangle tri_index[i], whose index the
+        // record keeps in pad[0] for avoidSelf; a leaf test is then one dependent load, not two
+        std::vector<rt::KTri> lt(b.tri_index.size());
+        for (size_t i = 0; i < lt.size(); ++i) {
+            const uint32_t idx = (uint32_t)b.tri_index[i];
+            if (idx >= kt.size()) return fail(c, RT_ERR_INVALID, "pathTrace triangle list index out of range");
+            lt[i] = kt[idx];
+            memcpy(&lt[i].pad[0], &idx, 4);
+        }
+        RT_HIP(c, up(&c->d_pt_tris, lt));
         RT_HIP(c, up(&c->d_pt_nodes, dev_nodes));
         RT_HIP(c, up(&c->d_pt_list, b.tri_index));
     }

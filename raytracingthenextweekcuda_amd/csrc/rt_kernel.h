@@ -130,7 +130,7 @@ struct KTri;
 struct CFNode;
 // Device tables of the pathTrace integrator (prepareCUDAscene, main.cu:404-553).
 struct PtSceneArgs {
-    const KTri* ktris;
+    const KTri* ktris;        // in tri_list order (record i = triangle tri_list[i], its index in pad[0])
     const CFNode* nodes;      // the reference's CacheFriendlyBVHNode array, exact bounds
     const int32_t* tri_list;  // leaf triangle lists in DFS order
 };

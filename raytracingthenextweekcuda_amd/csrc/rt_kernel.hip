@@ -219,22 +219,24 @@ __device__ __forceinline__ float tri_rcp(float det) {
     return y;
 }
 
-// One triangle of TriangleMesh::hit (TriangleMesh.cu:40-108) without the
-// closestSoFar comparison: returns t if every other acceptance test passes,
-// else NaN (compares false with anything). The caller applies closestSoFar.
+// One triangle of TriangleMesh::hit (TriangleMesh.cu:40-108) without the closestSoFar comparison: returns t if
+// every other acceptance test passes, else NaN (compares false with anything); the caller applies
+// closestSoFar. The backface cull (TriangleMesh.cu:40-43) is the final select, not an early return, so the
+// caller's record loads all issue at once instead of the normal first and the edges after the cull (the
+// batched BVH leaf tests: one dependent load round trip per batch instead of two; round 6).
 __device__ __forceinline__ float tri_t(const TriRec& tr, v3 o, v3 d) {
-    const float kNo = __builtin_nanf("");
     v3 n{tr.nx, tr.ny, tr.nz};
-    if (dot(d, n) > kFltEpsilon) return kNo;  // backface cull
+    const bool cull = dot(d, n) > kFltEpsilon;
     v3 e1{tr.e1x, tr.e1y, tr.e1z}, e2{tr.e2x, tr.e2y, tr.e2z};
     v3 s = sub(o, v3{tr.v0x, tr.v0y, tr.v0z});
     v3 s1 = cross(d, e2);
     v3 s2 = cross(s, e1);
-    const float coef = fdiv(1.0f, dot(s1, e1));  // (tri_rcp's guard costs the BVH kernels registers)
+    const float coef = fdiv(1.0f, dot(s1, e1));
     float t = coef * dot(s2, e2);
     float b1 = coef * dot(s1, s);
     float b2 = coef * dot(s2, d);
-    return tri_accept(t, b1, b2);
+    const float ta = tri_accept(t, b1, b2);
+    return cull ? __builtin_nanf("") : ta;
 }
 
 // tri_t for a pair already known to pass the backface cull.
@@ -491,10 +493,13 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
         const v3 po{lane_read(o.x, own), lane_read(o.y, own), lane_read(o.z, own)};
         const v3 pd{lane_read(d.x, own), lane_read(d.y, own), lane_read(d.z, own)};
         const float pt0 = lane_read(h.t, own);
-        // lanes past `count` test triangle 0 (valid) and drop the result: no branch around the loads
-        const float t = tri_t(tris[k], po, pd);
-        if (act && t <= pt0)
-            atomicMin(&W.key[own], ((unsigned long long)__float_as_uint(t) << 32) | tri_orig[2 * k]);
+        // lanes past `count` test triangle 0 (valid) and drop the result: no branch around the loads. The
+        // triangle's 48 B and its mesh-local index are loaded together, before the test needs either
+        const TriRec tr = tris[k];
+        const uint32_t orig = tri_orig[2 * k];
+        const float t = tri_t(tr, po, pd);
+        asm volatile("" ::"v"(orig));  // (keeps the index load beside the record's, not behind the test)
+        if (act && t <= pt0) atomicMin(&W.key[own], ((unsigned long long)__float_as_uint(t) << 32) | orig);
         qdone += count;
         __builtin_amdgcn_wave_barrier();
     };
@@ -2143,8 +2148,7 @@ struct PtBest {
 // ray's LDS minimum of (distance^2, list position) - the reference's first-in-DFS tie rule.
 // Pairs take their ray (origin, direction, avoidSelf) from the owner lane's registers.
 __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict__ ktris,
-                                                         const CFNode* __restrict__ nodes,
-                                                         const int32_t* __restrict__ tri_list, uint32_t* wstack,
+                                                         const CFNode* __restrict__ nodes, uint32_t* wstack,
                                                          unsigned long long* keys, int32_t* vlist, uint32_t* queue,
                                                          int lane, bool want, const PtRay& ray, int avoid_in,
                                                          float len_in, float eps_in, PtBest& out, Counters& cnt,
@@ -2194,9 +2198,11 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
             // (their exec-mask saves and restores are scalar instructions, this kernel's co-bound). The
             // acceptance keeps the reference's comparisons, NaN cases included: the edge tests are
             // `!(e < 0)`, which holds for NaN; the key of a rejected pair is ~0, a no-op for atomicMin.
-            const int idx = tri_list[act ? i : 0u];
-            const float4* T = reinterpret_cast<const float4*>(ktris + idx);
-            const float4 q0 = T[0], q1 = T[1], q2 = T[2], q3 = T[3];
+            // the record of list position i (rt_capi.cpp stores the triangles in list order, the triangle's
+            // index beside its material): one load round trip, no cudaTriIdxList indirection
+            const float4* T = reinterpret_cast<const float4*>(ktris + (act ? i : 0u));
+            const float4 q0 = T[0], q1 = T[1], q2 = T[2], q3 = T[3], q4 = T[4];
+            const int idx = __float_as_int(q4.y);
             const v3 nn{q0.x, q0.y, q0.z};
             const float k = dot(nn, pd);
             const float sd = fdiv(q0.w - dot(nn, po), k);
@@ -2210,29 +2216,6 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
             const float hz = df.x * df.x + df.y * df.y + df.z * df.z;  // distancesq
             const unsigned long long key = ((unsigned long long)__float_as_uint(hz) << 32) | i;
             atomicMin(&keys[own], ok ? key : ~0ull);
-        }
-        if (false) {
-            // the Kuchkuda test for list position i (CUDAPathTracer.cu:258-345)
-            const int idx = tri_list[i];
-            if (pav != idx) {
-                const float4* T = reinterpret_cast<const float4*>(ktris + idx);
-                const float4 q0 = T[0], q1 = T[1], q2 = T[2], q3 = T[3];
-                const v3 nn{q0.x, q0.y, q0.z};
-                const float k = dot(nn, pd);
-                if (k != 0.0f) {
-                    const float sd = fdiv(q0.w - dot(nn, po), k);
-                    if (sd > 0.0f && sd > 1e-3f) {  // NUDGE_FACTOR
-                        const v3 hit = add(scale(pd, sd), po);
-                        if (!(dot(v3{q1.x, q1.y, q1.z}, hit) - q1.w < 0.0f) &&
-                            !(dot(v3{q2.x, q2.y, q2.z}, hit) - q2.w < 0.0f) &&
-                            !(dot(v3{q3.x, q3.y, q3.z}, hit) - q3.w < 0.0f)) {
-                            const v3 df = sub(po, hit);
-                            const float hz = df.x * df.x + df.y * df.y + df.z * df.z;  // distancesq
-                            atomicMin(&keys[own], ((unsigned long long)__float_as_uint(hz) << 32) | i);
-                        }
-                    }
-                }
-            }
         }
         qdone += count;
         __builtin_amdgcn_wave_barrier();
@@ -2340,8 +2323,9 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
         if (key != ~0ull) {
             // the winner's hit point with the batch test's operations on the owner's ray
             const int i = (int)(uint32_t)(key & 0xFFFFFFFFu);
-            const int idx = tri_list[i];
-            const float4 q0 = reinterpret_cast<const float4*>(ktris + idx)[0];
+            const float4* T = reinterpret_cast<const float4*>(ktris + i);
+            const float4 q0 = T[0];
+            const int idx = __float_as_int(T[4].y);
             const v3 nn{q0.x, q0.y, q0.z};
             const float k = dot(nn, ray.d);
             const float sd = fdiv(q0.w - dot(nn, ray.o), k);
@@ -2361,7 +2345,7 @@ __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict_
 template <bool kQueue>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES))) void pathtrace_kernel(
     RenderLaunch L, const KTri* __restrict__ ktris, const CFNode* __restrict__ nodes,
-    const int32_t* __restrict__ tri_list, const CamRec* __restrict__ cam, float* __restrict__ out,
+    const CamRec* __restrict__ cam, float* __restrict__ out,
     unsigned long long* __restrict__ counters) {
     constexpr int kBW = block_waves(kQueue);
     extern __shared__ uint32_t dyn_stacks[];  // kBW x L.stack_depth x 64, sized at launch
@@ -2451,7 +2435,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
             // coordinates involved), with a 10x margin.
             const float eps = 1e-5f * (1.0f + fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) + L.pt_scale);
             r.eps = eps;
-            pt_traverse_coop_batched(ktris, nodes, tri_list, stack - lane, pt_keys[wave], pt_vlist[wave], pt_queue[wave],
+            pt_traverse_coop_batched(ktris, nodes, stack - lane, pt_keys[wave], pt_vlist[wave], pt_queue[wave],
                                      lane, alive, r, avoid, fsqrt(dot(d, d)), eps, best, cnt, L.stack_depth,
                                      L.pt_root_ref);
         }
@@ -2459,7 +2443,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
         if (!alive) continue;
         const int best_idx = best.idx;
         const v3 best_hit = best.hit;
-        const uint32_t best_mat = best_idx >= 0 ? (uint32_t)ktris[best_idx].material : kDiffuse;
+        const uint32_t best_mat = best_idx >= 0 ? (uint32_t)ktris[best.i].material : kDiffuse;
         const float hitdistance = best_idx >= 0 ? best.dist : 1e20f;
 
         // the six spheres, scanned i = 5 .. 0 (CUDAPathTracer.cu:400-404)
@@ -2495,7 +2479,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PT_WAVES
                 rt = sp.type;
                 accu = add(accu, mul(mask, v3{sp.emi[0], sp.emi[1], sp.emi[2]}));
             } else {
-                const KTri& T = ktris[best_idx];
+                const KTri& T = ktris[best.i];
                 hitp = best_hit;
                 normal = normalize(v3{T.n[0], T.n[1], T.n[2]});
                 oriented = dot(normal, d) < 0.0f ? normal : scale(normal, -1.0f);
@@ -2640,7 +2624,7 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
         const uint32_t blocks = std::min<uint32_t>((waves + kQueueBlockWaves - 1) / kQueueBlockWaves,
                                                    (uint32_t)L.queue);
         hipLaunchKernelGGL(pathtrace_kernel<true>, dim3(blocks), dim3(64 * kQueueBlockWaves),
-                           stack_bytes(L, kQueueBlockWaves), stream, L, sc.ktris, sc.nodes, sc.tri_list, cam, out,
+                           stack_bytes(L, kQueueBlockWaves), stream, L, sc.ktris, sc.nodes, cam, out,
                            counters);
         if (main_done) (void)hipEventRecord(main_done, stream);
         const uint32_t pixels = L.n_items / (uint32_t)L.lanes_per_pixel;
@@ -2651,7 +2635,7 @@ hipError_t launch_pathtrace(const PtSceneArgs& sc, const CamRec* cam, const Rend
               (L.local_rows + 2 * L.tile_h - 1) / (2 * L.tile_h));
     if (grid.x == 0 || grid.y == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
     hipLaunchKernelGGL(pathtrace_kernel<false>, grid, dim3(64 * kWavesPerBlock), stack_bytes(L, kWavesPerBlock),
-                       stream, L, sc.ktris, sc.nodes, sc.tri_list, cam, out, counters);
+                       stream, L, sc.ktris, sc.nodes, cam, out, counters);
     if (main_done) (void)hipEventRecord(main_done, stream);
     return hipGetLastError();
 }
