@@ -37,6 +37,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "rt_bvh.h"
 #include "rt_kernel.h"
@@ -318,19 +319,29 @@ struct Hit {
 
 constexpr int kMaxRun = (int)kMeshRunMax;  // meshes per run (rt_scene.cpp marks the runs)
 // The render kernels' traversal stacks hold L.stack_depth entries per lane (the scene's deepest path in
-// pair records, rt_scene.cpp PairBuilder::max_pairs) PLUS this spare slot: a lane that does not push
-// writes its would-be entry to slot stack_cap = L.stack_depth unconditionally (mesh_bvh_pairs' lane
-// selects), so that slot must exist in every lane's column. The kernel's stack base and the launch's
-// dynamic LDS size (stack_bytes) both count it; tests/test_fuzz_parity.py renders a chain BVH whose
-// deepest pair is reached with both children hit.
-constexpr int kStackSpare = 1;
+// pair records, rt_scene.cpp PairBuilder::max_pairs), PLUS one spare slot in kernels that traverse sphere
+// groups: a lane that does not push writes its would-be entry to slot stack_cap = L.stack_depth
+// unconditionally (sphere_group_batched's lane selects), so that slot must exist in every lane's column.
+// mesh_bvh_pairs writes its would-be entry to W.src[lane] instead, dead between the trip's steal round and
+// the next (round 6: the mesh-BVH-only kernels need no spare slot). The kernel's stack base and the launch's
+// dynamic LDS size (stack_bytes) both count it; tests/test_fuzz_parity.py renders a chain BVH whose deepest
+// pair is reached with both children hit.
+template <int kParts>
+constexpr int stack_spare() { return (kParts & 2) != 0 ? 1 : 0; }
 
-struct WaveLds {
+// A wave's LDS tables. The mesh-BVH-only kernels (kParts = 1: the bunny, Suzanne) use the core alone: they
+// keep no sphere-group counts, and their brute-force compaction's cull ring lives in the wave's traversal
+// stacks (empty between two mesh traversals: nothing is carried across) - 512 B per wave less, which with the
+// spare slot's 256 B lets six 4-wave blocks of the bunny's kernel (18-entry stacks) fit a CU's 160 KB.
+struct WaveLdsCore {
     unsigned long long key[64];  // per-ray (t bits << 32 | triangle) minima
     int32_t src[64];             // rank -> lane of the rays wanting a mesh
     uint32_t slot[kMaxRun * 64];  // mesh_run ray slots / the BVH traversals' deferred leaf pairs
-    uint32_t grp_s[64], grp_m[64];  // per-lane sphere-group test counts (Counters::grp drained per trip)
-    uint16_t ring[128];          // pair ids that passed the backface cull, awaiting the full test
+    uint32_t grp_s[64];          // per-lane sphere-group test counts / the mesh deferral's bits (kParts = 1)
+};
+struct WaveLds : WaveLdsCore {
+    uint32_t grp_m[64];  // per-lane moving-sphere test counts (Counters::grp drained per trip)
+    uint16_t ring[128];  // pair ids that passed the backface cull, awaiting the full test
 };
 
 // The sphere-group traversal's per-lane state that outlives a loop trip (kResume): a lane whose
@@ -468,7 +479,7 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
                                                const uint32_t* __restrict__ tri_orig,
                                                const BvhNode* __restrict__ nodes, uint32_t root, uint32_t frame,
                                                uint32_t base, bool want, v3 o, v3 d, v3 inv, Hit& h, int32_t obj,
-                                               uint32_t order, uint32_t* wstack, WaveLds& W, int lane,
+                                               uint32_t order, uint32_t* wstack, WaveLdsCore& W, int lane,
                                                Counters& cnt, int cap RT_TM_PARAM) {
     const uint64_t wm = __ballot(want);
     if (wm == 0) return;
@@ -566,7 +577,9 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
             if (__builtin_expect(__ballot(ovf) != 0, 0))
                 if (ovf) cnt.overflow();
             const bool push = both && !ovf;
-            wstack[(push ? sp : cap) * 64 + lane] = lf ? pr.ref[1] : pr.ref[0];
+            // (a lane that does not push writes its own W.src word, dead until the next trip's steal round)
+            uint32_t* const dst = push ? wstack + sp * 64 + lane : reinterpret_cast<uint32_t*>(&W.src[lane]);
+            *dst = lf ? pr.ref[1] : pr.ref[0];
             sp = ovf ? 0 : sp + (push ? 1 : 0);
             bot = ovf ? 0 : bot;
             cur = both ? (lf ? pr.ref[0] : pr.ref[1]) : (hl ? pr.ref[0] : pr.ref[1]);
@@ -653,7 +666,8 @@ __device__ __forceinline__ ObjRec load_obj(const ObjRec* __restrict__ objs, int 
 template <bool kOrdered, bool kLin>
 __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
                                          int i0, uint32_t g, uint32_t m, uint32_t magic, bool live, v3 o, v3 d,
-                                         v3 inv, Hit& h, Counters& cnt, WaveLds& W, int lane, int skip) {
+                                         v3 inv, Hit& h, Counters& cnt, WaveLdsCore& W, uint16_t* ring, int lane,
+                                         int skip) {
     uint32_t nslot = 0;  // wave-uniform
     bool any = false;
     const uint32_t lives = (uint32_t)__popcll(__ballot(live));
@@ -682,7 +696,7 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
     auto full_test = [&](uint32_t count) {
         const uint32_t i = tested + (uint32_t)lane;
         const bool act = (uint32_t)lane < count;
-        const uint32_t p = act ? (uint32_t)W.ring[i & 127u] : 0u;
+        const uint32_t p = act ? (uint32_t)ring[i & 127u] : 0u;
         const uint32_t r = slot_of(p);
         const uint32_t e = W.slot[r];
         const int src = (int)(e & 63u);
@@ -717,12 +731,12 @@ __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const 
         const bool keep = !(fmaxf(dn, lim) > kFltEpsilon);  // TriangleMesh.cu:72
         const uint64_t km = __ballot(keep);
         // (a non-keeper's rank is <= K <= 63, so rank | 63 = 63)
-        W.ring[(queued + ((uint32_t)lane_rank(km) | (keep ? 0u : 63u))) & 127u] = (uint16_t)p;
+        ring[(queued + ((uint32_t)lane_rank(km) | (keep ? 0u : 63u))) & 127u] = (uint16_t)p;
         queued += (uint32_t)__popcll(km);
         } else {
         const bool keep = act && !(dot(rd, v3{tr.nx, tr.ny, tr.nz}) > kFltEpsilon);  // TriangleMesh.cu:72
         const uint64_t km = __ballot(keep);
-        if (keep) W.ring[(queued + (uint32_t)lane_rank(km)) & 127u] = (uint16_t)p;
+        if (keep) ring[(queued + (uint32_t)lane_rank(km)) & 127u] = (uint16_t)p;
         queued += (uint32_t)__popcll(km);
         }
         __builtin_amdgcn_wave_barrier();
@@ -782,7 +796,7 @@ template <bool kResume>
 __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ objs,
                                                      const BvhNode* __restrict__ nodes, uint32_t root,
                                                      bool live, const Ray& ray, v3 inv, float inva, Hit& h,
-                                                     uint32_t* wstack, WaveLds& W, int lane, Counters& cnt,
+                                                     uint32_t* wstack, WaveLdsCore& W, int lane, Counters& cnt,
                                                      int cap, GroupLds* gl RT_TM_PARAM) {
     if (__ballot(live) == 0) return;
     unsigned long long* K = kResume ? gl->key : W.key;
@@ -1027,7 +1041,7 @@ __device__ __forceinline__ float plane_axial(const ObjRec& ob, v3 o, v3 d) {
 
 template <bool kBvh, bool kMed = false, bool kSph = true, int kParts = 3>
 __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v3 inv, bool live,
-                                           Rng& rng, WaveLds& W, uint32_t* stack, int lane,
+                                           Rng& rng, WaveLdsCore& W, uint16_t* ring, uint32_t* stack, int lane,
                                            Counters& cnt, int skip, GroupLds* gl
 #ifdef RT_STAMPS
                                            , uint64_t* tm
@@ -1103,7 +1117,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
                 RT_STAMP(t_m0);
                 if (g != 0u)
                     mesh_run<kOrd, !kBvh>(S.objs, S.tris, i, g, ob.u1, __float_as_uint(ob.f[6]), live, o, d, inv, h, cnt, W,
-                                   lane, skip);
+                                   ring, lane, skip);
                 RT_STAMP(t_m1);
                 RT_ACC(3, t_m0, t_m1);
             } else if constexpr ((kParts & 1) != 0) {
@@ -1242,7 +1256,7 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #define RT_GROUP_WAVES 5
 #endif
 #ifndef RT_BVH_SIMPLE_WAVES
-#define RT_BVH_SIMPLE_WAVES 5
+#define RT_BVH_SIMPLE_WAVES 6  // the bunny box: six 4-wave blocks fit since round 6 (slim LDS); 13 VGPRs spill outside the traversal
 #endif
 #ifndef RT_PT_WAVES
 #define RT_PT_WAVES 6
@@ -1483,7 +1497,7 @@ __device__ __forceinline__ void sample_done(const RenderLaunch& L, v3 contrib, i
 // and holds its radiance; the owner, once its own samples are done, folds the
 // held values in sample order and writes the partial sum. The partial sums are
 // therefore bit-identical; only the tail of the launch gets shorter.
-__device__ __forceinline__ void tail_steal(const RenderLaunch& L, WaveLds& W, int lane, int SP, bool& alive,
+__device__ __forceinline__ void tail_steal(const RenderLaunch& L, WaveLdsCore& W, int lane, int SP, bool& alive,
                                            bool& waiting, bool& held, int& towner, uint32_t& tl_pack,
                                            int& own_end, int& s, uint32_t& item, v3& sum, v3& thr,
                                            bool& need_cam) {
@@ -1601,7 +1615,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
     float* __restrict__ out, unsigned long long* __restrict__ counters) {
     const SceneArgs S{objs, tris, mats, nodes, tri_orig, n_objs, 0, kBvh, L.stack_depth};
     constexpr int kBW = block_waves(kQueue);
-    __shared__ WaveLds lds[kBW];
+    // the mesh-BVH-only kernels keep the core tables only (WaveLdsCore)
+    constexpr bool kSlim = kBvh && kParts == 1;
+    __shared__ std::conditional_t<kSlim, WaveLdsCore, WaveLds> lds[kBW];
     // camera slots: the linear-scan kernels only (the traversal kernels' LDS holds their stacks)
     constexpr bool kCamPf = !kBvh;
     // resumable sphere-group traversal (the sphere-group-only kernel)
@@ -1614,13 +1630,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    WaveLds& W = lds[wave];
+    WaveLdsCore& W = lds[wave];
     if (kBvh) {  // sphere groups exist only in BVH scenes
         W.grp_s[lane] = 0;
-        W.grp_m[lane] = 0;
+        if constexpr (!kSlim) lds[wave].grp_m[lane] = 0;
     }
     if (kResume) glds[wave].st[lane] = 0u;
-    uint32_t* stack = kBvh ? dyn_stacks + (size_t)wave * (L.stack_depth + kStackSpare) * 64 + lane : nullptr;
+    uint32_t* const wstack0 = kBvh ? dyn_stacks + (size_t)wave * (L.stack_depth + stack_spare<kParts>()) * 64 : nullptr;
+    uint32_t* stack = kBvh ? wstack0 + lane : nullptr;
+    // the brute-force compaction's cull ring: in the slim kernels the first level of the wave's stacks (256 B)
+    uint16_t* ring;
+    if constexpr (kSlim) ring = reinterpret_cast<uint16_t*>(wstack0);
+    else ring = lds[wave].ring;
 
     // Lane layout: SP = lanes_per_pixel adjacent lanes share one pixel and split
     // its samples (sub-lane c takes samples c, c+SP, c+2SP, ...). A wave covers
@@ -1788,7 +1809,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         // convex-shell skip: the convex mesh this segment starts on and leaves (shading below), kept beside the
         // path depth in the camera slot's spare word: bits 20-31 = its object index + 1
         const int skip = kCamPf ? (int)(cw >> 20) - 1 : -1;
-        const Hit h = closest_hit<kBvh, kMed, kSph, kParts>(S, ray, inv, live, rng, W, stack, lane, cnt, skip,
+        const Hit h = closest_hit<kBvh, kMed, kSph, kParts>(S, ray, inv, live, rng, W, ring, stack, lane, cnt, skip,
                                                             kResume ? &glds[wave] : nullptr
 #ifdef RT_STAMPS
                                         , tm
@@ -1802,7 +1823,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         cnt.segs += (uint32_t)__popcll(__ballot(live && !pend));
         if (kBvh && __ballot(cnt.grp != 0)) {  // drain the 16-bit sphere-group counts
             W.grp_s[lane] += cnt.grp & 0xFFFFu;
-            W.grp_m[lane] += cnt.grp >> 16;
+            if constexpr (!kSlim) lds[wave].grp_m[lane] += cnt.grp >> 16;
             cnt.grp = 0;
         }
         if (!live || pend) continue;
@@ -1962,7 +1983,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
     const uint64_t wb = cnt.box_tests;
     const uint64_t wn = wave_sum_u64(cnt.node_visits);
     const uint64_t wgs = kBvh && !kDef ? wave_sum_u64(W.grp_s[lane] + (cnt.grp & 0xFFFFu)) : 0;
-    const uint64_t wgm = kBvh && !kDef ? wave_sum_u64(W.grp_m[lane] + (cnt.grp >> 16)) : 0;
+    uint64_t wgm = 0;
+    if constexpr (kBvh && !kSlim) wgm = wave_sum_u64(lds[wave].grp_m[lane] + (cnt.grp >> 16));
 #ifdef RT_STAMPS
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(&counters[8 + k], (unsigned long long)tm[k]);
@@ -2655,8 +2677,11 @@ int queue_blocks(int n_cu, uint32_t variant, const RenderLaunch& L) {
         case RT_VARIANT_SCAN_MEDIA_STATIC: case RT_VARIANT_SCAN_SIMPLE_QUEUE: case RT_VARIANT_SCAN_SIMPLE_STATIC:
             lds = (size_t)bw * (sizeof(WaveLds) + sizeof(CamSlots));
             break;
+        case RT_VARIANT_BVH_MESH_QUEUE: case RT_VARIANT_BVH_MESH_SIMPLE_QUEUE:  // kParts = 1: the slim tables
+            lds = (size_t)bw * sizeof(WaveLdsCore) + stack_bytes(L, bw, stack_spare<1>());
+            break;
         default:
-            lds = (size_t)bw * sizeof(WaveLds) + stack_bytes(L, bw, kStackSpare);
+            lds = (size_t)bw * sizeof(WaveLds) + stack_bytes(L, bw, stack_spare<3>());
             // the sphere-group-only kernel also keeps its resumed traversals' state
             if (variant == RT_VARIANT_BVH_GROUP_QUEUE) lds += (size_t)bw * sizeof(GroupLds);
     }
@@ -2738,7 +2763,7 @@ uint32_t kernel_build_flags() {
 // the remaining knobs: occupancies, the queue's schedule and the numeric thresholds
 #if defined(RT_QUEUE_REFILL) || RT_QUEUE_SHARDS != 8 || RT_QUEUE_BLOCK_WAVES != 4 || RT_CAM_BATCH != 32 || \
     defined(RT_WAVES_PER_EU) || RT_BVH_WAVES != 4 || RT_SCAN_WAVES != 6 || RT_MED_WAVES != 6 || RT_NOSPH_WAVES != 7 || \
-    RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 5 || RT_BVH_MESH_WAVES != 5 || RT_PT_WAVES != 6 || \
+    RT_GROUP_WAVES != 5 || RT_BVH_SIMPLE_WAVES != 6 || RT_BVH_MESH_WAVES != 5 || RT_PT_WAVES != 6 || \
     RT_GROUP_MIN_TRIPS != 4 || RT_GROUP_EXIT_LANES != 8 || RT_BATCH_MIN != 64 || RT_GROUP_BATCH_MIN != 64 || \
     RT_PT_BATCH_MIN != 64 || RT_DEFER_MIN != 32 || defined(RT_U01_MULADD)
     f |= 4u;  // RT_BUILD_AB: same results, not the shipped schedule
@@ -2762,7 +2787,8 @@ hipError_t launch_render(uint32_t variant, const SceneArgs& sc, const CamRec* ca
                          unsigned long long* counters, hipStream_t stream, hipEvent_t main_done) {
     const int bw = block_waves(L.queue != 0);
     const dim3 block(64 * bw);
-    const size_t lds = stack_bytes(L, bw, kStackSpare);
+    const bool slim = variant == RT_VARIANT_BVH_MESH_QUEUE || variant == RT_VARIANT_BVH_MESH_SIMPLE_QUEUE;
+    const size_t lds = stack_bytes(L, bw, slim ? stack_spare<1>() : stack_spare<3>());
     dim3 grid;
     if (L.queue) {
         if (L.n_items == 0) return main_done ? hipEventRecord(main_done, stream) : hipSuccess;
