@@ -461,20 +461,13 @@ __device__ __forceinline__ const RenderLaunch& launch_args() {
     return *reinterpret_cast<const RenderLaunch*>((const char*)p);
 }
 
-// The batched mesh traversal over child-pair records (rt_scene.cpp build_mesh_pairs). A lane
-// holds one reference word instead of a node: a pair index, whose 64 B record carries both
-// children's boxes and references, or a leaf reference (first triangle, count). An inner
-// step is one aligned 64 B load and two box tests; the nearer hit child becomes the lane's
-// reference and the farther one is pushed as a word. Popping, stealing and reaching a leaf
-// load nothing: a leaf's triangles are queued for the wave's batched tests (up to three per
-// trip; a larger leaf keeps its lane for more trips) in the same trip that reached it, and
-// whenever 64 pairs are queued the whole wave tests them at once - one pair per lane, the
-// triangle loads of all 64 in flight together - merging each accepted hit into its ray's LDS
-// minimum of (t, mesh-local index); lanes then re-read their ray's minimum as the pruning
-// bound. (Superseded in round 3 and removed in round 4: per-lane traversal, node records
-// re-tested at every pop, per-lane leaf loops) A popped entry is not re-tested against the improved bound
-// (its children are, on their pair load); pruning stays conservative, so the candidate set
-// still contains the sequential scan's winner and the (t, index) minimum picks it.
+// The batched mesh traversal over quantized child-pair records (rt_scene.h QPair). A lane holds one reference
+// word: a pair index (one 32 B load, two box tests; the nearer hit child becomes the reference, the farther
+// is pushed) or a leaf reference (first triangle, count), whose triangles are queued - up to three per trip -
+// for the wave's batched tests: once 64 pairs are queued the wave tests them one per lane, merging accepted
+// hits into each ray's LDS minimum of (t, mesh-local index), which is then the lanes' pruning bound. Idle
+// lanes steal the oldest pending subtree of another ray. Pruning is conservative, so the candidate set holds
+// the sequential scan's winner and the (t, index) minimum picks it.
 __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
                                                const uint32_t* __restrict__ tri_orig,
                                                const BvhNode* __restrict__ nodes, uint32_t root, uint32_t frame,
@@ -649,20 +642,14 @@ __device__ __forceinline__ ObjRec load_obj(const ObjRec* __restrict__ objs, int 
     return r;
 }
 
-// A run of g consecutive brute-force meshes with the same triangle count m (instances
-// of one model; rt_scene.cpp stores g in the first record's f[7], 0 in the others)
-// compacted together: the rays wanting each mesh (box early-out, TriangleMesh.cu:34-38)
-// are listed one after the other as ray slots (lane, the mesh's triangle base), and the
-// slot x triangle pairs of the whole run are packed densely over the 64 lanes,
-// backface-culled, then fully tested in batches of 64. One partial batch per run instead of one per mesh. Triangles of
-// consecutive meshes are consecutive in `tris` (their bases rise with scan order), so
-// the per-lane minimum of (t, global triangle index) over the run is the candidate the
-// sequential hit() keeps: smallest t, then the earliest mesh, then its lowest triangle.
-// `skip`: the object index of a convex mesh the lane's ray starts on and leaves (render_kernel, the convex-shell skip;
-// -1: none): its triangles cannot accept the ray (rt_scene.cpp convex_shell), so the lane takes no ray slot
-// for it. The event counters still count the reference's AABB passes and triangle tests.
-// kLin (the linear-scan kernels): the branch-free cull loop and 1 / det through tri_rcp. In the BVH kernels
-// both cost registers (the sphere-group kernel spilled), so those keep the exec-mask form.
+// A run of g consecutive brute-force meshes with the same triangle count m (rt_scene.cpp: g in the first
+// record's f[7]) compacted together: the rays wanting each mesh (box early-out, TriangleMesh.cu:34-38) are
+// listed as ray slots (lane, the mesh's triangle base), and the run's slot x triangle pairs are packed over the
+// 64 lanes, backface-culled, then fully tested in batches of 64. The run's triangles are consecutive in
+// `tris`, so the per-lane minimum of (t, global triangle index) is what the sequential hit() keeps. `skip`: a
+// convex mesh the lane's ray starts on and leaves (-1: none; rt_scene.cpp convex_shell) takes no ray slot; the
+// counters still count the reference's AABB passes and tests. kLin (the linear-scan kernels): the branch-free
+// cull loop and tri_rcp's 1 / det (the BVH kernels keep the exec-mask form: registers).
 template <bool kOrdered, bool kLin>
 __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
                                          int i0, uint32_t g, uint32_t m, uint32_t magic, bool live, v3 o, v3 d,
@@ -785,13 +772,10 @@ __device__ __forceinline__ float sphere_candidate(const ObjRec& ob, v3 o, v3 d, 
 #ifndef RT_GROUP_EXIT_LANES
 #define RT_GROUP_EXIT_LANES 8  // the wave leaves once at most this many lanes still traverse
 #endif
-// kResume (the sphere-group-only kernel): once at most RT_GROUP_EXIT_LANES lanes of
-// the wave are still traversing (after RT_GROUP_MIN_TRIPS trips), the wave stops: it tests the pairs it
-// has queued, and the unfinished lanes keep their state in `gl` and skip shading. In the next loop trip
-// they resume, while the lanes that finished shade and start their next segments, which then traverse
-// beside them. A wave would otherwise run every trip until its deepest ray is done, with the other
-// lanes idle. A resumed lane re-scans the objects before the group (the same closestSoFar), keeps its
-// (t, ~order) minimum and prunes against it, so its candidate set and result are the single pass's.
+// kResume (the sphere-group-only kernel, no media: select_variant): once at most RT_GROUP_EXIT_LANES lanes still
+// traverse (after RT_GROUP_MIN_TRIPS trips) the wave tests its queued pairs and leaves; unfinished lanes keep their
+// state in `gl`, skip shading and resume next trip beside the new segments. A resumed lane re-scans the objects
+// before the group (the same closestSoFar) and prunes against its kept minimum: the single pass's result.
 template <bool kResume>
 __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ objs,
                                                      const BvhNode* __restrict__ nodes, uint32_t root,
@@ -814,9 +798,6 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
     constexpr uint32_t kQ = (uint32_t)kMaxRun * 64u;
     __builtin_amdgcn_wave_barrier();
     auto batch = [&](uint32_t count) {
-#ifdef RT_STAMPS_GROUP  // diagnostic: full and partial member batches timed apart (slots 0 and 7), partial pairs (5)
-        RT_STAMP(b0);
-#endif
         const bool act = (uint32_t)lane < count;
         const uint32_t e = act ? W.slot[(qdone + (uint32_t)lane) & (kQ - 1)] : 0u;
         const uint32_t k = e >> 6;
@@ -839,15 +820,6 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
         if (mine != ~0ull && K[own] == mine) SRC[own] = (int32_t)k;  // (t, order) is unique
         qdone += count;
         __builtin_amdgcn_wave_barrier();
-#ifdef RT_STAMPS_GROUP
-        RT_STAMP(b1);
-        if (count == 64u) {
-            tm[0] += b1 - b0;
-        } else {
-            tm[7] += b1 - b0;
-            tm[5] += count;
-        }
-#endif
     };
     for (int trip = 0;; ++trip) {
         const uint64_t bm = __ballot(has || sp > 0);
@@ -1718,9 +1690,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             tail_steal(L, W, lane, SP, alive, waiting, held, towner, tl_pack, own_end, s, item, sum, thr, need_cam);
         if (__ballot(alive || waiting || held || (kQueue && !exhausted)) == 0) break;  // wave-uniform exit
         RT_STAMP(t_a);
-#ifndef RT_STAMPS_GROUP
         RT_ACC(7, t_q, t_a);
-#endif
         if constexpr (kCamPf) {
             // Camera slots. A lane starting a sample takes it from its slot when it was prepared;
             // the camera pass (Philox seeding, getRay's draws and arithmetic) runs when some lane
@@ -1794,14 +1764,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         const bool live = alive && !need_cam;
         if constexpr (kDef) W.grp_s[lane] = (W.grp_s[lane] >> 1) & 1u;  // bit 0: deferred on the last trip
         RT_STAMP(t_b);
-#ifndef RT_STAMPS_GROUP
         RT_ACC(0, t_a, t_b);
-#endif
 #ifdef RT_STAMPS
         tm[4] += 1;                                  // loop trips (per wave)
-#ifndef RT_STAMPS_GROUP
         tm[5] += (uint64_t)__popcll(__ballot(live));  // lanes tracing a segment this trip
-#endif
         if (!kBvh) tm[6] += (uint64_t)__popcll(__ballot(valid)); // lanes that own a pixel (BVH kernels: slot 6 counts traversal lanes)
 #endif
 
@@ -2156,19 +2122,13 @@ struct PtBest {
     v3 hit;
 };
 
-// BVH_IntersectTriangles (CUDAPathTracer.cu:192-352) as a cooperative ordered traversal over
-// child-pair records (rt_bvh.cpp cf_child_pairs). The result is the minimum over (distance^2,
-// DFS list position) of the triangles in the leaves the reference reaches: every inner box gets
-// the reference's exact decision (pt_box_decide), leaf boxes are never box-tested (the child
-// record says which boxes are leaves'), and a subtree is skipped only when every point of its
-// eps-widened box lies beyond the best hit. Children are tested at their parent and the nearer
-// is descended first, which changes the order but not the set of candidates that can win.
-// Lanes without a subtree take the oldest pending subtree of a lane that has a spare one, with
-// its ray and pruning bound (as mesh_bvh_pairs). Leaves append (DFS list
-// position, ray owner) pairs to a per-wave LDS queue, three per lane and trip, and the wave
-// runs the Kuchkuda triangle test (CUDAPathTracer.cu:258-345) on 64 queued pairs at once, one per lane, each merged into its
-// ray's LDS minimum of (distance^2, list position) - the reference's first-in-DFS tie rule.
-// Pairs take their ray (origin, direction, avoidSelf) from the owner lane's registers.
+// BVH_IntersectTriangles (CUDAPathTracer.cu:192-352) as a cooperative ordered traversal over child-pair
+// records (rt_bvh.cpp cf_child_pairs): the minimum over (distance^2, DFS list position) of the triangles in the
+// leaves the reference reaches. Inner boxes get the reference's exact decision (pt_box_decide), leaf boxes are
+// never box-tested, and a subtree is skipped only when its eps-widened box lies beyond the best hit. Idle lanes
+// steal pending subtrees (as mesh_bvh_pairs); leaves queue (list position, owner) pairs, and the wave runs the
+// Kuchkuda test (CUDAPathTracer.cu:258-345) on 64 at once, merging into each ray's LDS minimum - the
+// reference's first-in-DFS tie rule.
 __device__ __forceinline__ void pt_traverse_coop_batched(const KTri* __restrict__ ktris,
                                                          const CFNode* __restrict__ nodes, uint32_t* wstack,
                                                          unsigned long long* keys, int32_t* vlist, uint32_t* queue,

@@ -1,8 +1,6 @@
 #!/bin/bash
 # Extra same-box steps after tools/gpu_session.sh (round 6), into gpurun_out/$TAG/:
 #   SHARD_ALT   libraries run beside the in-tree one at bench.py --rehearse-shard 8 (3 contexts), REPS rounds
-#   STAMPSG     tools/stamps_breakdown.py of these workloads with librtmi_stampsg.so (RT_STAMPS_GROUP build:
-#               sphere-group member batches, full vs partial)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${TAG:-session}
@@ -25,9 +23,5 @@ if [ "${GATHER_AB:-0}" = "1" ]; then  # rehearse-shard 8 with and without the or
     RTMI_GATHER_ORDER=0 timeout -k 10 180 python bench.py --rehearse-shard 8 --contexts 3 --steps 60 --warmup 6 --no-cpu-baseline > "$O/shard8_c3_order0_r$rep.log" 2>&1
     stop_if_fatal $? shard8_c3_order0_r$rep
   done
-fi
-if [ -n "${STAMPSG:-}" ] && [ -f raytracingthenextweekcuda_amd/librtmi_stampsg.so ]; then
-  STAMPS_GROUP=1 RTMI_LIB=raytracingthenextweekcuda_amd/librtmi_stampsg.so timeout -k 10 300 python tools/stamps_breakdown.py $STAMPSG > "$O/stamps_group.log" 2>&1
-  stop_if_fatal $? stamps_group
 fi
 echo done_extra

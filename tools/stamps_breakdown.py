@@ -33,11 +33,6 @@ for scene in sys.argv[1:] or ["cornellbox1"]:
         if bvh and k == 3:
             continue
         print(f"  {name:28s} {d[k] / tot:6.3f} of stamped cycles, {d[k] / trips:8.1f} cycles per wave-trip")
-    if os.environ.get("STAMPS_GROUP") == "1":  # the RT_STAMPS_GROUP build: slots 0 / 7 / 5 are the member batches
-        cl = max(d[1], 1)
-        print(f"  sphere-group member batches: full {d[0] / cl:6.3f} of closest-hit cycles ({d[0] / trips:8.1f} per "
-              f"wave-trip), partial {d[7] / cl:6.3f} ({d[7] / trips:8.1f} per wave-trip), partial-batch fill "
-              f"{d[5] / 64 / max(trips, 1):.3f} x 64 pairs per wave-trip")
     if bvh and d[3]:
         print(f"  BVH traversal: {d[3] / trips:.1f} loop trips per wave-trip, lane utilisation "
               f"{d[6] / (64 * d[3]):.3f} (lanes with a subtree or stack entry per trip)")
