@@ -897,27 +897,54 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
 // ConstantMedium::hit calls random_double(); the scan visits media in slot order,
 // so the draw order is the sequential hit()'s. Returns the scattering distance t,
 // or NaN.
-__device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, Rng& rng) {
+__device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, v3 inv, Rng& rng) {
     const float* f = ob.f;
     // blo = center - extend, bhi = center + extend (rt_scene.cpp, the restatement's p.a -/+ e.a):
     // faces at blo.x, bhi.x, bhi.y, blo.y, bhi.z, blo.z in createCube's order (kernels.h:139-154)
     const v3 blo{f[0], f[1], f[2]}, bhi{f[3], f[4], f[5]};
     float tf[6];
     bool ok[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        // Plane::hit with the face's unit normal +-e_a (a = k / 2): dot(n, d) is +-d_a and
-        // dot(p - o, n) is +-(p_a - o_a) - the zero terms only decide the sign of a zero,
-        // which no test below can see (the faces count only when |d_a| > tMin; ray origins
-        // and directions are finite, or all NaN) - and (-x) / (-y) = x / y, so
-        // t = (p_a - o_a) / d_a is the restatement's quotient bit for bit.
+    // face k: the axis a = k / 2 and its plane coordinate, in createCube's order
+    auto face = [&](int k, float& da, float& num, float& ia) {
         const int a = k >> 1;
         const bool high = (k == 1) | (k == 2) | (k == 4);
-        const float da = a == 0 ? d.x : (a == 1 ? d.y : d.z);
+        da = a == 0 ? d.x : (a == 1 ? d.y : d.z);
         const float oa = a == 0 ? o.x : (a == 1 ? o.y : o.z);
         const float pa = a == 0 ? (high ? bhi.x : blo.x) : (a == 1 ? (high ? bhi.y : blo.y) : (high ? bhi.z : blo.z));
-        const float den = da;
-        const float t = fdiv(pa - oa, da);
+        num = pa - oa;
+        ia = a == 0 ? inv.x : (a == 1 ? inv.y : inv.z);
+    };
+    // Plane::hit with the face's unit normal +-e_a: dot(n, d) is +-d_a and dot(p - o, n) is +-(p_a - o_a) - the
+    // zero terms only decide the sign of a zero, which no test below can see (the faces count only when
+    // |d_a| > tMin; ray origins and directions are finite, or all NaN) - and (-x) / (-y) = x / y, so
+    // t = (p_a - o_a) / d_a is the restatement's quotient bit for bit. It is RN((p_a - o_a) / d_a) by Markstein's
+    // correction with the ray's RN(1 / d_a) (rcp_exact; round 6) for |p_a - o_a| in [2^-100, 2^100) on the faces
+    // that count: their |d_a| lies in (tMin, 2) (this kernel's directions are unit vectors, metal's reflection
+    // plus a fuzz below 1, or isotropic draws inside the unit ball), which keeps the quotient in Markstein's
+    // domain. A wave with a counting face outside it (a zero or tiny numerator: the sign of a zero t must be the
+    // IEEE one) recomputes all six with the IEEE division.
+    bool slow = false;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        float da, num, ia;
+        face(k, da, num, ia);
+        tf[k] = div_y(num, da, ia);
+        // |num| in [2^-100, 2^100) iff bits(|num|) - bits(2^-100) < bits(2^100) - bits(2^-100) (unsigned)
+        slow = slow | ((fabsf(da) > kTMin) & ((__float_as_uint(num) & 0x7FFFFFFFu) - 0x0D800000u >= 0x64000000u));
+    }
+    if (__builtin_expect(__ballot(slow) != 0, 0)) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            float da, num, ia;
+            face(k, da, num, ia);
+            tf[k] = fdiv(num, da);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const int a = k >> 1;
+        const float den = a == 0 ? d.x : (a == 1 ? d.y : d.z);
+        const float t = tf[k];
         const v3 q = add(o, scale(d, t));
         bool in;
         if (k < 2)  // YZ faces
@@ -927,7 +954,6 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
         else  // XY faces
             in = (q.x > blo.x) & (q.x < bhi.x) & (q.y > blo.y) & (q.y < bhi.y);
         ok[k] = (fabsf(den) > kTMin) & in;
-        tf[k] = t;
     }
     // rec1 = boundary.hit(-inf, inf); rec2 = boundary.hit(rec1.t + 0.0001, inf)
     bool f1 = false, f2 = false;
@@ -984,18 +1010,21 @@ __device__ __forceinline__ float axis(v3 v) {
 // o_A or o_B) these are not, but then the hit point's coordinate on that axis, o_A + d_A * t, is NaN or
 // infinite and fails the open bounds test: the candidate is NaN (none) in both forms.
 template <int K, int A, int B>
-__device__ __forceinline__ float plane_axial(const ObjRec& ob, v3 o, v3 d) {
+__device__ __forceinline__ float plane_axial(const ObjRec& ob, v3 o, v3 d, v3 inv) {
     const float* f = ob.f;
     const float nk = f[3 + K];
     const float den = nk * axis<K>(d);
     // twoSide ? |den| > tMin : den > tMin, with u1 = the bits of 1.0f (two-sided) or 0 (rt_scene.cpp):
     // max(|den| * 1, den) = |den|; max(|den| * 0, den) > tMin iff den > tMin (+0 or NaN against den,
     // and fmaxf returns den for a NaN first operand); a NaN den fails both. No scalar select.
-    const float num = (f[K] - axis<K>(o)) * nk;
-    // t matters only where proceed holds (then |den| > tMin): a wave with any |num| or |den| >= 2^100
-    // takes the IEEE division (closest_hit's general plane argues the domain)
-    float t = div_y(num, den, rcp_nr(den));
-    if (__builtin_expect(__ballot(!(fmaxf(fabsf(num), fabsf(den)) < 0x1p100f)) != 0, 0)) t = fdiv(num, den);
+    // t = ((p_k - o_k) nk) / (nk d_k) with nk = +-1 is (p_k - o_k) / d_k exactly (IEEE division and
+    // Markstein's correction are odd in the signs of both operands), and the ray's inverse direction
+    // (rcp_exact: RN(1 / d_k) wherever |d_k| > tMin) is the reciprocal Markstein needs: no reciprocal per plane
+    // (round 6). t matters only where proceed holds (then |den| > tMin): a wave with any |num| or |den| >=
+    // 2^100 takes the IEEE division (closest_hit's general plane argues the domain)
+    const float num = f[K] - axis<K>(o);
+    float t = div_y(num, axis<K>(d), axis<K>(inv));
+    if (__builtin_expect(__ballot(!(fmaxf(fabsf(num), fabsf(den)) < 0x1p100f)) != 0, 0)) t = fdiv(num, axis<K>(d));
     const float pa = axis<A>(o) + axis<A>(d) * t;
     const float pb = axis<B>(o) + axis<B>(d) * t;
     // The six conditions as one compare: each is a difference that is > 0 exactly when it holds
@@ -1043,11 +1072,11 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
         const uint32_t ty = ob.type;
         auto is = [&](uint32_t k) { return ty == k; };
         if (is(kObjPlaneAxial + 2)) {
-            cand(plane_axial<1, 0, 2>(ob, o, d), false);  // XZ
+            cand(plane_axial<1, 0, 2>(ob, o, d, inv), false);  // XZ
         } else if (is(kObjPlaneAxial + 1)) {
-            cand(plane_axial<0, 1, 2>(ob, o, d), false);  // YZ
+            cand(plane_axial<0, 1, 2>(ob, o, d, inv), false);  // YZ
         } else if (is(kObjPlaneAxial)) {
-            cand(plane_axial<2, 0, 1>(ob, o, d), false);  // XY
+            cand(plane_axial<2, 0, 1>(ob, o, d, inv), false);  // XY
         } else if (is_plane(ob.type)) {
             // Plane::hit (Plane.cu:4-52); t is only used when `proceed` holds.
             const v3 nrm{f[3], f[4], f[5]};
@@ -1114,7 +1143,7 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
         } else if ((kMed || (kBvh && kSph)) && ob.type == kObjMedium) {
             // (the general linear-scan kernel never sees a medium: launch_render sends scenes with
             // media to the kMed variant, so its register allocation need not cover this test)
-            cand(live ? medium_candidate(ob, o, d, rng) : __builtin_nanf(""), false);
+            cand(live ? medium_candidate(ob, o, d, inv, rng) : __builtin_nanf(""), false);
         } else if (kBvh && (kParts & 2) != 0) {  // kObjSphereGroup
             sphere_group_batched<kBvh && kParts == 2>(S.objs, S.nodes, __float_as_uint(ob.f[8]), live,
                                                                          ray, inv, inva, h, stack - lane, W, lane, cnt,
