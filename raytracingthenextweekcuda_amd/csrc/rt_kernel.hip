@@ -1185,6 +1185,29 @@ __device__ __forceinline__ const T* opaque(const T* p) {
     return p;
 }
 
+// normalize(a) (LinearAlgebra.h:69-72) by Markstein quotients (round 6, the camera's ray): RN(c / n) for every
+// component c that is +0 or at least 2^-100 in magnitude when the norm n lies in [2^-100, 2^20) (the quotient
+// is then in Markstein's domain; +0 / n gives +0 as IEEE does). A wave with a lane outside - a -0 component
+// (Markstein's correction would return +0), a tiny one, or an extreme norm - takes the IEEE divisions.
+__device__ __forceinline__ v3 normalize_mk(v3 a) {
+    const float n = fsqrt(a.x * a.x + a.y * a.y + a.z * a.z);
+    const float y = rcp_nr(n);
+    v3 r{div_y(a.x, n, y), div_y(a.y, n, y), div_y(a.z, n, y)};
+    const uint32_t bx = __float_as_uint(a.x), by = __float_as_uint(a.y), bz = __float_as_uint(a.z);
+    // |c| in (0, 2^-100) iff bits(|c|) - 1 < bits(2^-100) - 1 (unsigned; +0 wraps); c = -0 iff bits ^ sign = 0
+    const uint32_t tiny = __builtin_elementwise_min(
+        __builtin_elementwise_min((bx & 0x7FFFFFFFu) - 1u, (by & 0x7FFFFFFFu) - 1u), (bz & 0x7FFFFFFFu) - 1u);
+    const uint32_t mz = __builtin_elementwise_min(__builtin_elementwise_min(bx ^ 0x80000000u, by ^ 0x80000000u),
+                                                  bz ^ 0x80000000u);
+    const bool ieee = (tiny < 0x0D7FFFFFu) | (mz == 0u) | !((n >= 0x1p-100f) & (n < 0x1p20f));
+    if (__builtin_expect(__ballot(ieee) != 0, 0))
+        if (ieee) r = normalize(a);
+    return r;
+}
+
+// kMk: the camera ray normalized by normalize_mk (the linear-scan kernels, whose camera pass runs batched from
+// the camera slots; in the traversal kernels the extra live values spilled the sphere-group kernel).
+template <bool kMk = false>
 __device__ __forceinline__ Ray camera_sample(const CamRec* camp, const RenderLaunch& L, Rng& rng,
                                              uint32_t pixel, int px, int y, int s, float fw, float fh) {
     const CamRec cam = *opaque(camp);
@@ -1200,7 +1223,7 @@ __device__ __forceinline__ Ray camera_sample(const CamRec* camp, const RenderLau
     const v3 offset = add(scale(cam.right, rnd.x), scale(cam.true_up, rnd.y));
     const v3 norig = add(cam.origin, offset);
     v3 dir = sub(add(add(cam.lower_left, scale(cam.horizontal, dx)), scale(cam.vertical, dy)), norig);
-    dir = normalize(dir);
+    dir = kMk ? normalize_mk(dir) : normalize(dir);
     const float tm = random_range(rng, cam.time0, cam.time1);
     return Ray{add(cam.origin, offset), dir, tm};
 }
@@ -1745,7 +1768,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                         pixel = (uint32_t)y * (uint32_t)L.width + (uint32_t)px;
                     }
                     Rng r2{1u, 0u, 0u, 0u};
-                    const Ray cr = camera_sample(cam, L, r2, pixel, px, y, now ? s : ns, (float)(L.width - 1),
+                    const Ray cr = camera_sample<true>(cam, L, r2, pixel, px, y, now ? s : ns, (float)(L.width - 1),
                                                  (float)(L.height - 1));
                     C.a[lane] = float4{cr.o.x, cr.o.y, cr.o.z, cr.d.x};
                     C.b[lane] = float4{cr.d.y, cr.d.z, cr.time, __uint_as_float(r2.s0)};
