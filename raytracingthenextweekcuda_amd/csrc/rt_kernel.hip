@@ -1,39 +1,27 @@
-// rt_kernel.hip — the per-pixel path-tracing megakernel for gfx950 (MI355X).
+// rt_kernel.hip — the per-pixel path-tracing megakernels for gfx950 (MI355X).
 //
-// Replaces renderKernel (main.cu:160-206) + rayColor (main.cu:63-94) + hit
-// (main.cu:43-57) + the Hitable/Material virtual calls (Sphere.cu, Plane.cu,
-// Cube.cu, TriangleMesh.cu, AABBox.h, Material.h/.cu) + Camera::getRay
-// (Camera.h:151-168) + cuRAND (main.cu:120-129) with one hand-written kernel.
+// Replaces renderKernel (main.cu:160-206) + rayColor (main.cu:63-94) + hit (main.cu:43-57) + the Hitable /
+// Material virtual calls (Sphere.cu, Plane.cu, Cube.cu, TriangleMesh.cu, AABBox.h, Material.h/.cu) +
+// Camera::getRay (Camera.h:151-168) + cuRAND (main.cu:120-129), and pathTrace (CUDAPathTracer.cu:358-622).
 //
 // Execution model:
-//  * a persistent grid takes work items (pixel, sub-stream of S = lanes_per_pixel)
-//    from 8 sharded queue heads (one per XCD band), one atomic per wave once
-//    L.refill lanes are idle (4 or 8, chosen per launch); each lane folds its
-//    sub-stream's samples in order and stores a partial sum, and combine_kernel
-//    sums a pixel's S partials in a fixed order (the static grid,
-//    rt_render_params.schedule = RT_SCHEDULE_STATIC, computes the same sums);
-//  * path regeneration: a lane whose path terminates starts its next sample in
-//    the same loop trip, so lanes stay busy until their last sample; once the
-//    queue is dry, idle lanes trace other lanes' last samples (tail stealing);
-//  * the main loop is wave-uniform (exits on an empty __ballot of live lanes),
-//    so the whole wave is available for cooperative work inside a trip;
-//  * small meshes (the reference's brute-force TriangleMesh) are tested with
-//    two-phase ballot compaction over runs of equal meshes: the (ray, triangle)
-//    pairs of the lanes whose rays hit a mesh box are packed densely over all 64
-//    lanes, backface-culled, then fully tested in batches; per-ray results merge
-//    with a 64-bit LDS atomic-min on (t, triangle index);
-//  * large meshes, sphere groups and the pathTrace triangles use the reference's
-//    binned-SAH BVH (BVH.cpp) over child-pair records, with per-lane traversal
-//    stacks in LDS (sized per scene, lane i always on bank i), cooperative
-//    traversal (idle lanes steal pending subtrees) and leaf tests deferred to
-//    wave-wide batches; per-ray minima merge by LDS atomic-min;
-//  * scene records of the closest-hit scan are read at wave-uniform addresses
-//    (scalar loads broadcast to 64 lanes); materials/nodes per lane;
-//  * counter-based RNG (rt_math.h): no init kernel and no RNG state in HBM.
+//  * a persistent grid takes work items (pixel, sub-stream of S = lanes_per_pixel) from 8 sharded queue heads
+//    (one per XCD band), one atomic per wave once L.refill lanes are idle; each lane folds its sub-stream's
+//    samples in order and stores a partial sum, and combine_kernel sums a pixel's S partials in a fixed order
+//    (the static grid, RT_SCHEDULE_STATIC, computes the same sums);
+//  * path regeneration: a lane whose path ends starts its next sample in the same loop trip; once the queue is
+//    dry, idle lanes trace other lanes' last samples (tail stealing);
+//  * the main loop is wave-uniform (it exits on an empty __ballot), so the whole wave can cooperate in a trip;
+//  * small meshes (the reference's brute-force TriangleMesh) are tested by two-phase ballot compaction over runs
+//    of equal meshes; per-ray results merge with a 64-bit LDS atomic-min on (t, triangle index);
+//  * large meshes, sphere groups and the pathTrace triangles use the reference's binned-SAH BVH (BVH.cpp) over
+//    child-pair records (quantized for meshes), with per-lane LDS stacks, cooperative traversal (idle lanes
+//    steal pending subtrees) and leaf tests deferred to wave-wide batches;
+//  * scan records are read at wave-uniform addresses (scalar loads); counter-based RNG (rt_math.h).
 //
-// Numerics: compiled with -ffp-contract=off and IEEE div/sqrt; every expression
-// keeps the reference's evaluation order (rt_math.h), so the output is
-// bit-identical to the CPU restatement in oracle/.
+// Numerics: compiled with -ffp-contract=off and IEEE div/sqrt (fast paths only where they give the same bits);
+// every expression keeps the reference's evaluation order (rt_math.h): the output is bit-identical to the CPU
+// restatement in oracle/.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -57,7 +45,6 @@ constexpr int kWavesPerBlock = 4;  // static-grid blocks: 2 x 2 wave tiles
 constexpr int kQueueBlockWaves = RT_QUEUE_BLOCK_WAVES;
 static_assert(kQueueBlockWaves == 1 || kQueueBlockWaves == 2 || kQueueBlockWaves == 4, "queue block waves");
 constexpr int block_waves(bool queue) { return queue ? kQueueBlockWaves : kWavesPerBlock; }
-
 
 struct Ray {
     v3 o, d;
@@ -103,9 +90,8 @@ __device__ __forceinline__ bool node_hit(const BvhNode& n, v3 o, v3 inv, float t
 // The mesh traversal's slab terms on a QPair grid (rt_scene.h): the plane c + q s of axis a is entered at
 // t(q) = fma(q, A_a, B_a) with A = s * inv (exact: s is a power of two) and B = (c - o) * inv, once per ray.
 // |t(q) - (c + q s - o) inv| <= 2^-22 (|B_a| + kQMax |A_a|) for every grid coordinate q <= kQMax (two roundings
-// in B, one in the fma); E is 4x that bound over the axes, and qpair_hit widens the interval by it, so the
-// test accepts every ray whose exact slab interval meets the grid box - which contains the inflated float
-// box of round 5's 64 B pairs. (inv = +-inf makes A, B, E infinite or NaN: that axis then never culls.)
+// in B, one in the fma); E is 4x that bound over the axes and qpair_hit widens the interval by it, so it accepts
+// every ray whose exact slab interval meets the grid box, which contains round 5's inflated float box.
 struct QRay {
     v3 A, B;
     float E;
@@ -163,9 +149,7 @@ __device__ __forceinline__ v3 moving_center(const float* f, float time) {
     return add(c0, scale(sub(c1, c0), (time - f[6]) / (f[7] - f[6])));
 }
 
-// Deferred leaf tests run when this many pairs are queued (64: full batches only). Fewer flushes a partial
-// batch earlier, so the rays' pruning bounds tighten sooner (fewer node visits) at the price of idle lanes
-// in the batch (A/B).
+// Deferred leaf tests run when this many pairs are queued (64: full batches; fewer measured slower).
 #ifndef RT_BATCH_MIN
 #define RT_BATCH_MIN 64  // mesh_bvh_pairs
 #endif
@@ -199,7 +183,10 @@ __device__ __forceinline__ float tri_accept(float t, float b1, float b2) {
     return m > 0.0f ? t : __builtin_nanf("");
 }
 
-// RN(1 / b) for |b| in [2^-126, 2^126); Markstein's RN(a / b) from it (callers bound the domain)
+// Correctly rounded reciprocal and quotient without the IEEE division expansion (11 VALU): v_rcp_f32 + one Newton
+// step is RN(1/b) for every 2^-126 <= |b| < 2^126 (exhaustive GPU check, tools/div_check.hip), and Markstein's
+// q0 + r y with that y is RN(a/b) for |a|, |b| in [2^-100, 2^101) and |a/b| in [2^-121, 2^125). Callers use them
+// only where the operands provably lie there, or fall back to the IEEE division for the wave.
 __device__ __forceinline__ float rcp_nr(float b) {
     const float y0 = __builtin_amdgcn_rcpf(b);
     return __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
@@ -254,13 +241,10 @@ __device__ __forceinline__ float tri_t_culled(const TriRec& tr, v3 o, v3 d) {
     return tri_accept(t, b1, b2);
 }
 
-// Closest-hit state with the reference's sequential tie rule (hit(),
-// main.cu:43-57, each object called with tMax = closestSoFar): planes and
-// triangles accept t < closestSoFar, spheres t <= closestSoFar (Sphere.cu:25).
-// Among candidates at the minimal t the lowest scan order wins, unless a
-// sphere of higher order is also at that t: then the highest-order such sphere
-// wins. Merging candidates in any order with this rule reproduces the
-// sequential scan, which lets BVHs visit objects out of order.
+// Closest-hit state with the reference's sequential tie rule (hit(), main.cu:43-57, each object called with
+// tMax = closestSoFar): planes and triangles accept t < closestSoFar, spheres t <= closestSoFar (Sphere.cu:25).
+// At the minimal t the lowest scan order wins, unless a higher-order sphere is also there (then the highest such
+// sphere). Merging candidates in any order with this rule reproduces the sequential scan.
 struct Hit {
     float t;
     int32_t obj;     // winner so far by lowest order (-1: none)
@@ -318,14 +302,12 @@ struct Hit {
 };
 
 constexpr int kMaxRun = (int)kMeshRunMax;  // meshes per run (rt_scene.cpp marks the runs)
-// The render kernels' traversal stacks hold L.stack_depth entries per lane (the scene's deepest path in
-// pair records, rt_scene.cpp PairBuilder::max_pairs), PLUS one spare slot in kernels that traverse sphere
-// groups: a lane that does not push writes its would-be entry to slot stack_cap = L.stack_depth
-// unconditionally (sphere_group_batched's lane selects), so that slot must exist in every lane's column.
-// mesh_bvh_pairs writes its would-be entry to W.src[lane] instead, dead between the trip's steal round and
-// the next (round 6: the mesh-BVH-only kernels need no spare slot). The kernel's stack base and the launch's
-// dynamic LDS size (stack_bytes) both count it; tests/test_fuzz_parity.py renders a chain BVH whose deepest
-// pair is reached with both children hit.
+// The render kernels' traversal stacks hold L.stack_depth entries per lane (the scene's deepest path in pair
+// records), PLUS one spare slot in kernels that traverse sphere groups: sphere_group_batched's non-pushing lanes
+// write their would-be entry to slot L.stack_depth (lane selects). mesh_bvh_pairs writes it to the lane's W.src
+// word instead, dead until the next trip's steal round, so the mesh-BVH-only kernels need no spare (round 6).
+// The kernel's stack base and the launch's LDS size (stack_bytes) both count it; tests/test_fuzz_parity.py
+// reaches the deepest pair of a chain BVH with both children hit.
 template <int kParts>
 constexpr int stack_spare() { return (kParts & 2) != 0 ? 1 : 0; }
 
@@ -354,12 +336,10 @@ struct GroupLds {
     uint32_t st[64];             // bit 31: pending; bit 8: `has`; bits 0-7: stack depth
 };
 
-// Event counters of one wave, laid out to keep the VGPR file free for the traversal:
-// amounts that differ per lane stay per lane (node visits, BVH-leaf triangle tests);
-// events counted at wave-uniform points (segments, mesh-box tests, brute-force
-// triangle tests) accumulate as wave-uniform scalars from ballots (SGPRs); the two
-// sphere-group counts share one VGPR (16 | 16 bits, drained to LDS every loop trip);
-// a stack overflow is a flag stored straight into the device counters.
+// Event counters of one wave, laid out to keep VGPRs free: per-lane amounts stay per lane (node visits, BVH-leaf
+// triangle tests); wave-uniform events (segments, mesh-box tests, brute-force triangle tests) are scalars from
+// ballots; the two sphere-group counts share one VGPR (16 | 16 bits, drained to LDS every trip); a stack
+// overflow is a flag stored straight into the device counters.
 struct Counters {
     uint32_t tri_tests, node_visits;     // per lane
     uint32_t grp;                        // per lane, this trip: spheres | moving spheres << 16
@@ -419,14 +399,6 @@ __device__ __forceinline__ float fresh_f32(float v) {
     asm volatile("" : "+v"(v));
     return v;
 }
-
-// Correctly rounded reciprocal and quotient without the IEEE division expansion (11 VALU):
-// v_rcp_f32 + one Newton step is RN(1/b) for every b with 2^-126 <= |b| < 2^126 (exhaustive GPU
-// check over all 4.2e9 such floats, tools/div_check.hip, profiles/r02/div_check.json), and
-// Markstein's correction q0 + r y with that y is RN(a/b) for |a|, |b| in [2^-100, 2^101) and
-// |a/b| in [2^-121, 2^125) (Markstein's theorem; the same check draws 4.3e9 random pairs of that
-// domain: no mismatch). Callers use them only where their operands provably lie in these domains,
-// or fall back to the IEEE division for the wave.
 
 // __shfl(v, src, 64) without HIP's lane-id arithmetic: ds_bpermute reads lane (address / 4) mod 64,
 // the same lane __shfl picks. HIP's version derives its own lane id (mbcnt) for the width mask,
@@ -616,7 +588,6 @@ __device__ __forceinline__ void mesh_bvh_pairs(const TriRec* __restrict__ tris,
     __builtin_amdgcn_wave_barrier();
 }
 
-
 // One object record (64 B) as a single wave-uniform scalar load; the same
 // helper serves per-lane loads of sphere-group members.
 __device__ __forceinline__ ObjRec load_obj(const ObjRec* __restrict__ objs, int i) {
@@ -756,16 +727,12 @@ __device__ __forceinline__ float sphere_candidate(const ObjRec& ob, v3 o, v3 d, 
     return sphere_root(o, d, c, r, kTMin, kInf, t, inva) ? t : __builtin_nanf("");
 }
 
-// Sphere group: the object BVH over the scene's spheres (members are ObjRecs stored after the
-// scan list, in leaf order), over child-pair records with deferred leaf tests (as
-// mesh_bvh_pairs, without stealing): the traversal
-// loop is wave-uniform, and lanes at a leaf queue (member, ray owner) pairs that the wave tests
-// 64 at a time. Every group member is a sphere, and among spheres at the same t the sequential
-// hit() keeps the one of highest scan order (the inclusive test, Sphere.cu:25), which also
-// wins against any other object at that t (Hit::finish). So one LDS minimum per ray of
-// (t, ~order) over the accepted members (t <= the ray's closestSoFar) is all the group adds
-// to the ray's Hit: merging that one candidate gives what merging every member would. The
-// lane whose pair set the final minimum records the member (orders are unique) in W.src.
+// Sphere group: the object BVH over the scene's spheres (members are ObjRecs after the scan list, in leaf order)
+// over float child-pair records with deferred leaf tests (as mesh_bvh_pairs, without stealing): lanes at a leaf
+// queue (member, ray owner) pairs that the wave tests 64 at a time. Among spheres at the same t the sequential
+// hit() keeps the highest scan order (Sphere.cu:25's inclusive test), which also wins against any other object
+// at that t (Hit::finish); so one LDS minimum of (t, ~order) per ray over the accepted members is all the group
+// adds to the ray's Hit. The lane whose pair set the final minimum records the member in W.src.
 #ifndef RT_GROUP_MIN_TRIPS
 #define RT_GROUP_MIN_TRIPS 4   // traversal trips before the wave may leave it
 #endif
@@ -890,13 +857,10 @@ __device__ __forceinline__ void sphere_group_batched(const ObjRec* __restrict__ 
     __builtin_amdgcn_wave_barrier();
 }
 
-// Constant medium bounded by a cube (rt_constant_medium, rtmi.h; "Ray Tracing:
-// The Next Week" ConstantMedium::hit with the boundary = the six two-sided faces
-// of createCube, kernels.h:139-154, each tested like Plane::hit). A ray that
-// crosses the boundary draws its free-flight uniform from the sample's stream, as
-// ConstantMedium::hit calls random_double(); the scan visits media in slot order,
-// so the draw order is the sequential hit()'s. Returns the scattering distance t,
-// or NaN.
+// Constant medium bounded by a cube (rt_constant_medium, rtmi.h; "Ray Tracing: The Next Week"'s ConstantMedium::hit
+// with the boundary = createCube's six two-sided faces, kernels.h:139-154, each tested like Plane::hit). A ray that
+// crosses the boundary draws its free-flight uniform from the sample's stream; the scan visits media in slot
+// order, so the draw order is the sequential hit()'s. Returns the scattering distance t, or NaN.
 __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, v3 inv, Rng& rng) {
     const float* f = ob.f;
     // blo = center - extend, bhi = center + extend (rt_scene.cpp, the restatement's p.a -/+ e.a):
@@ -987,53 +951,38 @@ __device__ __forceinline__ float medium_candidate(const ObjRec& ob, v3 o, v3 d, 
     return t1c + fdiv(hd, len);
 }
 
-// hit() over the flattened object table (main.cu:43-57). Called with the whole
-// wave active; `live` masks lanes without a path. Records are fetched one
-// object ahead (scalar loads overlap the current object's VALU work), and the
-// per-object tests are branch-free candidates merged with Hit's tie rule.
-// kMed: the scan-kernel variant for scenes with participating media (rt_capi.cpp picks it):
-// no record prefetch (the medium test is long and the next record's 16 SGPRs stay live
-// across it) and one merge per object (the type branches yield a candidate instead of
-// each updating the Hit state). Both were measured slower on the other scenes.
-// kParts (BVH kernels): 1 = the scene has BVH meshes, 2 = sphere groups; the other traversal is
-// not compiled in (rt_capi.cpp picks the variant from the committed scene).
+// hit() over the flattened object table (main.cu:43-57), called with the whole wave active (`live` masks lanes
+// without a path); records are fetched one object ahead and the per-object tests are branch-free candidates
+// merged with Hit's tie rule. kMed (scenes with media): no record prefetch (the long medium test would keep the
+// next record's SGPRs live) and one merge per object; both measured slower elsewhere. kParts (BVH
+// kernels): 1 = BVH meshes, 2 = sphere groups; the other traversal is not compiled in.
 template <int K>
 __device__ __forceinline__ float axis(v3 v) {
     return K == 0 ? v.x : K == 1 ? v.y : v.z;
 }
 
-// Plane::hit (Plane.cu:4-52) for a kObjPlaneAxial record: normal n = +-1 on the orientation's normal
-// axis K and +-0 on the in-plane axes A, B. Plane.cu's den = dot(n, d) and num = dot(p - o, n) are
-// (0 * d_A + 0 * d_B) + n_K * d_K and the like: exactly n_K * d_K and (p_K - o_K) * n_K whenever those are
-// non-zero, so t is the same float. A zero den or num (of either sign) fails |den| > tMin (or
-// den > tMin) or t >= tMin in both forms. Where the full dot products are NaN (a NaN or inf d_A, d_B,
-// o_A or o_B) these are not, but then the hit point's coordinate on that axis, o_A + d_A * t, is NaN or
-// infinite and fails the open bounds test: the candidate is NaN (none) in both forms.
+// Plane::hit (Plane.cu:4-52) for a kObjPlaneAxial record: n = +-1 on the normal axis K, +-0 on the in-plane axes
+// A, B. Plane.cu's den = dot(n, d) and num = dot(p - o, n) are exactly n_K d_K and (p_K - o_K) n_K when non-zero,
+// so t is the same float; a zero den or num fails |den| > tMin or t >= tMin in both forms, and where the full dot
+// products are NaN (NaN or inf on A or B) the hit point's A or B coordinate fails the bounds test in both forms.
 template <int K, int A, int B>
 __device__ __forceinline__ float plane_axial(const ObjRec& ob, v3 o, v3 d, v3 inv) {
     const float* f = ob.f;
     const float nk = f[3 + K];
     const float den = nk * axis<K>(d);
-    // twoSide ? |den| > tMin : den > tMin, with u1 = the bits of 1.0f (two-sided) or 0 (rt_scene.cpp):
-    // max(|den| * 1, den) = |den|; max(|den| * 0, den) > tMin iff den > tMin (+0 or NaN against den,
-    // and fmaxf returns den for a NaN first operand); a NaN den fails both. No scalar select.
-    // t = ((p_k - o_k) nk) / (nk d_k) with nk = +-1 is (p_k - o_k) / d_k exactly (IEEE division and
-    // Markstein's correction are odd in the signs of both operands), and the ray's inverse direction
-    // (rcp_exact: RN(1 / d_k) wherever |d_k| > tMin) is the reciprocal Markstein needs: no reciprocal per plane
-    // (round 6). t matters only where proceed holds (then |den| > tMin): a wave with any |num| or |den| >=
-    // 2^100 takes the IEEE division (closest_hit's general plane argues the domain)
+    // t = ((p_K - o_K) n_K) / (n_K d_K) is (p_K - o_K) / d_K exactly (IEEE division and Markstein's correction
+    // are odd in the signs of both operands), and rcp_exact already holds RN(1 / d_K): no reciprocal per plane
+    // (round 6). t matters only where |den| > tMin; a wave with |num| or |den| >= 2^100 takes the IEEE division.
     const float num = f[K] - axis<K>(o);
     float t = div_y(num, axis<K>(d), axis<K>(inv));
     if (__builtin_expect(__ballot(!(fmaxf(fabsf(num), fabsf(den)) < 0x1p100f)) != 0, 0)) t = fdiv(num, axis<K>(d));
     const float pa = axis<A>(o) + axis<A>(d) * t;
     const float pb = axis<B>(o) + axis<B>(d) * t;
-    // The six conditions as one compare: each is a difference that is > 0 exactly when it holds
-    // (x - y > 0 iff x > y for floats with gradual underflow; t >= tMin iff t > the float below tMin),
-    // and the candidate stands iff their minimum is > 0. That needs no lane-mask ANDs (scalar
-    // instructions, the co-bound of this kernel: DESIGN §5). NaNs: den is finite (directions are), so
-    // the proceed term is a number; where it is <= 0 the minimum is too, whatever fminf drops, and
-    // where it is > 0, |den| > tMin and the quotient, pa and pb are finite: the same result as the
-    // compares for every ray.
+    // The six conditions as one compare: proceed (twoSide ? |den| > tMin : den > tMin, with u1 = the bits of 1.0f
+    // or 0: max(|den| u1, den)), t >= tMin (t > the float below it) and the four open bounds are differences that
+    // are > 0 exactly when they hold, so the candidate stands iff their minimum is > 0 - no lane-mask ANDs (scalar
+    // instructions). den is finite, so the proceed term is a number: where it is <= 0 so is the
+    // minimum; where it is > 0 the quotient and pa, pb are finite.
     const float p1 = fmaxf(fabsf(den) * __uint_as_float(ob.u1), den) - kTMin;
     const float m = fminf(fminf(fminf(pa - f[6], f[7] - pa), fminf(pb - f[8], f[9] - pb)),
                           fminf(p1, t - 0x1.0624dcp-10f /* the float below kTMin */));
@@ -1175,14 +1124,23 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
 
 // renderKernel sample loop body (main.cu:179-185) + Camera::getRay
 // (Camera.h:151-168): starts sample s's stream and returns its camera ray.
-// The camera record is re-read from its device copy (scalar loads, K$ hits) at each
-// sample start instead of being held in 21 SGPRs for the whole persistent loop: the empty asm makes the pointer opaque, so the loads cannot be
-// hoisted. SGPRs are the scarce resource of the megakernels (their spills take VGPR
-// lanes and VALU readlane/writelane instructions).
+// The camera record is re-read from its device copy at each sample start instead of being held in 21 SGPRs for
+// the whole persistent loop (SGPRs are the megakernels' scarce resource: their spills take VGPR lanes):
+// scalar_record's empty asm makes the pointer opaque, so the loads cannot be hoisted, and puts it in the
+// constant address space (the record does not change during a launch), so they are wave-uniform scalar loads
+// (s_load, K$ hits). Through a generic pointer they were per-lane FLAT loads whose first use waited for every
+// outstanding vector-memory operation of the wave (round 6).
 template <typename T>
-__device__ __forceinline__ const T* opaque(const T* p) {
-    asm volatile("" : "+s"(p));
-    return p;
+__device__ __forceinline__ T scalar_record(const T* p) {
+    static_assert(sizeof(T) % 4 == 0, "whole words");
+    const __attribute__((address_space(4))) uint32_t* w = (const __attribute__((address_space(4))) uint32_t*)p;
+    asm volatile("" : "+s"(w));
+    uint32_t buf[sizeof(T) / 4];
+#pragma unroll
+    for (size_t i = 0; i < sizeof(T) / 4; ++i) buf[i] = w[i];
+    T r;
+    __builtin_memcpy(&r, buf, sizeof(T));
+    return r;
 }
 
 // normalize(a) (LinearAlgebra.h:69-72) by Markstein quotients (round 6, the camera's ray): RN(c / n) for every
@@ -1210,7 +1168,7 @@ __device__ __forceinline__ v3 normalize_mk(v3 a) {
 template <bool kMk = false>
 __device__ __forceinline__ Ray camera_sample(const CamRec* camp, const RenderLaunch& L, Rng& rng,
                                              uint32_t pixel, int px, int y, int s, float fw, float fh) {
-    const CamRec cam = *opaque(camp);
+    const CamRec cam = scalar_record(camp);
     rng.begin(L.seed, pixel, L.sample_offset + (uint32_t)s);
     const float rx = rng.next();
     const float ry = rng.next();
@@ -1228,12 +1186,9 @@ __device__ __forceinline__ Ray camera_sample(const CamRec* camp, const RenderLau
     return Ray{add(cam.origin, offset), dir, tm};
 }
 
-// The Ray ctor's inverse direction (Ray.h:10-16), 1.0f / d per component, correctly rounded.
-// v_rcp_f32 + one Newton step is RN(1/x) for every x with 2^-126 <= |x| < 2^126 (exhaustive
-// GPU check over all 4.2e9 such floats, tools/div_check.hip, profiles/r02/div_check.json): 3 VALU
-// per component instead of the IEEE division's 11. A wave with any component outside that range
-// (zero, subnormal, huge, inf or NaN: practically never, for normalized directions) takes the IEEE
-// division for its lanes. Called by all lanes of the wave (wave-uniform branch).
+// The Ray ctor's inverse direction (Ray.h:10-16), 1.0f / d per component, correctly rounded: rcp_nr is RN(1/x)
+// for every 2^-126 <= |x| < 2^126 (3 VALU instead of the IEEE division's 11); a wave with a component outside
+// that range (zero, subnormal, huge, inf, NaN) takes the IEEE division. Called by the whole wave.
 __device__ __forceinline__ v3 rcp_exact(v3 d) {
     v3 r{rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z)};
     const float lo = fminf(fminf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
@@ -1252,14 +1207,9 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 
 }  // namespace
 
-// Occupancy per kernel (min waves per SIMD; VGPR budget 512 / waves): the BVH rayColor
-// kernel at 4 (128 VGPRs, spill-free; its sphere-group-only and simple-scene mesh variants at 5), the linear-scan
-// rayColor kernel at 6 (89 VGPRs at 5
-// since it no longer carries the medium test; 9 spilled at 6 and still faster), its
-// sphere-free variant at 7, its media variant at 6 and the pathTrace kernel at 6 (same-box
-// A/B in DESIGN.md §4; profiles/r02/ab_occ*.txt, ab_no_medium.txt, ab_no_spheres.txt; pathTrace
-// at 6 since it derives the pixel from the work item, 6 VGPRs spilled and 7 % faster than 5:
-// profiles/r03/ptd/).
+// Occupancy per kernel (waves per SIMD; VGPR budget 512 / waves), each measured on the same box:
+// the general BVH kernel 4, the sphere-group and mesh-BVH kernels 5, the bunny's simple-scene mesh kernel 6
+// (round 6: slim LDS), the linear-scan kernels 6, CornellBox1's sphere-free one 7, pathTrace 6.
 // -DRT_WAVES_PER_EU=k forces all to k.
 #ifndef RT_BVH_WAVES
 #define RT_BVH_WAVES 4
@@ -2846,6 +2796,5 @@ hipError_t launch_render(uint32_t variant, const SceneArgs& sc, const CamRec* ca
     }
     return hipGetLastError();
 }
-
 
 }  // namespace rt
