@@ -64,7 +64,7 @@ typedef struct rt_render_params {
     int32_t width;
     int32_t height;
     int32_t spp;            /* samples per pixel (reference: 32 offline, 1 realtime) */
-    int32_t max_depth;      /* reference BOUNCES (main.cu:23); < 2^20 for a rayColor scene without BVHs */
+    int32_t max_depth;      /* reference BOUNCES (main.cu:23); rayColor: < 2^30, < 2^20 for a scene without BVHs */
     uint32_t seed;          /* reference 1984 (main.cu:127) */
     uint32_t sample_offset; /* first global sample index (progressive accumulation) */
     int32_t row_block;      /* rows per tile block (>= 1) */

@@ -681,10 +681,12 @@ rt_status rtc::validate(rt_ctx* c, const rt_render_params* p, rt::RenderLaunch& 
     if ((int64_t)p->width * p->height > (int64_t)1 << 31) return fail(c, RT_ERR_INVALID, "frame too large");
     if (p->spp < 1 || p->max_depth < 0) return fail(c, RT_ERR_INVALID, "spp must be >= 1, max_depth >= 0");
     // the linear-scan rayColor kernels (scenes without BVHs) keep a path's depth in 20 bits of an LDS
-    // word (rt_kernel.hip, the camera slot's spare word); the BVH and pathTrace kernels keep it in a
-    // register and take any max_depth
+    // word (rt_kernel.hip, the camera slot's spare word), the mesh-BVH-only kernels in 30 bits of one
+    // (W.grp_s); the other BVH kernels and pathTrace keep it in a register
     if (p->integrator == RT_INTEGRATOR_RAYCOLOR && c->scene.nodes.empty() && p->max_depth >= (1 << 20))
         return fail(c, RT_ERR_INVALID, "max_depth must be < 2^20 for a scene without BVHs");
+    if (p->integrator == RT_INTEGRATOR_RAYCOLOR && p->max_depth >= (1 << 30))
+        return fail(c, RT_ERR_INVALID, "max_depth must be < 2^30");
     if (p->row_block < 1 || p->row_world < 1 || p->row_rank < 0 || p->row_rank >= p->row_world)
         return fail(c, RT_ERR_INVALID, "bad row tiling");
     L.width = p->width;

@@ -319,7 +319,7 @@ struct WaveLdsCore {
     unsigned long long key[64];  // per-ray (t bits << 32 | triangle) minima
     int32_t src[64];             // rank -> lane of the rays wanting a mesh
     uint32_t slot[kMaxRun * 64];  // mesh_run ray slots / the BVH traversals' deferred leaf pairs
-    uint32_t grp_s[64];          // per-lane sphere-group test counts / the mesh deferral's bits (kParts = 1)
+    uint32_t grp_s[64];          // sphere-group test counts / (kParts = 1) deferral bits 0-1, path depth bits 2-31
 };
 struct WaveLds : WaveLdsCore {
     uint32_t grp_m[64];  // per-lane moving-sphere test counts (Counters::grp drained per trip)
@@ -613,14 +613,13 @@ __device__ __forceinline__ ObjRec load_obj(const ObjRec* __restrict__ objs, int 
     return r;
 }
 
-// A run of g consecutive brute-force meshes with the same triangle count m (rt_scene.cpp: g in the first
-// record's f[7]) compacted together: the rays wanting each mesh (box early-out, TriangleMesh.cu:34-38) are
-// listed as ray slots (lane, the mesh's triangle base), and the run's slot x triangle pairs are packed over the
-// 64 lanes, backface-culled, then fully tested in batches of 64. The run's triangles are consecutive in
-// `tris`, so the per-lane minimum of (t, global triangle index) is what the sequential hit() keeps. `skip`: a
-// convex mesh the lane's ray starts on and leaves (-1: none; rt_scene.cpp convex_shell) takes no ray slot; the
-// counters still count the reference's AABB passes and tests. kLin (the linear-scan kernels): the branch-free
-// cull loop and tri_rcp's 1 / det (the BVH kernels keep the exec-mask form: registers).
+// A run of g consecutive brute-force meshes with the same triangle count m (g in the first record's f[7])
+// compacted together: the rays wanting each mesh (box early-out, TriangleMesh.cu:34-38) become ray slots (lane,
+// triangle base); the run's slot x triangle pairs are packed over 64 lanes, backface-culled, then tested in
+// batches of 64. The triangles are consecutive in `tris`, so the per-lane minimum of (t, global triangle index)
+// is what the sequential hit() keeps. `skip`: a convex mesh the ray starts on and leaves (rt_scene.cpp
+// convex_shell) takes no slot; the counters still count the reference's AABB passes and tests. kLin (the scan
+// kernels): branch-free cull loop and tri_rcp's 1 / det (the BVH kernels keep the exec-mask form: registers).
 template <bool kOrdered, bool kLin>
 __device__ __forceinline__ void mesh_run(const ObjRec* __restrict__ objs, const TriRec* __restrict__ tris,
                                          int i0, uint32_t g, uint32_t m, uint32_t magic, bool live, v3 o, v3 d,
@@ -1122,14 +1121,11 @@ __device__ __forceinline__ Hit closest_hit(const SceneArgs& S, const Ray& ray, v
     return h;
 }
 
-// renderKernel sample loop body (main.cu:179-185) + Camera::getRay
-// (Camera.h:151-168): starts sample s's stream and returns its camera ray.
-// The camera record is re-read from its device copy at each sample start instead of being held in 21 SGPRs for
-// the whole persistent loop (SGPRs are the megakernels' scarce resource: their spills take VGPR lanes):
-// scalar_record's empty asm makes the pointer opaque, so the loads cannot be hoisted, and puts it in the
-// constant address space (the record does not change during a launch), so they are wave-uniform scalar loads
-// (s_load, K$ hits). Through a generic pointer they were per-lane FLAT loads whose first use waited for every
-// outstanding vector-memory operation of the wave (round 6).
+// renderKernel sample loop body (main.cu:179-185) + Camera::getRay (Camera.h:151-168): starts sample s's stream
+// and returns its camera ray. The camera record is re-read at each sample start, not held in 21 SGPRs (their
+// spills take VGPR lanes): scalar_record's empty asm makes the pointer opaque (no hoisting) and puts it in the
+// constant address space, so the loads are wave-uniform s_loads (K$ hits). Through a generic pointer they were
+// per-lane FLAT loads whose first use waited for every outstanding vector-memory operation (round 6).
 template <typename T>
 __device__ __forceinline__ T scalar_record(const T* p) {
     static_assert(sizeof(T) % 4 == 0, "whole words");
@@ -1230,7 +1226,7 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #define RT_GROUP_WAVES 5
 #endif
 #ifndef RT_BVH_SIMPLE_WAVES
-#define RT_BVH_SIMPLE_WAVES 6  // the bunny box: six 4-wave blocks fit since round 6 (slim LDS); 13 VGPRs spill outside the traversal
+#define RT_BVH_SIMPLE_WAVES 6  // the bunny box: six 4-wave blocks fit since round 6 (slim LDS); 9 VGPRs spill outside the traversal
 #endif
 #ifndef RT_PT_WAVES
 #define RT_PT_WAVES 6
@@ -1754,7 +1750,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
             }
             ray = camera_sample(cam, L, rng, pixel, px, y, s, (float)(L.width - 1), (float)(L.height - 1));
             thr = v3{1.0f, 1.0f, 1.0f};
-            depth = 0;
+            if constexpr (kDef) W.grp_s[lane] &= 3u;  // the path depth (bits 2-31)
+            else depth = 0;
             need_cam = false;
             if (L.max_depth <= 0)  // rayColor with BOUNCES = 0 returns black
                 sample_done(L, v3{0.0f, 0.0f, 0.0f}, SP, item, own_end, s, sum, thr, alive, need_cam, towner,
@@ -1764,7 +1761,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         uint32_t cw = 0u;
         if constexpr (kCamPf) cw = reinterpret_cast<const uint32_t*>(&cslots[wave].c[lane])[3];
         const bool live = alive && !need_cam;
-        if constexpr (kDef) W.grp_s[lane] = (W.grp_s[lane] >> 1) & 1u;  // bit 0: deferred on the last trip
+        if constexpr (kDef) W.grp_s[lane] = (W.grp_s[lane] & ~3u) | ((W.grp_s[lane] >> 1) & 1u);  // bit 0: deferred last trip
         RT_STAMP(t_b);
         RT_ACC(0, t_a, t_b);
 #ifdef RT_STAMPS
@@ -1789,7 +1786,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
         const bool pend = (kResume && live && (glds[kResume ? wave : 0].st[lane] >> 31) != 0u) ||
                           (kDef && live && (W.grp_s[lane] & 2u) != 0u);
         cnt.segs += (uint32_t)__popcll(__ballot(live && !pend));
-        if (kBvh && __ballot(cnt.grp != 0)) {  // drain the 16-bit sphere-group counts
+        if (kBvh && !kDef && __ballot(cnt.grp != 0)) {  // drain the 16-bit sphere-group counts
             W.grp_s[lane] += cnt.grp & 0xFFFFu;
             if constexpr (!kSlim) lds[wave].grp_m[lane] += cnt.grp >> 16;
             cnt.grp = 0;
@@ -1900,8 +1897,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(render_wave
                     const uint32_t dn = (*dw & kDepthMask) + 1u;  // (max_depth < 2^20: rt_capi.cpp validate)
                     *dw = dn | (self_bits << 20);
                     done = (int)dn >= L.max_depth;
-                } else
-                {
+                } else if constexpr (kDef) {
+                    // the mesh-BVH-only kernels keep the path depth in bits 2-31 of W.grp_s (a VGPR was spilled
+                    // and reloaded every scatter at their occupancy; max_depth < 2^30: rt_capi.cpp validate)
+                    const uint32_t g = W.grp_s[lane] + 4u;
+                    W.grp_s[lane] = g;
+                    done = (int)(g >> 2) >= L.max_depth;
+                } else {
                     ++depth;
                     done = depth >= L.max_depth;
                 }
@@ -2041,13 +2043,11 @@ struct PtRay {
     bool exact;    // a direction component is tiny but non-zero: always divide
 };
 
-// Exact-decision box test: the same accept/reject as RayIntersectsBox
-// (pt_box). The slab parameters come from the reciprocal (relative error
-// < 2^-21 against the correctly rounded quotient); the decision reduces to
-// `tnear > tfar || tfar < 0` (the early-outs are monotone), the signs are
-// exact, and only a tnear/tfar gap inside the rounding band falls back to the
-// divisions. `tn` is a lower bound of the entry parameter of the box widened
-// by eps (pruning only); `order` is the unwidened entry (child ordering).
+// Exact-decision box test: the same accept/reject as RayIntersectsBox (pt_box). The slab parameters come from
+// the reciprocal (relative error < 2^-21 against the correctly rounded quotient); the decision reduces to
+// `tnear > tfar || tfar < 0` (the early-outs are monotone), the signs are exact, and only a tnear/tfar gap
+// inside the rounding band falls back to the divisions. `tn` is a lower bound of the entry parameter of the box
+// widened by eps (pruning only); `order` is the unwidened entry (child ordering).
 __device__ __forceinline__ bool pt_box_decide(const CFNode& n, const PtRay& r, float& tn_prune,
                                               float& order) {
     float tn = -3.40282347e+38f, tf = 3.40282347e+38f, tw = -3.40282347e+38f;

@@ -132,3 +132,38 @@ def test_variant_parity(variant, scene, schedule, depth):
         ref, ref_st = SCENES[scene][1]().render(W, H, SPP, depth, lanes_per_pixel=LANES)
     assert st["segments"] == ref_st["segments"], (variant, st["segments"], ref_st["segments"])
     assert np.array_equal(img, ref), (variant, float(np.max(np.abs(img - ref))))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,variant", [("bunny_small", "BVH_MESH_SIMPLE_QUEUE"), ("suzanne", "BVH_MESH_QUEUE")])
+def test_mesh_bvh_kernels_path_depth(scene, variant):
+    """The mesh-BVH-only kernels keep a path's depth in bits 2-31 of the lane's LDS word W.grp_s, beside the
+    deferral bits (rt_kernel.hip): paths of 0, 1 and 2 bounces match the restatement bit for bit, segment
+    counts included, and max_depth >= 2^30 is refused (rt_capi.cpp validate)."""
+    import raytracingthenextweekcuda_amd as rtmi
+    from raytracingthenextweekcuda_amd import _lib
+
+    oracle_scene = SCENES[scene][1]()
+    with rtmi.Renderer(0) as r:
+        SCENES[scene][0](r, rtmi)
+        for depth in (0, 1, 2):
+            img = r.render(W, H, SPP, depth, lanes_per_pixel=LANES)
+            st = r.stats()
+            assert _lib.VARIANTS[st["variant"]] == variant
+            ref, ref_st = oracle_scene.render(W, H, SPP, depth, lanes_per_pixel=LANES)
+            assert st["segments"] == ref_st["segments"], (depth, st["segments"], ref_st["segments"])
+            assert np.array_equal(img, ref), (depth, float(np.max(np.abs(img - ref))))
+        with pytest.raises(_lib.RTError, match=r"2\^30"):
+            r.render(W, H, 1, 1 << 30)
+
+
+@pytest.mark.gpu
+def test_scan_kernel_depth_limit():
+    """The linear-scan kernels keep the depth in 20 bits of the camera slot's spare word."""
+    import raytracingthenextweekcuda_amd as rtmi
+    from raytracingthenextweekcuda_amd import _lib
+
+    with rtmi.Renderer(0) as r:
+        SCENES["cornellbox1"][0](r, rtmi)
+        with pytest.raises(_lib.RTError, match=r"2\^20"):
+            r.render(W, H, 1, 1 << 20)
