@@ -124,6 +124,18 @@ RT_HD float u01(uint32_t x) {
 
 RT_HD uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
 
+// a ^ b ^ c as one gfx950 v_bitop3_b32 (truth table 0x96): the compiler shares the two-input xor that
+// xoshiro's update has in common and then issues two of them
+RT_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return a ^ b ^ c;
+#endif
+}
+
 // Per-lane stream state (4 registers).
 struct Rng {
     uint32_t s0, s1, s2, s3;
@@ -142,13 +154,13 @@ struct Rng {
 #else
         const uint32_t r = s0 + s3;
 #endif
-        const uint32_t t = s1 << 9;
-        s2 ^= s0;
-        s3 ^= s1;
-        s1 ^= s2;
-        s0 ^= s3;
-        s2 ^= t;
-        s3 = rotl32(s3, 11);
+        // s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= t (t = s1 << 9); s3 = rotl(s3, 11)
+        const uint32_t t = s1 << 9, s3a = s3 ^ s1;
+        const uint32_t n1 = xor3(s1, s2, s0), n2 = xor3(s2, s0, t);
+        s0 ^= s3a;
+        s1 = n1;
+        s2 = n2;
+        s3 = rotl32(s3a, 11);
         return r;
     }
     RT_HD float next() { return u01(next_u32()); }
