@@ -91,6 +91,28 @@ RT_HD void mulhilo(uint32_t a, uint32_t b, uint32_t& hi, uint32_t& lo) {
     lo = (uint32_t)p;
 }
 
+// a ^ b ^ c as one gfx950 v_bitop3_b32 (truth table 0x96); the compiler leaves such chains as two-input xors
+// (in xoshiro's update because a two-input term is shared, in Philox's round because a key is a scalar)
+RT_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return a ^ b ^ c;
+#endif
+}
+// the same with a wave-uniform third operand, read from its SGPR (Philox's k0 = the launch seed)
+RT_HD uint32_t xor3_uniform(uint32_t a, uint32_t b, uint32_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(__builtin_amdgcn_readfirstlane(k)));
+    return r;
+#else
+    return a ^ b ^ k;
+#endif
+}
+
 RT_HD u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
 #if defined(__HIPCC__)
 #pragma unroll
@@ -102,7 +124,11 @@ RT_HD u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
         uint32_t hi0, lo0, hi1, lo1;
         mulhilo(kPhiloxM0, c.x, hi0, lo0);
         mulhilo(kPhiloxM1, c.z, hi1, lo1);
+#if defined(__HIP_DEVICE_COMPILE__)
+        c = u4{xor3_uniform(hi1, c.y, k0), lo1, xor3(hi0, c.w, k1), lo0};
+#else
         c = u4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+#endif
         k0 += kPhiloxW0;
         k1 += kPhiloxW1;
     }
@@ -123,18 +149,6 @@ RT_HD float u01(uint32_t x) {
 }
 
 RT_HD uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
-
-// a ^ b ^ c as one gfx950 v_bitop3_b32 (truth table 0x96): the compiler shares the two-input xor that
-// xoshiro's update has in common and then issues two of them
-RT_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-#else
-    return a ^ b ^ c;
-#endif
-}
 
 // Per-lane stream state (4 registers).
 struct Rng {
